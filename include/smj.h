@@ -1,0 +1,203 @@
+/*
+ * smj.h -- C-ABI of libsmj_hip.so, the MI355X sort-merge-join library.
+ *
+ * This is the drop-in boundary for the reference's DPU path.  The reference
+ * host (sort-merge-join/app.c) drives four UPMEM kernels through the UPMEM
+ * host API (include/dpu/dpu.h): dpu_alloc / dpu_load / dpu_prepare_xfer /
+ * dpu_push_xfer / dpu_launch / dpu_free.  Each entry point below replaces one
+ * reference kernel together with the transfers around it; the comment on
+ * each cites the reference interface it replaces.
+ *
+ * Conventions (mirroring dpu_error_t, include/dpu/dpu_error.h:19):
+ *   - every int-returning call returns SMJ_OK (0) or a negative SMJ_ERR_*;
+ *   - SMJ_ASSERT() mirrors DPU_ASSERT (include/dpu/dpu.h:130-144): print and
+ *     exit(EXIT_FAILURE) on error;
+ *   - host-pointer calls are blocking (like dpu_launch(set, DPU_SYNCHRONOUS),
+ *     app.c:247) and not re-entrant; one host thread drives the library;
+ *   - tables are row-major T[row_num * col_num] (common.h), T = int64_t;
+ *   - all row counts must be < 2^30 per call and col_num in [1, 8].
+ *
+ * Two layers:
+ *   smj_*      host pointers, exactly the reference's data flow (app.c);
+ *   smj_dev_*  device pointers + a HIP stream, for device-resident pipelines
+ *              (bench.py, the multi-GPU driver).  No torch types anywhere.
+ */
+#ifndef SMJ_H
+#define SMJ_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "common.h"
+
+#ifndef INT64
+#error "libsmj_hip is built for T = int64_t (common.h INT64, the reference default)"
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (dpu_error_t analogue) ------------------------------- */
+#define SMJ_OK 0
+#define SMJ_ERR_INVALID (-1)      /* bad argument / descriptor             */
+#define SMJ_ERR_HIP (-2)          /* a HIP runtime call failed             */
+#define SMJ_ERR_NOMEM (-3)        /* device or host allocation failed      */
+#define SMJ_ERR_NODEVICE (-4)     /* no gfx950 device / smj_init missing   */
+#define SMJ_ERR_TOO_LARGE (-5)    /* row count >= 2^30 or too many columns */
+#define SMJ_ERR_TIMEOUT (-6)      /* an in-kernel look-back wait timed out */
+#define SMJ_ERR_UNSUPPORTED (-7)
+
+#define SMJ_MAX_COLS 8
+#define SMJ_MAX_ROWS ((int64_t)1 << 30)
+
+const char *smj_strerror(int code);
+
+/* DPU_ASSERT analogue (include/dpu/dpu.h:130-144). */
+#define SMJ_ASSERT(stmt)                                                              \
+    do {                                                                              \
+        int smj_assert_rc_ = (stmt);                                                  \
+        if (smj_assert_rc_ != SMJ_OK) {                                               \
+            fprintf(stderr, "%s:%d(%s): SMJ error in %s: %s\n", __FILE__, __LINE__,   \
+                    __func__, #stmt, smj_strerror(smj_assert_rc_));                   \
+            exit(EXIT_FAILURE);                                                       \
+        }                                                                             \
+    } while (0)
+
+/* Phase timing in the reference's three buckets (app.c:136-138, :763-772):
+ * host->device copies, device kernels, device->host copies (milliseconds). */
+typedef struct {
+    double cpu_gpu_ms;
+    double gpu_ms;
+    double gpu_cpu_ms;
+} smj_timing_t;
+
+/* ---- lifetime ----------------------------------------------------------- */
+/* Replaces dpu_alloc(NR_DPUS, profile, &set) (include/dpu/dpu.h:164; called
+ * at app.c:175,315,422,638).  n_gpus <= 0 means "all visible".  Selects
+ * device 0 for the host-pointer API.  Returns the number of GPUs in use
+ * (>= 1) or a negative error. */
+int smj_init(int n_gpus);
+/* Replaces dpu_free(set) (include/dpu/dpu.h:189; app.c:307,402,503,761). */
+void smj_finalize(void);
+/* Version string of the library build. */
+const char *smj_version(void);
+
+/* ---- host-pointer API: one call per reference kernel ------------------- */
+
+/* select.c (main :63-194; host side app.c:172-307):
+ *   out <- rows of `in` with row[select_col] > select_val (signed 64-bit),
+ *   input order kept.  bl->col_num / bl->row_num describe `in`; `out` must
+ *   hold bl->row_num rows; *out_rows gets the kept count. */
+int smj_select(const dpu_block_t *bl, const T *in, T *out, int select_col, T select_val,
+               int *out_rows);
+
+/* sort_dpu.c (main :189-328; host side app.c:309-406) + the merge tree:
+ *   stable ascending sort of bl->row_num rows on row[key_col] (signed),
+ *   in place from the caller's view.  Stability matches cpu_app.c
+ *   insertion_sort_in_cpu (:172-202), the parity target. */
+int smj_sort(const dpu_block_t *bl, T *rows, int key_col);
+
+/* merge_dpu.c (main :55-223; host tournament app.c:412-547):
+ *   out <- stable merge of two sorted runs a (bl1) and b (bl2) on key_col;
+ *   equal keys take run a first.  bl1->col_num must equal bl2->col_num;
+ *   out holds bl1->row_num + bl2->row_num rows. */
+int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const T *b,
+              int key_col, T *out);
+
+/* join.c (main :58-266; host splitters app.c:585-692):
+ *   1:1 zip merge join of two tables sorted on key1 / key2 (cpu_app.c
+ *   join_in_cpu :204-266).  Output row = all R columns then the S columns
+ *   except key2 (c1 + c2 - 1 columns), rows in key order.  *out is
+ *   malloc'd by the library and free()'d by the caller (app.c:679,759);
+ *   *out_rows gets the joined row count. */
+int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, const T *S, int key1,
+             int key2, T **out, int64_t *out_rows);
+
+/* The whole app.c pipeline (select -> sort -> merge -> join, :172-692) in one
+ * call with one H2D copy per table and one D2H copy of the result.
+ * *out is malloc'd (caller frees).  timing may be NULL. */
+int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, const T *S,
+                        int select_col1, T select_val1, int select_col2, T select_val2,
+                        int key1, int key2, T **out, int64_t *out_rows, smj_timing_t *timing);
+
+/* ---- device-pointer API ------------------------------------------------ */
+/* All smj_dev_* calls enqueue on `stream` (a hipStream_t, NULL = the legacy
+ * default stream) on the CURRENT HIP device and use library-owned scratch
+ * memory for that device (grow-only; calls on one device must be serialised
+ * on one stream).  Buffers must be distinct unless stated. */
+
+/* Stable select + sort (fused): out <- sort_stable(select(in)).  When
+ * use_select == 0 every row is kept.  key_base: keys are radix-sorted on
+ * (key ^ 2^63) - key_base; pass 0 unless every key is known to be >= the
+ * signed value whose biased form is key_base (the multi-GPU driver passes
+ * its partition's lower bound).  Blocks until the row count is known
+ * (one small device->host read); *out_rows gets it. */
+int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                        T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                        void *stream);
+
+/* Stable select alone (a stable compaction). *out_rows is written after a
+ * stream synchronisation. */
+int smj_dev_select(const T *in, int64_t n_rows, int col_num, int select_col, T select_val, T *out,
+                   int64_t *out_rows, void *stream);
+
+/* Stable merge of sorted runs a (na rows) and b (nb rows) -> out. Async. */
+int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int col_num, int key_col,
+                  T *out, void *stream);
+
+/* 1:1 zip join of sorted R (nr x c1) and S (ns x c2) into out, which must
+ * hold min(nr, ns) rows of (c1 + c2 - 1) columns.  The joined row count is
+ * written to *d_out_rows (DEVICE int64) asynchronously; if h_out_rows is not
+ * NULL the call synchronises and also stores it there. */
+int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t ns, int c2, int key1,
+                 int key2, T *out, int64_t *d_out_rows, int64_t *h_out_rows, void *stream);
+
+/* Multi-GPU range partition, step 1: counts of selected rows
+ * per destination bucket, bucket(k) = #{splitters < k} over n_split sorted
+ * splitters (n_split + 1 <= 16 buckets), plus the min / max selected key.
+ * Synchronises; h_counts gets n_split + 1 entries, h_minmax 2 (INT64_MAX /
+ * INT64_MIN when nothing is selected). */
+int smj_dev_partition_count(const T *in, int64_t n_rows, int col_num, int use_select,
+                            int select_col, T select_val, int key_col, const T *d_splitters,
+                            int n_split, int64_t *h_counts, T *h_minmax, void *stream);
+
+/* Step 2: stable scatter of the selected rows into bucket-contiguous `out`
+ * (bucket b starts at the exclusive prefix of h_counts).  Async. */
+int smj_dev_partition_scatter(const T *in, int64_t n_rows, int col_num, int use_select,
+                              int select_col, T select_val, int key_col, const T *d_splitters,
+                              int n_split, const int64_t *h_counts, T *out, void *stream);
+
+/* Synthetic 2-column table (key, payload) for rows [row0, row0 + rows):
+ * key = 1 + floor(splitmix64(g + seed * 0xD1B54A32D192ED03) * key_range / 2^64),
+ * payload = g (the global row index).  Identical to the oracle's
+ * smj_ref_gen_uniform.  Async. */
+int smj_dev_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
+                        void *stream);
+
+/* Zipf(theta) keys over [1, domain]: rank r is drawn with
+ * Gray et al.'s closed-form approximation (SIGMOD'94 "Quickly generating
+ * billion-record synthetic databases", as used by YCSB) from uniform
+ * u = splitmix64(g + seed * 0xD1B54A32D192ED03) / 2^64, and the key is the
+ * rank scattered over [1, domain] by a bijective affine hash so hot keys are
+ * spread over the key space.  zeta_n = smj_zipf_zeta(domain, theta).
+ * payload = g.  Async. */
+int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
+                     double theta, double zeta_n, void *stream);
+/* sum_{i=1..n} i^-theta (host). */
+double smj_zipf_zeta(int64_t n, double theta);
+
+/* ---- profiling ---------------------------------------------------------- */
+/* When enabled, every kernel launch is bracketed by hipEvents recorded on
+ * the stream it is launched on, tagged with the kernel's name and its
+ * algorithmic byte count.  smj_prof_report() synchronises, writes
+ * a JSON object {name: {"launches", "ms", "bytes"}} into buf and resets. */
+void smj_prof_enable(int on);
+int smj_prof_report(char *buf, size_t buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMJ_H */

@@ -1,0 +1,157 @@
+"""Python handle on the CPU oracle (oracle/cpu_ref.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / the CPU baseline.  Every function
+restates sort-merge-join/cpu_app.c (see cpu_ref.c for the line map); parity
+of the restatement itself is pinned by tests/golden/ (outputs of the real
+cpu_app.c, see tests/golden/make_goldens.py).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libsmj_oracle.so")
+CLI = os.path.join(HERE, "build", "cpu_ref")
+REF_LIB = os.path.join(HERE, "_ref", "libcpu_app_ref.so")   # the real cpu_app.c (when built)
+REF_DRIVER = os.path.join(HERE, "_ref", "ref_driver")
+
+_lib = None
+_P = ctypes.c_void_p
+_L = ctypes.c_int64
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        l = ctypes.CDLL(LIB)
+        l.smj_ref_select_into.restype = _L
+        l.smj_ref_select_into.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P]
+        l.smj_ref_insertion_sort.restype = None
+        l.smj_ref_insertion_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
+        l.smj_ref_stable_sort.restype = ctypes.c_int
+        l.smj_ref_stable_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
+        l.smj_ref_join_count.restype = _L
+        l.smj_ref_join_count.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int]
+        l.smj_ref_join.restype = _L
+        l.smj_ref_join.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int,
+                                   ctypes.POINTER(_P)]
+        l.smj_ref_gen_uniform.restype = None
+        l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
+        l.smj_ref_csv_size.restype = ctypes.c_int
+        l.smj_ref_csv_size.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        l.smj_ref_load_csv.restype = ctypes.c_int
+        l.smj_ref_load_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]
+        l.smj_ref_save_csv.restype = ctypes.c_int
+        l.smj_ref_save_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, _L, _P]
+        l.smj_ref_pipeline_csv.restype = _L
+        l.smj_ref_pipeline_csv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _L,
+                                           ctypes.c_int, _L, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double)]
+        _lib = l
+    return _lib
+
+
+_libc = ctypes.CDLL(None)
+_libc.free.argtypes = [_P]
+
+
+def _c(a):
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    return a, a.ctypes.data_as(_P)
+
+
+def select(table, select_col, select_val):
+    """cpu_app.c select_in_cpu (:81-112)."""
+    t, p = _c(table)
+    out = np.empty_like(t)
+    m = lib().smj_ref_select_into(t.shape[1], t.shape[0], p, select_col, int(select_val), out.ctypes.data_as(_P))
+    return out[:m].copy()
+
+
+def sort(table, key_col=0, insertion=False):
+    """cpu_app.c insertion_sort_in_cpu (:172-202); stable.  insertion=False
+    runs the O(n log n) merge sort with the identical output order."""
+    t, p = _c(table)
+    t = t.copy()
+    p = t.ctypes.data_as(_P)
+    if insertion:
+        lib().smj_ref_insertion_sort(t.shape[1], t.shape[0], key_col, p)
+    else:
+        if lib().smj_ref_stable_sort(t.shape[1], t.shape[0], key_col, p) != 0:
+            raise MemoryError("oracle sort")
+    return t
+
+
+def select_sort(table, key_col=0, select_col=0, select_val=None):
+    t = table if select_val is None else select(table, select_col, select_val)
+    return sort(t, key_col)
+
+
+def join(R, S, key1=0, key2=0):
+    """cpu_app.c join_in_cpu (:204-266)."""
+    r, pr = _c(R)
+    s, ps = _c(S)
+    out = _P()
+    j = lib().smj_ref_join(r.shape[1], r.shape[0], pr, s.shape[1], s.shape[0], ps, key1, key2, ctypes.byref(out))
+    if j < 0:
+        raise MemoryError("oracle join")
+    tc = r.shape[1] + s.shape[1] - 1
+    res = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_int64)), shape=(max(j, 1) * tc,))
+    res = res[: j * tc].reshape(j, tc).copy()
+    _libc.free(out)
+    return res
+
+
+def merge(a, b, key_col=0):
+    """Stable merge of sorted runs (ties: a first) == sort(concat(a, b))."""
+    return sort(np.concatenate([np.asarray(a, dtype=np.int64), np.asarray(b, dtype=np.int64)]), key_col)
+
+
+def gen_uniform(rows, row0=0, seed=1, key_range=None):
+    if key_range is None:
+        key_range = 3 * rows
+    out = np.empty((rows, 2), dtype=np.int64)
+    lib().smj_ref_gen_uniform(out.ctypes.data_as(_P), row0, rows, seed, key_range)
+    return out
+
+
+def load_csv(path):
+    """cpu_app.c set_csv_size + load_csv (:15-79)."""
+    c, r = ctypes.c_int(0), ctypes.c_int(0)
+    if lib().smj_ref_csv_size(path.encode(), ctypes.byref(c), ctypes.byref(r)) != 0:
+        raise FileNotFoundError(path)
+    out = _P()
+    lib().smj_ref_load_csv(path.encode(), c.value, r.value, ctypes.byref(out))
+    n = c.value * r.value
+    arr = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_int64)), shape=(max(n, 1),))
+    res = arr[:n].reshape(r.value, c.value).copy()
+    _libc.free(out)
+    return res
+
+
+def save_csv(path, table):
+    t, p = _c(table)
+    if t.ndim != 2:
+        raise ValueError("2-D table expected")
+    if lib().smj_ref_save_csv(path.encode(), t.shape[1], t.shape[0], p) != 0:
+        raise OSError(path)
+
+
+def pipeline_csv(path1, path2, out_path, sel=(0, 5000, 0, 5000), keys=(0, 0), insertion=False):
+    """cpu_app.c main (:303-361) with save_to_csv enabled; returns (rows, ms)."""
+    ms = ctypes.c_double(0)
+    j = lib().smj_ref_pipeline_csv(path1.encode(), path2.encode(), out_path.encode() if out_path else None,
+                                   sel[0], int(sel[1]), sel[2], int(sel[3]), keys[0], keys[1], int(insertion),
+                                   ctypes.byref(ms))
+    if j < 0:
+        raise OSError("oracle pipeline failed")
+    return j, ms.value

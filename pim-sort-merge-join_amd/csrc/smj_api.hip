@@ -1,0 +1,668 @@
+// smj_api.hip -- the C-ABI of libsmj_hip.so (declared in include/smj.h).
+//
+// Host orchestration of the hot-path kernels: per-device scratch, the
+// select+sort plan, pass scheduling, the merge-path join, and the
+// host-pointer entry points that replace the reference's DPU calls
+// (app.c: dpu_alloc/dpu_load/dpu_push_xfer/dpu_launch/dpu_free).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "smj.h"
+#include "smj_internal.h"
+
+using namespace smj;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+extern "C" const char *smj_strerror(int code) {
+    switch (code) {
+    case SMJ_OK: return "ok";
+    case SMJ_ERR_INVALID: return "invalid argument";
+    case SMJ_ERR_HIP: return "HIP runtime error";
+    case SMJ_ERR_NOMEM: return "out of memory";
+    case SMJ_ERR_NODEVICE: return "no usable gfx950 device";
+    case SMJ_ERR_TOO_LARGE: return "table too large (rows >= 2^30 or cols > 8)";
+    case SMJ_ERR_TIMEOUT: return "look-back wait timed out in a kernel";
+    case SMJ_ERR_UNSUPPORTED: return "unsupported";
+    default: return "unknown error";
+    }
+}
+
+extern "C" const char *smj_version(void) { return "smj-mi355x 0.1 (gfx950, radix10 onesweep, merge-path join)"; }
+
+#define HIP_TRY(x)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "smj: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_),     \
+                    __FILE__, __LINE__);                                                   \
+            return e_ == hipErrorOutOfMemory ? SMJ_ERR_NOMEM : SMJ_ERR_HIP;               \
+        }                                                                                  \
+    } while (0)
+
+#define SMJ_TRY(x)                      \
+    do {                                \
+        int rc_ = (x);                  \
+        if (rc_ != SMJ_OK) return rc_;  \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// profiling: hipEvents around every launch, on the launch's stream
+// ---------------------------------------------------------------------------
+namespace {
+struct ProfRec {
+    const char *name;
+    hipEvent_t a, b;
+    double bytes;
+};
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+std::vector<hipEvent_t> g_event_pool;
+
+hipEvent_t take_event() {
+    if (!g_event_pool.empty()) {
+        hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct ProfScope {
+    ProfRec rec{};
+    hipStream_t s;
+    bool on;
+    ProfScope(const char *name, double bytes, hipStream_t st) : s(st), on(g_prof_on) {
+        if (!on) return;
+        rec.name = name;
+        rec.bytes = bytes;
+        rec.a = take_event();
+        rec.b = take_event();
+        if (rec.a) hipEventRecord(rec.a, s);
+    }
+    ~ProfScope() {
+        if (!on || !rec.a || !rec.b) return;
+        hipEventRecord(rec.b, s);
+        g_prof.push_back(rec);
+    }
+};
+}  // namespace
+
+extern "C" void smj_prof_enable(int on) { g_prof_on = on != 0; }
+
+extern "C" int smj_prof_report(char *buf, size_t buflen) {
+    struct Agg { long launches = 0; double ms = 0, bytes = 0; };
+    std::map<std::string, Agg> agg;
+    for (auto &r : g_prof) {
+        hipEventSynchronize(r.b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, r.a, r.b);
+        Agg &a = agg[r.name];
+        a.launches++;
+        a.ms += ms;
+        a.bytes += r.bytes;
+        g_event_pool.push_back(r.a);
+        g_event_pool.push_back(r.b);
+    }
+    g_prof.clear();
+    std::string out = "{";
+    bool first = true;
+    for (auto &kv : agg) {
+        char tmp[256];
+        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f}",
+                 first ? "" : ", ", kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes);
+        out += tmp;
+        first = false;
+    }
+    out += "}";
+    if (!buf || buflen == 0) return (int)out.size() + 1;
+    snprintf(buf, buflen, "%s", out.c_str());
+    return out.size() + 1 <= buflen ? SMJ_OK : (int)out.size() + 1;
+}
+
+// ---------------------------------------------------------------------------
+// per-device scratch (grow-only)
+// ---------------------------------------------------------------------------
+namespace {
+struct DevScratch {
+    int dev = -1;
+    void *tmp = nullptr;  size_t tmp_bytes = 0;     // ping-pong rows
+    void *status = nullptr; size_t status_bytes = 0; // look-back words
+    void *apart = nullptr; size_t apart_bytes = 0;   // merge-path partition
+    uint32_t *hist = nullptr;                        // kNumPos * kRadix
+    SortPlan *plan = nullptr;                        // device
+    Counters *ctr = nullptr;                         // device, 8 slots
+    int64_t *dcount = nullptr;                       // device scratch int64 x 32
+    SortPlan *h_plan = nullptr;                      // pinned
+    int64_t *h_small = nullptr;                      // pinned, 64 int64
+};
+std::map<int, DevScratch> g_scratch;
+int g_ngpus = 0;
+hipStream_t g_host_stream = nullptr;  // stream of the host-pointer API (device 0)
+
+int grow(void **p, size_t *cap, size_t need) {
+    if (need <= *cap) return SMJ_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    size_t n = std::max(need, (size_t)1 << 20);
+    HIP_TRY(hipMalloc(p, n));
+    *cap = n;
+    return SMJ_OK;
+}
+
+int scratch(DevScratch **out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    DevScratch &s = g_scratch[dev];
+    if (s.dev < 0) {
+        s.dev = dev;
+        HIP_TRY(hipMalloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
+        HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
+        HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
+        HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 32));
+        HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 64, hipHostMallocDefault));
+    }
+    *out = &s;
+    return SMJ_OK;
+}
+
+int check_table(int64_t n, int cols, int col_a, int col_b) {
+    if (n < 0 || cols < 1 || col_a < 0 || col_a >= cols || col_b < 0 || col_b >= cols)
+        return SMJ_ERR_INVALID;
+    if (cols > SMJ_MAX_COLS || n >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    return SMJ_OK;
+}
+
+// Look-back timeouts are reported by the kernels through Counters::err.
+int check_err(DevScratch *sc, int slot, hipStream_t s) {
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, &sc->ctr[slot].err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return err ? SMJ_ERR_TIMEOUT : SMJ_OK;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// select + sort
+// ---------------------------------------------------------------------------
+static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                           int key_col, uint64_t key_base, T *out, int64_t *out_rows, hipStream_t s) {
+    SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    if (!out_rows) return SMJ_ERR_INVALID;
+    *out_rows = 0;
+    if (n == 0) return SMJ_OK;
+    if (!in || !out || in == out) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    const double rowb = 8.0 * cols;
+
+    HIP_TRY(hipMemsetAsync(sc->hist, 0, sizeof(uint32_t) * kNumPos * kRadix, s));
+    HIP_TRY(hipMemsetAsync(&sc->ctr[0], 0, sizeof(Counters), s));
+    {
+        ProfScope ps("hist_radix", rowb * n, s);
+        HIP_TRY(launch_hist_radix(in, n, cols, use_select, sel_col, sel_val, key_col, key_base, sc->hist, s));
+    }
+    {
+        ProfScope ps("plan", 0, s);
+        HIP_TRY(launch_plan(sc->hist, sc->plan, s));
+    }
+    HIP_TRY(hipMemcpyAsync(sc->h_plan, sc->plan, sizeof(SortPlan), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const SortPlan plan = *sc->h_plan;
+    const int64_t m = plan.m;
+    if (m == 0) return SMJ_OK;
+    const int P = plan.npasses;
+    if (P > 1) SMJ_TRY(grow(&sc->tmp, &sc->tmp_bytes, (size_t)m * cols * 8));
+    const int64_t tile_rows = sort_tile_rows(cols);
+    const size_t max_tiles = (size_t)((n + tile_rows - 1) / tile_rows);
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, max_tiles * kRadix * sizeof(uint32_t)));
+    const T *src = in;
+    for (int k = 0; k < P; k++) {
+        const int64_t nsrc = k == 0 ? n : m;
+        T *dst = ((P - 1 - k) % 2 == 0) ? out : (T *)sc->tmp;
+        const size_t tiles = (size_t)((nsrc + tile_rows - 1) / tile_rows);
+        HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * kRadix * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(&sc->ctr[0], 0, 8, s));
+        ProfScope ps("radix_pass", rowb * (nsrc + m), s);
+        HIP_TRY(launch_radix_pass(src, nsrc, dst, cols, k == 0 ? use_select : 0, sel_col, sel_val, key_col,
+                                  key_base, plan.pos[k] * kRadixBits, sc->hist + plan.pos[k] * kRadix,
+                                  (uint32_t *)sc->status, &sc->ctr[0], s));
+        src = dst;
+    }
+    *out_rows = m;
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                                   T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                                   void *stream) {
+    return dev_select_sort(in, n_rows, col_num, use_select, select_col, select_val, key_col, key_base, out,
+                           out_rows, (hipStream_t)stream);
+}
+
+extern "C" int smj_dev_select(const T *in, int64_t n, int cols, int sel_col, T sel_val, T *out,
+                              int64_t *out_rows, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(n, cols, sel_col, 0));
+    if (!out_rows) return SMJ_ERR_INVALID;
+    *out_rows = 0;
+    if (n == 0) return SMJ_OK;
+    if (!in || !out || in == out) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    const int64_t tile_rows = sort_tile_rows(cols);
+    const size_t tiles = (size_t)((n + tile_rows - 1) / tile_rows);
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, tiles * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(&sc->ctr[1], 0, sizeof(Counters), s));
+    {
+        ProfScope ps("select_compact", 8.0 * cols * n, s);
+        HIP_TRY(launch_compact_pass(in, n, out, cols, sel_col, sel_val, (uint32_t *)sc->status, &sc->ctr[1], s));
+    }
+    Counters c;
+    HIP_TRY(hipMemcpyAsync(&c, &sc->ctr[1], sizeof(Counters), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (c.err) return SMJ_ERR_TIMEOUT;
+    *out_rows = c.count;
+    return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// merge and join
+// ---------------------------------------------------------------------------
+extern "C" int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int cols, int key_col, T *out,
+                             void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(na, cols, key_col, key_col));
+    SMJ_TRY(check_table(nb, cols, key_col, key_col));
+    if (na + nb >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    if (na + nb == 0) return SMJ_OK;
+    if (!out || (na && !a) || (nb && !b)) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    const int64_t ntiles = (na + nb + kJoinTile - 1) / kJoinTile;
+    SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(ntiles + 1) * sizeof(int64_t)));
+    {
+        ProfScope ps("merge_partition", 0, s);
+        HIP_TRY(launch_merge_partition(a, na, cols, key_col, b, nb, cols, key_col, (int64_t *)sc->apart, ntiles, s));
+    }
+    ProfScope ps("merge_tiles", 2.0 * 8 * cols * (na + nb), s);
+    HIP_TRY(launch_merge_tiles(a, na, b, nb, cols, key_col, (const int64_t *)sc->apart, ntiles, out, s));
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t ns, int c2, int key1, int key2,
+                            T *out, int64_t *d_out_rows, int64_t *h_out_rows, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(nr, c1, key1, key1));
+    SMJ_TRY(check_table(ns, c2, key2, key2));
+    if (nr + ns >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    if (!d_out_rows) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    if (nr == 0 || ns == 0) {
+        HIP_TRY(hipMemsetAsync(d_out_rows, 0, sizeof(int64_t), s));
+    } else {
+        if (!R || !S || !out) return SMJ_ERR_INVALID;
+        const int64_t ntiles = (nr + ns + kJoinTile - 1) / kJoinTile;
+        SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(ntiles + 1) * sizeof(int64_t)));
+        SMJ_TRY(grow(&sc->status, &sc->status_bytes, (size_t)ntiles * sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(sc->status, 0, (size_t)ntiles * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(&sc->ctr[2], 0, sizeof(Counters), s));
+        {
+            ProfScope ps("join_partition", 0, s);
+            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, (int64_t *)sc->apart, ntiles, s));
+        }
+        // algorithmic bytes: read R and S once; the output bytes are added by
+        // the caller-visible row count in smj_prof_report consumers (bench.py)
+        ProfScope ps("join_tiles", 8.0 * (c1 * nr + c2 * ns), s);
+        HIP_TRY(launch_join_tiles(R, nr, c1, key1, S, ns, c2, key2, (const int64_t *)sc->apart, ntiles, out,
+                                  d_out_rows, (uint32_t *)sc->status, &sc->ctr[2], s));
+    }
+    if (h_out_rows) {
+        HIP_TRY(hipMemcpyAsync(sc->h_small, d_out_rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        *h_out_rows = sc->h_small[0];
+        if (nr && ns) SMJ_TRY(check_err(sc, 2, s));
+    }
+    return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU range partition
+// ---------------------------------------------------------------------------
+extern "C" int smj_dev_partition_count(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                                       int key_col, const T *d_splitters, int n_split, int64_t *h_counts,
+                                       T *h_minmax, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    if (n_split < 0 || n_split > kMaxSplitters || !h_counts || !h_minmax) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    int64_t spl[kMaxSplitters];
+    if (n_split) {
+        if (!d_splitters) return SMJ_ERR_INVALID;
+        HIP_TRY(hipMemcpyAsync(spl, d_splitters, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    unsigned long long *gcount = (unsigned long long *)sc->dcount;
+    long long *gminmax = (long long *)(sc->dcount + 16);
+    HIP_TRY(hipMemsetAsync(gcount, 0, sizeof(int64_t) * 16, s));
+    const long long init[2] = {INT64_MAX, INT64_MIN};
+    HIP_TRY(hipMemcpyAsync(gminmax, init, sizeof init, hipMemcpyHostToDevice, s));
+    if (n > 0) {
+        ProfScope ps("partition_count", 8.0 * cols * n, s);
+        HIP_TRY(launch_hist_bucket(in, n, cols, use_select, sel_col, sel_val, key_col, spl, n_split, gcount,
+                                   gminmax, s));
+    }
+    HIP_TRY(hipMemcpyAsync(sc->h_small, sc->dcount, sizeof(int64_t) * 18, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int b = 0; b <= n_split; b++) h_counts[b] = sc->h_small[b];
+    h_minmax[0] = sc->h_small[16];
+    h_minmax[1] = sc->h_small[17];
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_partition_scatter(const T *in, int64_t n, int cols, int use_select, int sel_col,
+                                         T sel_val, int key_col, const T *d_splitters, int n_split,
+                                         const int64_t *h_counts, T *out, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    if (n_split < 0 || n_split > kMaxSplitters || !h_counts || !out || in == out) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    if (n == 0) return SMJ_OK;
+    int64_t spl[kMaxSplitters];
+    if (n_split) {
+        HIP_TRY(hipMemcpyAsync(spl, d_splitters, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    // global bucket starts -> device (one tiny copy)
+    uint32_t *h_base = (uint32_t *)sc->h_small;
+    int64_t run = 0, total = 0;
+    for (int b = 0; b < (1 << kBucketBits); b++) {
+        h_base[b] = (uint32_t)run;
+        if (b <= n_split) run += h_counts[b];
+    }
+    total = run;
+    if (total >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    uint32_t *d_base = (uint32_t *)(sc->dcount);
+    HIP_TRY(hipMemcpyAsync(d_base, h_base, sizeof(uint32_t) * (1 << kBucketBits), hipMemcpyHostToDevice, s));
+    const int64_t tile_rows = sort_tile_rows(cols);
+    const size_t tiles = (size_t)((n + tile_rows - 1) / tile_rows);
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, tiles * (1 << kBucketBits) * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * (1 << kBucketBits) * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(&sc->ctr[3], 0, sizeof(Counters), s));
+    ProfScope ps("partition_scatter", 8.0 * cols * (n + total), s);
+    HIP_TRY(launch_bucket_pass(in, n, out, cols, use_select, sel_col, sel_val, key_col, spl, n_split, d_base,
+                               (uint32_t *)sc->status, &sc->ctr[3], s));
+    // the pinned staging buffer is reused by the next call: wait for the copy
+    HIP_TRY(hipStreamSynchronize(s));
+    return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic data
+// ---------------------------------------------------------------------------
+extern "C" int smj_dev_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
+                                   void *stream) {
+    if (rows < 0 || (rows && !out) || key_range == 0) return SMJ_ERR_INVALID;
+    if (rows == 0) return SMJ_OK;
+    HIP_TRY(launch_gen_uniform(out, row0, rows, seed, key_range, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
+extern "C" double smj_zipf_zeta(int64_t n, double theta) {
+    // exact sum for the head, Euler-Maclaurin for the tail (n up to 1e10)
+    const int64_t H = std::min<int64_t>(n, 1000000);
+    double z = 0;
+    for (int64_t i = H; i >= 1; i--) z += pow((double)i, -theta);
+    if (n > H) {
+        const double a = (double)H, b = (double)n, s = 1.0 - theta;
+        z += (pow(b, s) - pow(a, s)) / s + 0.5 * (pow(b, -theta) - pow(a, -theta)) -
+             theta / 12.0 * (pow(b, -theta - 1) - pow(a, -theta - 1));
+    }
+    return z;
+}
+
+extern "C" int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain, double theta,
+                                double zeta_n, void *stream) {
+    if (rows < 0 || (rows && !out) || domain < 2 || !(theta > 0 && theta < 1)) return SMJ_ERR_INVALID;
+    if (rows == 0) return SMJ_OK;
+    HIP_TRY(launch_gen_zipf(out, row0, rows, seed, domain, theta, zeta_n, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// lifetime + host-pointer API (the app.c drop-in)
+// ---------------------------------------------------------------------------
+extern "C" int smj_init(int n_gpus) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SMJ_ERR_NODEVICE;
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, 0));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fprintf(stderr, "smj: device 0 is %s, this library is built for gfx950\n", prop.gcnArchName);
+        return SMJ_ERR_NODEVICE;
+    }
+    g_ngpus = (n_gpus <= 0 || n_gpus > count) ? count : n_gpus;
+    HIP_TRY(hipSetDevice(0));
+    if (!g_host_stream) HIP_TRY(hipStreamCreateWithFlags(&g_host_stream, hipStreamNonBlocking));
+    return g_ngpus;
+}
+
+extern "C" void smj_finalize(void) {
+    for (auto &kv : g_scratch) {
+        DevScratch &s = kv.second;
+        hipSetDevice(kv.first);
+        hipFree(s.tmp);
+        hipFree(s.status);
+        hipFree(s.apart);
+        hipFree(s.hist);
+        hipFree(s.plan);
+        hipFree(s.ctr);
+        hipFree(s.dcount);
+        hipHostFree(s.h_plan);
+        hipHostFree(s.h_small);
+    }
+    g_scratch.clear();
+    for (auto e : g_event_pool) hipEventDestroy(e);
+    g_event_pool.clear();
+    if (g_host_stream) {
+        hipSetDevice(0);
+        hipStreamDestroy(g_host_stream);
+        g_host_stream = nullptr;
+    }
+    g_ngpus = 0;
+}
+
+namespace {
+// RAII device buffer for the host-pointer API
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() { if (p) hipFree(p); }
+    int alloc(size_t bytes) {
+        HIP_TRY(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+        return SMJ_OK;
+    }
+};
+
+int need_init() {
+    if (g_ngpus <= 0) return SMJ_ERR_NODEVICE;
+    HIP_TRY(hipSetDevice(0));
+    return SMJ_OK;
+}
+
+int check_block(const dpu_block_t *bl, const void *ptr) {
+    if (!bl || bl->row_num < 0 || bl->col_num < 1) return SMJ_ERR_INVALID;
+    if (bl->row_num > 0 && !ptr) return SMJ_ERR_INVALID;
+    if (bl->col_num > SMJ_MAX_COLS || bl->row_num >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    return SMJ_OK;
+}
+
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+}  // namespace
+
+extern "C" int smj_select(const dpu_block_t *bl, const T *in, T *out, int select_col, T select_val,
+                          int *out_rows) {
+    SMJ_TRY(need_init());
+    SMJ_TRY(check_block(bl, in));
+    if (!out_rows || (bl->row_num > 0 && !out) || select_col < 0 || select_col >= bl->col_num)
+        return SMJ_ERR_INVALID;
+    const size_t bytes = (size_t)bl->row_num * bl->col_num * sizeof(T);
+    DevBuf din, dout;
+    SMJ_TRY(din.alloc(bytes));
+    SMJ_TRY(dout.alloc(bytes));
+    hipStream_t s = g_host_stream;
+    HIP_TRY(hipMemcpyAsync(din.p, in, bytes, hipMemcpyHostToDevice, s));
+    int64_t m = 0;
+    SMJ_TRY(smj_dev_select((T *)din.p, bl->row_num, bl->col_num, select_col, select_val, (T *)dout.p, &m, s));
+    HIP_TRY(hipMemcpyAsync(out, dout.p, (size_t)m * bl->col_num * sizeof(T), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *out_rows = (int)m;
+    return SMJ_OK;
+}
+
+extern "C" int smj_sort(const dpu_block_t *bl, T *rows, int key_col) {
+    SMJ_TRY(need_init());
+    SMJ_TRY(check_block(bl, rows));
+    if (key_col < 0 || key_col >= bl->col_num) return SMJ_ERR_INVALID;
+    if (bl->row_num < 2) return SMJ_OK;
+    const size_t bytes = (size_t)bl->row_num * bl->col_num * sizeof(T);
+    DevBuf din, dout;
+    SMJ_TRY(din.alloc(bytes));
+    SMJ_TRY(dout.alloc(bytes));
+    hipStream_t s = g_host_stream;
+    HIP_TRY(hipMemcpyAsync(din.p, rows, bytes, hipMemcpyHostToDevice, s));
+    int64_t m = 0;
+    SMJ_TRY(dev_select_sort((T *)din.p, bl->row_num, bl->col_num, 0, 0, 0, key_col, 0, (T *)dout.p, &m, s));
+    HIP_TRY(hipMemcpyAsync(rows, dout.p, bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    return check_err(sc, 0, s);
+}
+
+extern "C" int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const T *b, int key_col,
+                         T *out) {
+    SMJ_TRY(need_init());
+    SMJ_TRY(check_block(bl1, a));
+    SMJ_TRY(check_block(bl2, b));
+    if (bl1->col_num != bl2->col_num || key_col < 0 || key_col >= bl1->col_num) return SMJ_ERR_INVALID;
+    const int cols = bl1->col_num;
+    const int64_t na = bl1->row_num, nb = bl2->row_num;
+    if (na + nb == 0) return SMJ_OK;
+    if (!out) return SMJ_ERR_INVALID;
+    DevBuf da, db, dout;
+    SMJ_TRY(da.alloc((size_t)na * cols * 8));
+    SMJ_TRY(db.alloc((size_t)nb * cols * 8));
+    SMJ_TRY(dout.alloc((size_t)(na + nb) * cols * 8));
+    hipStream_t s = g_host_stream;
+    if (na) HIP_TRY(hipMemcpyAsync(da.p, a, (size_t)na * cols * 8, hipMemcpyHostToDevice, s));
+    if (nb) HIP_TRY(hipMemcpyAsync(db.p, b, (size_t)nb * cols * 8, hipMemcpyHostToDevice, s));
+    SMJ_TRY(smj_dev_merge((T *)da.p, na, (T *)db.p, nb, cols, key_col, (T *)dout.p, s));
+    HIP_TRY(hipMemcpyAsync(out, dout.p, (size_t)(na + nb) * cols * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SMJ_OK;
+}
+
+extern "C" int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_, const T *S, int key1, int key2,
+                        T **out, int64_t *out_rows) {
+    SMJ_TRY(need_init());
+    SMJ_TRY(check_block(r, R));
+    SMJ_TRY(check_block(s_, S));
+    if (!out || !out_rows || key1 < 0 || key1 >= r->col_num || key2 < 0 || key2 >= s_->col_num)
+        return SMJ_ERR_INVALID;
+    const int c1 = r->col_num, c2 = s_->col_num, tc = c1 + c2 - 1;
+    const int64_t nr = r->row_num, ns = s_->row_num, cap = std::min(nr, ns);
+    DevBuf dr, ds, dout, dcnt;
+    SMJ_TRY(dr.alloc((size_t)nr * c1 * 8));
+    SMJ_TRY(ds.alloc((size_t)ns * c2 * 8));
+    SMJ_TRY(dout.alloc((size_t)cap * tc * 8));
+    SMJ_TRY(dcnt.alloc(sizeof(int64_t)));
+    hipStream_t st = g_host_stream;
+    if (nr) HIP_TRY(hipMemcpyAsync(dr.p, R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
+    if (ns) HIP_TRY(hipMemcpyAsync(ds.p, S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
+    int64_t j = 0;
+    SMJ_TRY(smj_dev_join((T *)dr.p, nr, c1, (T *)ds.p, ns, c2, key1, key2, (T *)dout.p, (int64_t *)dcnt.p, &j, st));
+    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
+    if (!res) return SMJ_ERR_NOMEM;
+    if (j) HIP_TRY(hipMemcpyAsync(res, dout.p, (size_t)j * tc * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *out = res;
+    *out_rows = j;
+    return SMJ_OK;
+}
+
+extern "C" int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_, const T *S,
+                                   int select_col1, T select_val1, int select_col2, T select_val2, int key1,
+                                   int key2, T **out, int64_t *out_rows, smj_timing_t *timing) {
+    SMJ_TRY(need_init());
+    SMJ_TRY(check_block(r, R));
+    SMJ_TRY(check_block(s_, S));
+    if (!out || !out_rows) return SMJ_ERR_INVALID;
+    const int c1 = r->col_num, c2 = s_->col_num, tc = c1 + c2 - 1;
+    if (key1 < 0 || key1 >= c1 || key2 < 0 || key2 >= c2 || select_col1 < 0 || select_col1 >= c1 ||
+        select_col2 < 0 || select_col2 >= c2)
+        return SMJ_ERR_INVALID;
+    const int64_t nr = r->row_num, ns = s_->row_num;
+    hipStream_t st = g_host_stream;
+    hipEvent_t ev[5];
+    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 5; i++) hipEventDestroy(e[i]); } } evf{ev};
+    DevBuf dr, ds, drs, dss, dout, dcnt;
+    SMJ_TRY(dr.alloc((size_t)nr * c1 * 8));
+    SMJ_TRY(ds.alloc((size_t)ns * c2 * 8));
+    SMJ_TRY(drs.alloc((size_t)nr * c1 * 8));
+    SMJ_TRY(dss.alloc((size_t)ns * c2 * 8));
+    SMJ_TRY(dcnt.alloc(sizeof(int64_t)));
+    HIP_TRY(hipEventRecord(ev[0], st));
+    if (nr) HIP_TRY(hipMemcpyAsync(dr.p, R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
+    if (ns) HIP_TRY(hipMemcpyAsync(ds.p, S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
+    int64_t mr = 0, ms = 0, j = 0;
+    SMJ_TRY(dev_select_sort((T *)dr.p, nr, c1, 1, select_col1, select_val1, key1, 0, (T *)drs.p, &mr, st));
+    SMJ_TRY(dev_select_sort((T *)ds.p, ns, c2, 1, select_col2, select_val2, key2, 0, (T *)dss.p, &ms, st));
+    SMJ_TRY(dout.alloc((size_t)std::min(mr, ms) * tc * 8));
+    SMJ_TRY(smj_dev_join((T *)drs.p, mr, c1, (T *)dss.p, ms, c2, key1, key2, (T *)dout.p, (int64_t *)dcnt.p, &j,
+                         st));
+    HIP_TRY(hipEventRecord(ev[2], st));
+    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
+    if (!res) return SMJ_ERR_NOMEM;
+    if (j) HIP_TRY(hipMemcpyAsync(res, dout.p, (size_t)j * tc * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(ev[3], st));
+    HIP_TRY(hipStreamSynchronize(st));
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    int rc = check_err(sc, 0, st);
+    if (rc != SMJ_OK) {
+        free(res);
+        return rc;
+    }
+    if (timing) {
+        timing->cpu_gpu_ms = ev_ms(ev[0], ev[1]);
+        timing->gpu_ms = ev_ms(ev[1], ev[2]);
+        timing->gpu_cpu_ms = ev_ms(ev[2], ev[3]);
+    }
+    *out = res;
+    *out_rows = j;
+    return SMJ_OK;
+}

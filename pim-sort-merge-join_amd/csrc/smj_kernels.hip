@@ -1,0 +1,858 @@
+// smj_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the sort-merge-join
+// hot path.  Row layout: row-major int64 tables (include/common.h), any column
+// count 1..8, key / select columns chosen at run time.
+//
+// Reference map (the DPU kernels these replace; /root/reference/sort-merge-join):
+//   hist_radix_kernel + onesweep_kernel  <- select.c (:63-194) fused with
+//       sort_dpu.c (:189-328) and the merge tree (merge_dpu.c :55-223, app.c
+//       :412-547): a stable LSD radix sort whose first pass also applies the
+//       WHERE predicate (cpu_app.c select_in_cpu :81-112 + insertion_sort_in_cpu
+//       :172-202 semantics: stable, signed ascending).
+//   merge_partition_kernel + join_tile_kernel <- join.c (:58-266) + host
+//       splitters (app.c :585-633): merge-path partitioned 1:1 zip join
+//       (cpu_app.c join_in_cpu :204-266 semantics).
+//   merge_tile_kernel <- merge_dpu.c (:55-223): stable merge-path merge.
+//
+// Everything here is HBM-bandwidth-bound integer work: no MFMA.  See DESIGN.md
+// for the roofline and per-kernel algorithmic bytes.
+#include "smj_internal.h"
+
+#include <math.h>
+
+#include <algorithm>
+
+namespace smj {
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint64_t biased(int64_t k) { return (uint64_t)k ^ 0x8000000000000000ull; }
+
+template <int COLS>
+__device__ __forceinline__ void load_row(const int64_t *__restrict__ p, int64_t (&r)[COLS]) {
+    if constexpr (COLS % 2 == 0) {
+        const i64x2 *q = reinterpret_cast<const i64x2 *>(p);
+#pragma unroll
+        for (int c = 0; c < COLS / 2; c++) {
+            i64x2 t = q[c];
+            r[2 * c] = t.x;
+            r[2 * c + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < COLS; c++) r[c] = p[c];
+    }
+}
+
+template <int COLS>
+__device__ __forceinline__ void store_row(int64_t *__restrict__ p, const int64_t (&r)[COLS]) {
+    if constexpr (COLS % 2 == 0) {
+        i64x2 *q = reinterpret_cast<i64x2 *>(p);
+#pragma unroll
+        for (int c = 0; c < COLS / 2; c++) {
+            i64x2 t;
+            t.x = r[2 * c];
+            t.y = r[2 * c + 1];
+            q[c] = t;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < COLS; c++) p[c] = r[c];
+    }
+}
+
+// r[col] with a run-time col, compile-time indexing only (no scratch).
+template <int COLS>
+__device__ __forceinline__ int64_t pick(const int64_t (&r)[COLS], int col) {
+    int64_t v = r[0];
+#pragma unroll
+    for (int c = 1; c < COLS; c++) v = (col == c) ? r[c] : v;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t ld_status(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll one look-back status word until a predecessor has published it.
+// Bounded: after ~2^22 polls (seconds) the wait gives up, flags the error
+// word and returns an inclusive 0 so that the grid always drains.
+__device__ __forceinline__ uint32_t spin_status(const uint32_t *p, uint32_t *err) {
+    uint32_t w = ld_status(p);
+    uint32_t spins = 0;
+    while ((w & (kFlagAgg | kFlagInc)) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        w = ld_status(p);
+        if (++spins > (1u << 22)) {
+            atomicOr(err, 1u);
+            return kFlagInc;
+        }
+    }
+    return w;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// lower_bound / upper_bound over an LDS key array
+__device__ __forceinline__ int lds_lower_bound(const int64_t *a, int n, int64_t k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int lds_upper_bound(const int64_t *a, int n, int64_t k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] <= k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------
+// digit functors
+// ---------------------------------------------------------------------------
+struct RadixDigit {   // digit of the biased key, relative to a base
+    uint64_t base;
+    int shift;
+    __device__ __forceinline__ uint32_t operator()(int64_t key) const {
+        return (uint32_t)((biased(key) - base) >> shift);
+    }
+};
+struct ZeroDigit {    // select-only compaction: one bin
+    __device__ __forceinline__ uint32_t operator()(int64_t) const { return 0; }
+};
+struct BucketDigit {  // multi-GPU range partition: #splitters < key
+    int64_t spl[kMaxSplitters];
+    int nspl;
+    __device__ __forceinline__ uint32_t operator()(int64_t key) const {
+        uint32_t b = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxSplitters; i++) b += (i < nspl && spl[i] < key) ? 1u : 0u;
+        return b;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// onesweep pass
+// ---------------------------------------------------------------------------
+template <class DigitF>
+struct PassParams {
+    const int64_t *src;
+    int64_t *dst;
+    int64_t nsrc;
+    int64_t sel_val;
+    int use_select, sel_col, key_col, pad;
+    DigitF digit;
+    const uint32_t *bin_base;  // global exclusive digit prefix (nullptr = 0)
+    uint32_t *status;          // [tiles][RADIX] look-back words, zeroed
+    Counters *ctr;             // zeroed
+};
+
+template <int COLS, int DBITS>
+struct PassLds {
+    static constexpr int RADIX = 1 << DBITS;
+    static constexpr int TILE = sort_tile_rows(COLS);
+    static constexpr int ROW_BYTES = TILE * COLS * 8;
+    static constexpr int CNT_BYTES = kSortWaves * RADIX * 4;
+    static constexpr int A = ROW_BYTES > CNT_BYTES ? ROW_BYTES : CNT_BYTES;
+    static constexpr int OFF_BIN = A;
+    static constexpr int OFF_ADJ = OFF_BIN + ((RADIX * 4 + 15) / 16) * 16;
+    static constexpr int OFF_MISC = OFF_ADJ + ((RADIX * 8 + 15) / 16) * 16;
+    static constexpr int BYTES = OFF_MISC + 64;
+};
+
+// One tile per workgroup; tiles are claimed in launch order through an
+// atomic counter so a tile's predecessors are always running or done when
+// it looks back (forward progress of the spin waits).
+template <int COLS, int DBITS, class DigitF>
+__global__ __launch_bounds__(kSortThreads, 4) void onesweep_kernel(const PassParams<DigitF> p) {
+    using L = PassLds<COLS, DBITS>;
+    constexpr int RADIX = L::RADIX;
+    constexpr int ITEMS = sort_items(COLS);
+    constexpr int TILE = L::TILE;
+    constexpr uint32_t MASK = RADIX - 1;
+    constexpr int BPT = RADIX >= kSortThreads ? RADIX / kSortThreads : 1;
+
+    __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
+    int64_t *s_rows = reinterpret_cast<int64_t *>(smem);          // after ranking
+    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(smem);        // during ranking
+    uint32_t *s_binstart = reinterpret_cast<uint32_t *>(smem + L::OFF_BIN);
+    int64_t *s_adj = reinterpret_cast<int64_t *>(smem + L::OFF_ADJ);
+    uint32_t *s_misc = reinterpret_cast<uint32_t *>(smem + L::OFF_MISC);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_misc[0] = atomicAdd(&p.ctr->tile, 1u);
+    for (int i = tid; i < kSortWaves * RADIX; i += kSortThreads) s_wcnt[i] = 0;
+    __syncthreads();
+    const uint32_t tile = s_misc[0];
+
+    // ---- load: wave w owns rows [w*ITEMS*64, (w+1)*ITEMS*64) of the tile,
+    //      item i is 64 consecutive rows -> 64 x (8*COLS) B per instruction.
+    const int64_t row0 = (int64_t)tile * TILE + (int64_t)wave * (ITEMS * 64) + lane;
+    int64_t rows[ITEMS][COLS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const int64_t r = row0 + it * 64;
+        if (r < p.nsrc) load_row<COLS>(p.src + r * COLS, rows[it]);
+        else {
+#pragma unroll
+            for (int c = 0; c < COLS; c++) rows[it][c] = 0;
+        }
+    }
+    uint32_t dig[ITEMS];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const int64_t r = row0 + it * 64;
+        bool v = r < p.nsrc;
+        if (p.use_select) v = v && (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+        dig[it] = v ? (p.digit(pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
+        vmask |= v ? (1u << it) : 0u;
+    }
+
+    // ---- rank: stable within the tile.  Peers with the same digit in one
+    //      64-row item are found with DBITS ballots; per-wave running digit
+    //      counters in LDS order items within the wave.
+    uint32_t rank[ITEMS];
+    uint32_t *wc = s_wcnt + wave * RADIX;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const bool v = (vmask >> it) & 1u;
+        uint64_t peers = __ballot(v);
+#pragma unroll
+        for (int b = 0; b < DBITS; b++) {
+            const bool bit = (dig[it] >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        rank[it] = 0;
+        if (v) {
+            const uint32_t base = wc[dig[it]];
+            rank[it] = base + (uint32_t)__popcll(peers & lt_mask);
+            if ((peers >> lane) == 1ull) wc[dig[it]] = base + (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+
+    // ---- per-digit totals and cross-wave exclusive prefix (in place)
+    uint32_t tot[BPT];
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; j++) {
+        const int d = tid * BPT + j;
+        uint32_t run = 0;
+        if (d < RADIX) {
+#pragma unroll
+            for (int w = 0; w < kSortWaves; w++) {
+                const uint32_t c = s_wcnt[w * RADIX + d];
+                s_wcnt[w * RADIX + d] = run;
+                run += c;
+            }
+        }
+        tot[j] = run;
+        tsum += run;
+    }
+    // publish this tile's digit counts at once (unblocks successors)
+    uint32_t *st = p.status + (size_t)tile * RADIX;
+#pragma unroll
+    for (int j = 0; j < BPT; j++) {
+        const int d = tid * BPT + j;
+        if (d < RADIX) st_status(st + d, (tile == 0 ? kFlagInc : kFlagAgg) | tot[j]);
+    }
+    // block exclusive scan of digit totals -> tile-local digit starts
+    const uint32_t incl = wave_incl_scan(tsum, lane);
+    if (lane == 63) s_misc[4 + wave] = incl;
+    __syncthreads();
+    uint32_t woff = 0, tile_total = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) {
+        const uint32_t x = s_misc[4 + w];
+        woff += (w < wave) ? x : 0u;
+        tile_total += x;
+    }
+    {
+        uint32_t run = woff + incl - tsum;
+#pragma unroll
+        for (int j = 0; j < BPT; j++) {
+            const int d = tid * BPT + j;
+            if (d < RADIX) s_binstart[d] = run;
+            run += tot[j];
+        }
+    }
+    __syncthreads();
+
+    // ---- tile-local destination of every row
+    uint32_t pos[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++)
+        pos[it] = ((vmask >> it) & 1u) ? s_binstart[dig[it]] + wc[dig[it]] + rank[it] : 0u;
+    __syncthreads();  // counters dead from here: the region becomes the row tile
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++)
+        if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)pos[it] * COLS, rows[it]);
+
+    // ---- decoupled look-back: global start of each digit's run of this tile
+#pragma unroll
+    for (int j = 0; j < BPT; j++) {
+        const int d = tid * BPT + j;
+        if (d < RADIX) {
+            uint32_t excl = 0;
+            if (tile > 0) {
+                int64_t t = (int64_t)tile - 1;
+                while (true) {
+                    const uint32_t w = spin_status(p.status + (size_t)t * RADIX + d, &p.ctr->err);
+                    excl += w & kValueMask;
+                    if ((w & kFlagInc) || t == 0) break;
+                    --t;
+                }
+                st_status(st + d, kFlagInc | (excl + tot[j]));
+            }
+            const int64_t gbase = p.bin_base ? (int64_t)p.bin_base[d] : 0;
+            s_adj[d] = gbase + (int64_t)excl - (int64_t)s_binstart[d];
+        }
+    }
+    if (tid == 0 && tile_total) atomicAdd(&p.ctr->count, tile_total);
+    __syncthreads();
+
+    // ---- scatter: consecutive LDS rows of one digit -> consecutive HBM rows
+    for (uint32_t i = tid; i < tile_total; i += kSortThreads) {
+        int64_t r[COLS];
+        load_row<COLS>(s_rows + (size_t)i * COLS, r);
+        const uint32_t d = p.digit(pick<COLS>(r, p.key_col)) & MASK;
+        store_row<COLS>(p.dst + (s_adj[d] + (int64_t)i) * COLS, r);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// histogram (upsweep) of all digit positions of the selected rows
+// ---------------------------------------------------------------------------
+template <int COLS>
+__global__ __launch_bounds__(512) void hist_radix_kernel(const int64_t *__restrict__ src, int64_t n,
+                                                         int use_select, int sel_col, int64_t sel_val,
+                                                         int key_col, uint64_t base,
+                                                         uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t sh[kNumPos * kRadix];
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int i = tid; i < kNumPos * kRadix; i += 512) sh[i] = 0;
+    __syncthreads();
+    constexpr int U = 4;
+    const int64_t stride = (int64_t)gridDim.x * 512 * U;
+    for (int64_t r0 = (int64_t)blockIdx.x * 512 * U; r0 < n; r0 += stride) {
+        int64_t key[U], sv[U];
+        bool v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t r = r0 + u * 512 + tid;
+            v[u] = r < n;
+            key[u] = v[u] ? src[r * COLS + key_col] : 0;
+            sv[u] = (v[u] && use_select) ? src[r * COLS + sel_col] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool ok = v[u] && (!use_select || sv[u] > sel_val);
+            const uint64_t act = __ballot(ok);
+            if (act == 0) continue;
+            const int leader = __ffsll((unsigned long long)act) - 1;
+            const uint64_t x = biased(key[u]) - base;
+#pragma unroll
+            for (int ps = 0; ps < kNumPos; ps++) {
+                const uint32_t d = (uint32_t)(x >> (ps * kRadixBits)) & (kRadix - 1);
+                const uint32_t dl = __shfl(d, leader, 64);
+                const uint64_t same = __ballot(ok && d == dl);
+                if (same == act) {
+                    if (lane == leader) atomicAdd(&sh[ps * kRadix + dl], (uint32_t)__popcll(act));
+                } else if (ok) {
+                    atomicAdd(&sh[ps * kRadix + d], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < kNumPos * kRadix; i += 512) {
+        const uint32_t c = sh[i];
+        if (c) atomicAdd(&ghist[i], c);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// plan: selected row count, non-trivial digit positions, in-place exclusive
+// scan of their histograms.  One workgroup of 1024 threads (= kRadix).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_sum_1024(uint32_t v, uint32_t *scratch) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) scratch[wave] = v;
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) s += scratch[w];
+    return s;
+}
+__device__ __forceinline__ uint32_t block_max_1024(uint32_t v, uint32_t *scratch) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
+    __syncthreads();
+    if (lane == 0) scratch[wave] = v;
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) s = max(s, scratch[w]);
+    return s;
+}
+__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t *scratch) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    __syncthreads();
+    if (lane == 63) scratch[wave] = incl;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) off += (w < wave) ? scratch[w] : 0u;
+    return off + incl - v;
+}
+
+__global__ __launch_bounds__(1024) void plan_kernel(uint32_t *ghist, SortPlan *plan) {
+    __shared__ uint32_t scratch[16];
+    __shared__ int s_np;
+    __shared__ int s_pos[8];
+    const int tid = threadIdx.x;
+    const uint32_t m = block_sum_1024(ghist[tid], scratch);
+    if (tid == 0) s_np = 0;
+    __syncthreads();
+    for (int ps = 0; ps < kNumPos; ps++) {
+        const uint32_t mx = block_max_1024(ghist[ps * kRadix + tid], scratch);
+        if (tid == 0 && m > 0 && mx < m) s_pos[s_np++] = ps;
+        __syncthreads();
+    }
+    if (tid == 0 && s_np == 0) { s_pos[0] = 0; s_np = 1; }  // still one pass: it compacts
+    __syncthreads();
+    const int np = s_np;
+    for (int k = 0; k < np; k++) {
+        uint32_t *h = ghist + s_pos[k] * kRadix;
+        const uint32_t e = block_excl_scan_1024(h[tid], scratch);
+        h[tid] = e;
+    }
+    if (tid == 0) {
+        plan->m = m;
+        plan->npasses = np;
+        for (int k = 0; k < 8; k++) plan->pos[k] = k < np ? s_pos[k] : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU partition: per-bucket counts + min/max of selected keys
+// ---------------------------------------------------------------------------
+template <int COLS>
+__global__ __launch_bounds__(512) void hist_bucket_kernel(const int64_t *__restrict__ src, int64_t n,
+                                                          int use_select, int sel_col, int64_t sel_val,
+                                                          int key_col, const BucketDigit dg,
+                                                          unsigned long long *gcount,
+                                                          long long *gminmax) {
+    __shared__ uint32_t sh[1 << kBucketBits];
+    __shared__ long long smin[8], smax[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < (1 << kBucketBits)) sh[tid] = 0;
+    __syncthreads();
+    long long mn = INT64_MAX, mx = INT64_MIN;
+    for (int64_t r = (int64_t)blockIdx.x * 512 + tid; r < n; r += (int64_t)gridDim.x * 512) {
+        const int64_t key = src[r * COLS + key_col];
+        const bool ok = !use_select || src[r * COLS + sel_col] > sel_val;
+        if (ok) {
+            atomicAdd(&sh[dg(key)], 1u);
+            mn = min(mn, (long long)key);
+            mx = max(mx, (long long)key);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (long long)__shfl_xor(mn, o, 64));
+        mx = max(mx, (long long)__shfl_xor(mx, o, 64));
+    }
+    if (lane == 0) { smin[wave] = mn; smax[wave] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 8; w++) { mn = min(mn, smin[w]); mx = max(mx, smax[w]); }
+        if (mn != INT64_MAX) {
+            atomicMin(&gminmax[0], mn);
+            atomicMax(&gminmax[1], mx);
+        }
+    }
+    if (tid < (1 << kBucketBits) && sh[tid]) atomicAdd(&gcount[tid], (unsigned long long)sh[tid]);
+}
+
+// ---------------------------------------------------------------------------
+// merge path: a_t = #rows of A among the first min(t*kJoinTile, na+nb) rows
+// of the stable merge (A first on equal keys).
+// ---------------------------------------------------------------------------
+__global__ void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na, int ca, int ka,
+                                       const int64_t *__restrict__ b, int64_t nb, int cb, int kb,
+                                       int64_t *apart, int64_t ntiles) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const int64_t d = min(t * (int64_t)kJoinTile, na + nb);
+    int64_t lo = max((int64_t)0, d - nb), hi = min(d, na);
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        // A[mid] precedes B[d-1-mid] iff A.key <= B.key  -> take more of A
+        if (a[mid * ca + ka] <= b[(d - 1 - mid) * cb + kb]) lo = mid + 1; else hi = mid;
+    }
+    apart[t] = lo;
+}
+
+// ---------------------------------------------------------------------------
+// join: one merge-path tile per workgroup.  For every R row i (key k):
+//   lbS(k) = b0 + #{S-piece keys < k}      (merge path: S[<b0] < k <= S[>=b1])
+//   lbR(k) = first R row with key k        (local, or galloped for the tile's first key)
+//   occ = i - lbR(k);  partner p = lbS(k) + occ;  match iff S[p].key == k
+// which is exactly cpu_app.c's zip (:211-227): the occ-th R occurrence of k
+// pairs with the occ-th S occurrence.  Output rows in R order; tile offsets
+// by single-word decoupled look-back.
+// ---------------------------------------------------------------------------
+struct JoinParams {
+    const int64_t *R;
+    const int64_t *S;
+    const int64_t *apart;
+    int64_t *out;
+    int64_t *out_rows;
+    uint32_t *status;
+    Counters *ctr;
+    int64_t nr, ns, ntiles;
+    int c1, key1, c2, key2;
+};
+
+__global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParams p) {
+    __shared__ int64_t s_keys[kJoinTile];
+    __shared__ uint32_t s_scan[kJoinThreads / 64];
+    __shared__ int64_t s_lbr0;
+    __shared__ uint32_t s_tile, s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(&p.ctr->tile, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t L = p.nr + p.ns;
+    const int64_t d0 = tile * kJoinTile, d1 = min(d0 + kJoinTile, L);
+    const int64_t a0 = p.apart[tile], a1 = p.apart[tile + 1];
+    const int64_t b0 = d0 - a0, b1 = d1 - a1;
+    const int nR = (int)(a1 - a0), nS = (int)(b1 - b0);
+    for (int j = tid; j < nR + nS; j += kJoinThreads)
+        s_keys[j] = j < nR ? p.R[(a0 + j) * p.c1 + p.key1] : p.S[(b0 + j - nR) * p.c2 + p.key2];
+    if (tid == 0 && nR > 0) {
+        // first R row carrying R[a0].key: gallop backwards, then bisect
+        const int64_t k = p.R[a0 * p.c1 + p.key1];
+        int64_t first = a0;
+        if (a0 > 0 && p.R[(a0 - 1) * p.c1 + p.key1] == k) {
+            int64_t hi = a0 - 1, lo = -1, step = 1;  // R[hi] == k
+            while (true) {
+                const int64_t c = hi - step;
+                if (c < 0) { lo = -1; break; }
+                if (p.R[c * p.c1 + p.key1] != k) { lo = c; break; }
+                hi = c;
+                step <<= 1;
+            }
+            int64_t l = lo + 1, h = hi;  // first equal lies in (lo, hi]
+            while (l < h) {
+                const int64_t mid = (l + h) >> 1;
+                if (p.R[mid * p.c1 + p.key1] == k) h = mid; else l = mid + 1;
+            }
+            first = l;
+        }
+        const int64_t hi = first;
+        s_lbr0 = hi;
+    }
+    __syncthreads();
+
+    const int64_t *sk = s_keys + nR;
+    uint32_t mmask = 0;
+    int64_t part[kJoinPer];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kJoinPer; q++) {
+        const int j = tid * kJoinPer + q;
+        part[q] = 0;
+        if (j < nR) {
+            const int64_t k = s_keys[j];
+            const int lb_loc = lds_lower_bound(s_keys, j, k);
+            const int64_t lbr = lb_loc == 0 ? s_lbr0 : a0 + lb_loc;
+            const int64_t lbs = b0 + lds_lower_bound(sk, nS, k);
+            const int64_t pidx = lbs + (a0 + j - lbr);
+            if (pidx < p.ns) {
+                const int64_t skey = pidx < b1 ? sk[pidx - b0] : p.S[pidx * p.c2 + p.key2];
+                if (skey == k) {
+                    mmask |= 1u << q;
+                    part[q] = pidx;
+                    cnt++;
+                }
+            }
+        }
+    }
+    // block exclusive scan of match counts
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    if (lane == 63) s_scan[wave] = incl;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kJoinThreads / 64; w++) {
+        const uint32_t x = s_scan[w];
+        off += (w < wave) ? x : 0u;
+        total += x;
+    }
+    off += incl - cnt;
+    if (tid == 0) {
+        uint32_t excl = 0;
+        if (tile == 0) {
+            st_status(p.status, kFlagInc | total);
+        } else {
+            st_status(p.status + tile, kFlagAgg | total);
+            int64_t t = tile - 1;
+            while (true) {
+                const uint32_t w = spin_status(p.status + t, &p.ctr->err);
+                excl += w & kValueMask;
+                if ((w & kFlagInc) || t == 0) break;
+                --t;
+            }
+            st_status(p.status + tile, kFlagInc | (excl + total));
+        }
+        s_excl = excl;
+        if (tile == p.ntiles - 1) *p.out_rows = (int64_t)excl + total;
+    }
+    __syncthreads();
+    if (!mmask) return;
+    const int tc = p.c1 + p.c2 - 1;
+    int64_t o = (int64_t)s_excl + off;
+#pragma unroll
+    for (int q = 0; q < kJoinPer; q++) {
+        if ((mmask >> q) & 1u) {
+            const int64_t i = a0 + tid * kJoinPer + q;
+            int64_t *dst = p.out + o * tc;
+            const int64_t *rr = p.R + i * p.c1;
+            const int64_t *ss = p.S + part[q] * p.c2;
+            for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
+            for (int c = 0, k = p.c1; c < p.c2; c++)
+                if (c != p.key2) dst[k++] = ss[c];
+            ++o;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stable merge of two sorted runs (merge_dpu.c replacement)
+// ---------------------------------------------------------------------------
+template <int COLS>
+__global__ __launch_bounds__(kJoinThreads) void merge_tile_kernel(const int64_t *__restrict__ a, int64_t na,
+                                                                  const int64_t *__restrict__ b, int64_t nb,
+                                                                  int key_col, const int64_t *apart,
+                                                                  int64_t *__restrict__ out) {
+    __shared__ int64_t s_keys[kJoinTile];
+    const int tid = threadIdx.x;
+    const int64_t tile = blockIdx.x;
+    const int64_t d0 = tile * kJoinTile, d1 = min(d0 + kJoinTile, na + nb);
+    const int64_t a0 = apart[tile], a1 = apart[tile + 1];
+    const int64_t b0 = d0 - a0, b1 = d1 - a1;
+    const int nA = (int)(a1 - a0), nB = (int)(b1 - b0);
+    for (int j = tid; j < nA + nB; j += kJoinThreads)
+        s_keys[j] = j < nA ? a[(a0 + j) * COLS + key_col] : b[(b0 + j - nA) * COLS + key_col];
+    __syncthreads();
+    for (int j = tid; j < nA + nB; j += kJoinThreads) {
+        int64_t r[COLS];
+        int64_t dst;
+        if (j < nA) {
+            dst = d0 + j + lds_lower_bound(s_keys + nA, nB, s_keys[j]);
+            load_row<COLS>(a + (a0 + j) * COLS, r);
+        } else {
+            const int jj = j - nA;
+            dst = d0 + jj + lds_upper_bound(s_keys, nA, s_keys[j]);
+            load_row<COLS>(b + (b0 + jj) * COLS, r);
+        }
+        store_row<COLS>(out + dst * COLS, r);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic tables: splitmix64, payload = global row index
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ void gen_uniform_kernel(int64_t *out, int64_t row0, int64_t rows, uint64_t seed,
+                                   uint64_t key_range) {
+    const uint64_t salt = seed * 0xD1B54A32D192ED03ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = (uint64_t)(row0 + i);
+        const uint64_t h = splitmix64(g + salt);
+        i64x2 v;
+        v.x = (long long)(1 + __umul64hi(h, key_range));
+        v.y = (long long)g;
+        reinterpret_cast<i64x2 *>(out)[i] = v;
+    }
+}
+
+__global__ void gen_zipf_kernel(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t n,
+                                double theta, double zetan) {
+    const uint64_t salt = seed * 0xD1B54A32D192ED03ull;
+    const double alpha = 1.0 / (1.0 - theta);
+    const double zeta2 = 1.0 + pow(0.5, theta);
+    const double eta = (1.0 - pow(2.0 / (double)n, 1.0 - theta)) / (1.0 - zeta2 / zetan);
+    const uint64_t A = 2654435761ull;  // odd prime, coprime with any 2^a 5^b domain
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = (uint64_t)(row0 + i);
+        const double u = (double)(splitmix64(g + salt) >> 11) * 0x1.0p-53;
+        const double uz = u * zetan;
+        int64_t rank;  // 1-based
+        if (uz < 1.0) rank = 1;
+        else if (uz < zeta2) rank = 2;
+        else rank = 1 + (int64_t)((double)n * pow(eta * u - eta + 1.0, alpha));
+        rank = rank < 1 ? 1 : (rank > n ? n : rank);
+        const uint64_t key = (uint64_t)(((unsigned __int128)(uint64_t)(rank - 1) * A + 12345u) %
+                                        (unsigned __int128)(uint64_t)n);
+        i64x2 v;
+        v.x = (long long)(key + 1);
+        v.y = (long long)g;
+        reinterpret_cast<i64x2 *>(out)[i] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+#define SMJ_COLS_SWITCH(cols, ...)                    \
+    switch (cols) {                                   \
+    case 1: { constexpr int C = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int C = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int C = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int C = 4; __VA_ARGS__; } break; \
+    case 5: { constexpr int C = 5; __VA_ARGS__; } break; \
+    case 6: { constexpr int C = 6; __VA_ARGS__; } break; \
+    case 7: { constexpr int C = 7; __VA_ARGS__; } break; \
+    case 8: { constexpr int C = 8; __VA_ARGS__; } break; \
+    default: return hipErrorInvalidValue;             \
+    }
+
+static inline unsigned blocks_for(int64_t n, int64_t per) { return (unsigned)((n + per - 1) / per); }
+
+hipError_t launch_hist_radix(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
+                             int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist,
+                             hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, 2048), 1024));
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((hist_radix_kernel<C>), dim3(grid), dim3(512), 0, s, src, n,
+                                             use_select, sel_col, sel_val, key_col, key_base, ghist));
+    return hipGetLastError();
+}
+
+hipError_t launch_plan(uint32_t *ghist, SortPlan *plan, hipStream_t s) {
+    hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(1024), 0, s, ghist, plan);
+    return hipGetLastError();
+}
+
+hipError_t launch_radix_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int use_select,
+                             int sel_col, int64_t sel_val, int key_col, uint64_t key_base, int shift,
+                             const uint32_t *bin_base, uint32_t *status, Counters *ctr, hipStream_t s) {
+    PassParams<RadixDigit> p{src, dst, nsrc, sel_val, use_select, sel_col, key_col, 0,
+                             RadixDigit{key_base, shift}, bin_base, status, ctr};
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, kRadixBits, RadixDigit>),
+                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
+                                             dim3(kSortThreads), 0, s, p));
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int sel_col,
+                               int64_t sel_val, uint32_t *status, Counters *ctr, hipStream_t s) {
+    PassParams<ZeroDigit> p{src, dst, nsrc, sel_val, 1, sel_col, 0, 0, ZeroDigit{}, nullptr, status, ctr};
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, 0, ZeroDigit>),
+                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
+                                             dim3(kSortThreads), 0, s, p));
+    return hipGetLastError();
+}
+
+static BucketDigit make_bucket(const int64_t *spl, int nspl) {
+    BucketDigit d{};
+    for (int i = 0; i < kMaxSplitters; i++) d.spl[i] = i < nspl ? spl[i] : INT64_MAX;
+    d.nspl = nspl;
+    return d;
+}
+
+hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
+                              int64_t sel_val, int key_col, const int64_t *spl, int nspl,
+                              unsigned long long *gcount, long long *gminmax, hipStream_t s) {
+    const BucketDigit dg = make_bucket(spl, nspl);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, 2048), 1024));
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((hist_bucket_kernel<C>), dim3(grid), dim3(512), 0, s, src, n,
+                                             use_select, sel_col, sel_val, key_col, dg, gcount, gminmax));
+    return hipGetLastError();
+}
+
+hipError_t launch_bucket_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int use_select,
+                              int sel_col, int64_t sel_val, int key_col, const int64_t *spl, int nspl,
+                              const uint32_t *bin_base, uint32_t *status, Counters *ctr, hipStream_t s) {
+    PassParams<BucketDigit> p{src, dst, nsrc, sel_val, use_select, sel_col, key_col, 0,
+                              make_bucket(spl, nspl), bin_base, status, ctr};
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, kBucketBits, BucketDigit>),
+                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
+                                             dim3(kSortThreads), 0, s, p));
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
+                                  int64_t nb, int cb, int kb, int64_t *apart, int64_t ntiles,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(merge_partition_kernel, dim3(blocks_for(ntiles + 1, 256)), dim3(256), 0, s, a, na,
+                       ca, ka, b, nb, cb, kb, apart, ntiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_join_tiles(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns,
+                             int c2, int key2, const int64_t *apart, int64_t ntiles, int64_t *out,
+                             int64_t *out_rows, uint32_t *status, Counters *ctr, hipStream_t s) {
+    JoinParams p{R, S, apart, out, out_rows, status, ctr, nr, ns, ntiles, c1, key1, c2, key2};
+    hipLaunchKernelGGL(join_tile_kernel, dim3((unsigned)ntiles), dim3(kJoinThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_tiles(const int64_t *a, int64_t na, const int64_t *b, int64_t nb, int cols,
+                              int key_col, const int64_t *apart, int64_t ntiles, int64_t *out,
+                              hipStream_t s) {
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((merge_tile_kernel<C>), dim3((unsigned)ntiles),
+                                             dim3(kJoinThreads), 0, s, a, na, b, nb, key_col, apart, out));
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
+                              hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(rows, 256), 8192));
+    hipLaunchKernelGGL(gen_uniform_kernel, dim3(grid), dim3(256), 0, s, out, row0, rows, seed, key_range);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
+                           double theta, double zeta_n, hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(rows, 256), 8192));
+    hipLaunchKernelGGL(gen_zipf_kernel, dim3(grid), dim3(256), 0, s, out, row0, rows, seed, domain, theta,
+                       zeta_n);
+    return hipGetLastError();
+}
+
+}  // namespace smj

@@ -1,0 +1,177 @@
+"""Device-resident operators of the sort-merge-join hot path (torch tensors in,
+torch tensors out; the work is done by the HIP kernels behind libsmj_hip.so).
+
+Tables are 2-D int64 CUDA tensors [rows, cols], row-major and contiguous --
+the reference's T[row_num * col_num] layout (common.h).  Names follow the
+reference pipeline (cpu_app.c / app.c): select, sort, merge, join.
+"""
+import ctypes
+import json
+
+import torch
+
+from . import _lib
+
+BIAS = 1 << 63
+
+
+def biased(key: int) -> int:
+    """The unsigned radix order of a signed key: key ^ 2^63 (as uint64)."""
+    return (int(key) + BIAS) & ((1 << 64) - 1)
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else ctypes.c_void_p(0)
+
+
+def _table(t, name):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.int64 and t.dim() == 2
+            and t.is_contiguous()):
+        raise ValueError(f"{name} must be a contiguous 2-D int64 CUDA tensor")
+    return t
+
+
+def select_sort(table, key_col=0, select_col=0, select_val=None, key_base=0, out=None, stream=None):
+    """out[:m] <- stable sort on table[:, key_col] of the rows with
+    table[:, select_col] > select_val (all rows when select_val is None).
+    Returns the view out[:m] (m is read back: the call synchronises once)."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    if out is None:
+        out = torch.empty_like(table)
+    m = ctypes.c_int64(0)
+    use = select_val is not None
+    _lib.check(lib.smj_dev_select_sort(_ptr(table), n, cols, int(use), select_col,
+                                       int(select_val) if use else 0, key_col, biased_base(key_base),
+                                       _ptr(out), ctypes.byref(m), _stream(stream)), "smj_dev_select_sort")
+    return out[: m.value]
+
+
+def biased_base(key_base):
+    return int(key_base) & ((1 << 64) - 1)
+
+
+def select(table, select_col, select_val, out=None, stream=None):
+    """Stable compaction: rows with table[:, select_col] > select_val."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    if out is None:
+        out = torch.empty_like(table)
+    m = ctypes.c_int64(0)
+    _lib.check(lib.smj_dev_select(_ptr(table), n, cols, select_col, int(select_val), _ptr(out),
+                                  ctypes.byref(m), _stream(stream)), "smj_dev_select")
+    return out[: m.value]
+
+
+def merge(a, b, key_col=0, out=None, stream=None):
+    """Stable merge of two runs sorted on key_col (a's rows first on ties)."""
+    lib = _lib.load()
+    _table(a, "a")
+    _table(b, "b")
+    if a.shape[1] != b.shape[1]:
+        raise ValueError("runs must have the same column count")
+    if out is None:
+        out = torch.empty((a.shape[0] + b.shape[0], a.shape[1]), dtype=torch.int64, device=a.device)
+    _lib.check(lib.smj_dev_merge(_ptr(a), a.shape[0], _ptr(b), b.shape[0], a.shape[1], key_col, _ptr(out),
+                                 _stream(stream)), "smj_dev_merge")
+    return out
+
+
+def join(R, S, key1=0, key2=0, out=None, count=None, sync=True, stream=None):
+    """1:1 zip merge join of sorted R and S.  Returns out[:J] when sync, else
+    (out, count) with the row count left on the device in `count`."""
+    lib = _lib.load()
+    _table(R, "R")
+    _table(S, "S")
+    nr, c1 = R.shape
+    ns, c2 = S.shape
+    tc = c1 + c2 - 1
+    if out is None:
+        out = torch.empty((max(min(nr, ns), 1), tc), dtype=torch.int64, device=R.device)
+    if count is None:
+        count = torch.zeros(1, dtype=torch.int64, device=R.device)
+    j = ctypes.c_int64(0)
+    _lib.check(lib.smj_dev_join(_ptr(R), nr, c1, _ptr(S), ns, c2, key1, key2, _ptr(out),
+                                ctypes.c_void_p(count.data_ptr()), ctypes.byref(j) if sync else None,
+                                _stream(stream)), "smj_dev_join")
+    if sync:
+        return out[: j.value]
+    return out, count
+
+
+def partition_count(table, splitters, key_col=0, select_col=0, select_val=None, stream=None):
+    """Rows per destination bucket (bucket(k) = #{splitters < k}) + (min, max)
+    of the selected keys.  splitters: 1-D int64 CUDA tensor, sorted."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    ns = int(splitters.numel())
+    counts = (ctypes.c_int64 * (ns + 1))()
+    mm = (ctypes.c_int64 * 2)()
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition_count(_ptr(table), n, cols, int(use), select_col,
+                                           int(select_val) if use else 0, key_col, _ptr(splitters), ns,
+                                           counts, mm, _stream(stream)), "smj_dev_partition_count")
+    return [int(c) for c in counts], (int(mm[0]), int(mm[1]))
+
+
+def partition_scatter(table, splitters, counts, key_col=0, select_col=0, select_val=None, out=None,
+                      stream=None):
+    """Stable scatter of the selected rows into bucket-contiguous order."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    total = sum(counts)
+    if out is None:
+        out = torch.empty((max(total, 1), cols), dtype=torch.int64, device=table.device)
+    c = (ctypes.c_int64 * len(counts))(*counts)
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition_scatter(_ptr(table), n, cols, int(use), select_col,
+                                             int(select_val) if use else 0, key_col, _ptr(splitters),
+                                             int(splitters.numel()), c, _ptr(out), _stream(stream)),
+               "smj_dev_partition_scatter")
+    return out[:total]
+
+
+def gen_uniform(rows, row0=0, seed=1, key_range=None, device="cuda", out=None, stream=None):
+    """Synthetic (key, payload) table: keys iid uniform in [1, key_range],
+    payload = global row index."""
+    lib = _lib.load()
+    if key_range is None:
+        key_range = 3 * rows
+    if out is None:
+        out = torch.empty((rows, 2), dtype=torch.int64, device=device)
+    _lib.check(lib.smj_dev_gen_uniform(_ptr(out), row0, rows, seed, key_range, _stream(stream)),
+               "smj_dev_gen_uniform")
+    return out
+
+
+def gen_zipf(rows, row0=0, seed=3, domain=100_000_000, theta=0.9, device="cuda", out=None, stream=None):
+    """Synthetic Zipf(theta) keys over [1, domain]."""
+    lib = _lib.load()
+    zeta = lib.smj_zipf_zeta(domain, theta)
+    if out is None:
+        out = torch.empty((rows, 2), dtype=torch.int64, device=device)
+    _lib.check(lib.smj_dev_gen_zipf(_ptr(out), row0, rows, seed, domain, theta, zeta, _stream(stream)),
+               "smj_dev_gen_zipf")
+    return out
+
+
+def prof_enable(on=True):
+    _lib.load().smj_prof_enable(int(bool(on)))
+
+
+def prof_report():
+    """{kernel: {"launches", "ms", "bytes"}} since the last report."""
+    lib = _lib.load()
+    need = lib.smj_prof_report(None, 0)
+    buf = ctypes.create_string_buffer(max(need, 2))
+    lib.smj_prof_report(buf, len(buf))
+    return json.loads(buf.value.decode())
