@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X sort-merge-join throughput (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+Workload (BASELINE.json configs[2], "C3"): per GPU |R| = |S| = 1e8 rows of
+(int64 key, int64 payload), keys iid uniform in [1, 3n] (n = rows of the
+whole job's table), payload = global row index, R seed 1 / S seed 2, the
+reference's user.h WHERE col0 > 5000 and JOIN_KEY 0.  Inputs are generated
+on the device and resident in HBM before timing.  One step = the whole hot
+path: select + stable sort of R and of S, then the 1:1 zip join (N = 1);
+for N > 1 the range partition + RCCL all-to-all exchange comes first and
+per-GPU work is fixed (weak scaling: the N=8 job is 8e8 x 8e8).
+
+value = (|R| + |S| over all ranks) / max-over-ranks seconds per step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "pim-sort-merge-join_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from smj import ops  # noqa: E402
+from smj import dist as sdist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+SELECT = (0, 5000, 0, 5000)    # user.h SELECT_COL1/VAL1, SELECT_COL2/VAL2
+KEYS = (0, 0)                  # user.h JOIN_KEY1/2
+METRIC = "joined rows/sec on |R|=|S|=1e8 int64-key tables; achieved HBM GB/s vs peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rows", type=int, default=100_000_000, help="rows per table per GPU")
+    p.add_argument("--cpu-sample", type=int, default=131072,
+                   help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
+    p.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                   help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field")
+    return p.parse_args()
+
+
+def step_single(R, S, bufs):
+    Rs = ops.select_sort(R, KEYS[0], SELECT[0], SELECT[1], out=bufs["R"])
+    Ss = ops.select_sort(S, KEYS[1], SELECT[2], SELECT[3], out=bufs["S"])
+    out, cnt = ops.join(Rs, Ss, KEYS[0], KEYS[1], out=bufs["J"], count=bufs["cnt"], sync=False)
+    return cnt
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = a.rows
+    total = n * world
+    key_range = 3 * total
+    R = ops.gen_uniform(n, row0=rank * n, seed=1, key_range=key_range, device=dev)
+    S = ops.gen_uniform(n, row0=rank * n, seed=2, key_range=key_range, device=dev)
+    bufs = None
+    if world == 1:
+        bufs = {"R": torch.empty_like(R), "S": torch.empty_like(S),
+                "J": torch.empty((n, 3), dtype=torch.int64, device=dev),
+                "cnt": torch.zeros(1, dtype=torch.int64, device=dev)}
+    torch.cuda.synchronize()
+
+    def step():
+        if world == 1:
+            return step_single(R, S, bufs)
+        return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+    ops.prof_enable(True)
+    ops.prof_report()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for i in range(a.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ops.prof_enable(False)
+    prof = ops.prof_report()
+
+    joined = int(res.item()) if world == 1 else int(res.shape[0])
+    t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tt = t.clone()
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        joined = int(tt[1].item())
+        dt = float(t[0].item())
+    ms_step = dt / a.steps * 1e3
+    rows_step = 2 * total
+    value = rows_step / (dt / a.steps)
+
+    # roofline of the dominant kernel: algorithmic bytes / its event time
+    dom = max(prof.items(), key=lambda kv: kv[1]["ms"]) if prof else (None, None)
+    roof = None
+    if dom[0]:
+        name, d = dom
+        ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.pmc):
+            with open(a.pmc) as f:
+                pmc = json.load(f)
+            k = pmc.get("kernels", {}).get(name)
+            if k and pmc.get("rows_per_table") == n:
+                traffic = k.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": d["bytes"] / max(d["launches"], 1),
+                "avg_launch_ms": round(d["ms"] / max(d["launches"], 1), 4),
+                "share_of_step": round(d["ms"] / a.steps / ms_step, 3)}
+    # whole-pipeline roofline: 48 B per input row + 24 B per joined row
+    b_alg = 48.0 * rows_step + 24.0 * joined
+    pipe_gbs = b_alg / (dt / a.steps) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # CPU baseline leg only
+        m = min(a.cpu_sample, n)
+        Rh = R[:m].cpu().numpy()
+        Sh = S[:m].cpu().numpy()
+        secs, jrows, kind = oracle.time_cpu_pipeline(Rh, Sh, SELECT, KEYS)
+        cpu = {"value": round(2 * m / secs, 1), "unit": "rows/s", "cores": 1, "kind": kind,
+               "sample": f"first {m} rows of R and of S of this workload (keys in [1,{key_range}]); "
+                         f"cpu_app.c select + O(n^2) insertion sort + zip join, 1 thread, gcc -O2; "
+                         f"{secs:.2f} s, {jrows} joined rows"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "rows/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic: splitmix64 keys iid uniform in [1,3n], payload = global row index (generated on device)",
+            "config": {"workload": "C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, "
+                                   "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
+                       "rows_per_table_per_gpu": n, "rows_per_table_total": total, "key_range": key_range,
+                       "joined_rows": joined, "parallelism": f"range-partition x{world}"},
+            "roofline": roof,
+            "pipeline_roofline": {"alg_bytes_per_step": b_alg, "achieved": round(pipe_gbs, 1),
+                                  "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                  "frac": round(pipe_gbs / (HBM_PEAK_GBS * world), 4)},
+            "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / a.steps, 4),
+                            "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in prof.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

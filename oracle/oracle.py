@@ -8,7 +8,7 @@ cpu_app.c, see tests/golden/make_goldens.py).
 """
 import ctypes
 import os
-import subprocess
+import subprocess  # noqa: F401 (build)
 
 import numpy as np
 
@@ -144,6 +144,58 @@ def save_csv(path, table):
         raise ValueError("2-D table expected")
     if lib().smj_ref_save_csv(path.encode(), t.shape[1], t.shape[0], p) != 0:
         raise OSError(path)
+
+
+def time_cpu_pipeline(R, S, sel=(0, 5000, 0, 5000), keys=(0, 0)):
+    """Time cpu_app.c's select -> insertion sort -> join (:336-344) on two
+    in-memory tables, single thread.  Uses the REAL reference functions
+    (oracle/_ref/libcpu_app_ref.so, built from /root/reference by
+    `make -C oracle ref`) when present -> kind "reference"; otherwise our
+    restatement -> kind "port".  Returns (seconds, joined_rows, kind)."""
+    import time
+    R = np.ascontiguousarray(R, dtype=np.int64)
+    S = np.ascontiguousarray(S, dtype=np.int64)
+    libc = ctypes.CDLL(None)
+    libc.malloc.restype = _P
+    libc.malloc.argtypes = [ctypes.c_size_t]
+
+    def cbuf(a):
+        p = libc.malloc(max(a.nbytes, 8))
+        ctypes.memmove(p, a.ctypes.data, a.nbytes)
+        return _P(p)
+
+    if os.path.exists(REF_LIB):
+        ref = ctypes.CDLL(REF_LIB)
+        ref.select_in_cpu.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(_P), _L, _L]
+        ref.insertion_sort_in_cpu.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]
+        ref.join_in_cpu.argtypes = [ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
+                                    ctypes.c_int]
+        a, b = cbuf(R), cbuf(S)
+        ra, rb = ctypes.c_int(R.shape[0]), ctypes.c_int(S.shape[0])
+        t0 = time.perf_counter()
+        ref.select_in_cpu(R.shape[1], ctypes.byref(ra), ctypes.byref(a), sel[0], sel[1])
+        ref.select_in_cpu(S.shape[1], ctypes.byref(rb), ctypes.byref(b), sel[2], sel[3])
+        ref.insertion_sort_in_cpu(R.shape[1], ra.value, keys[0], ctypes.byref(a))
+        ref.insertion_sort_in_cpu(S.shape[1], rb.value, keys[1], ctypes.byref(b))
+        ref.join_in_cpu(R.shape[1], ra.value, a, S.shape[1], rb.value, b, keys[0], keys[1])
+        dt = time.perf_counter() - t0
+        rows = ctypes.c_int.in_dll(ref, "result_row_num").value
+        res = _P.in_dll(ref, "result")
+        for p in (a, b, res):
+            _libc.free(p)
+        res.value = None
+        return dt, rows, "reference"
+    t0 = time.perf_counter()
+    Rs = select(R, sel[0], sel[1])
+    Ss = select(S, sel[2], sel[3])
+    Rs = sort(Rs, keys[0], insertion=True)
+    Ss = sort(Ss, keys[1], insertion=True)
+    rows = lib().smj_ref_join_count(Rs.shape[1], Rs.shape[0], Rs.ctypes.data_as(_P), Ss.shape[1], Ss.shape[0],
+                                    Ss.ctypes.data_as(_P), keys[0], keys[1])
+    j = join(Rs, Ss, keys[0], keys[1])
+    dt = time.perf_counter() - t0
+    assert len(j) == rows
+    return dt, rows, "port"
 
 
 def pipeline_csv(path1, path2, out_path, sel=(0, 5000, 0, 5000), keys=(0, 0), insertion=False):

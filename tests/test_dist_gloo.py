@@ -1,0 +1,118 @@
+"""The multi-GPU driver (smj/dist.py) on CPU: world sizes 2 and 3 over gloo.
+
+The HIP operators are replaced -- in this test only -- by an oracle-backed
+stand-in with the same interface, so what is tested here is the distributed
+orchestration: splitter choice, stable bucket scatter semantics, the
+all_to_all exchange in source-rank order, the per-rank radix base, and that
+concatenating rank outputs in rank order reproduces cpu_app.c's result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+
+
+class OracleOps:
+    """CPU stand-in for smj.dist.HipOps (test infrastructure)."""
+
+    @staticmethod
+    def select_sort(table, key_col=0, select_col=0, select_val=None, key_base=0):
+        t = table.numpy()
+        out = oracle.select_sort(t, key_col, select_col, select_val)
+        if len(out):  # the radix base must be a lower bound of every key
+            biased = (out[:, key_col].astype(np.uint64) ^ np.uint64(1 << 63))
+            assert int(biased.min()) >= key_base
+        return torch.from_numpy(out.reshape(-1, t.shape[1]))
+
+    @staticmethod
+    def join(R, S, key1=0, key2=0):
+        return torch.from_numpy(oracle.join(R.numpy(), S.numpy(), key1, key2).reshape(-1, R.shape[1] + S.shape[1] - 1))
+
+    @staticmethod
+    def _keep(T, key, sc, sv, spl):
+        t = T.numpy()
+        keep = t if sv is None else t[t[:, sc] > sv]
+        bucket = np.searchsorted(spl.numpy(), keep[:, key], side="left")
+        return keep, bucket
+
+    @staticmethod
+    def partition_count(T, spl, key=0, sc=0, sv=None):
+        keep, bucket = OracleOps._keep(T, key, sc, sv, spl)
+        counts = np.bincount(bucket, minlength=spl.numel() + 1).tolist()
+        mm = (int(keep[:, key].min()), int(keep[:, key].max())) if len(keep) else ((1 << 63) - 1, -(1 << 63))
+        return counts, mm
+
+    @staticmethod
+    def partition_scatter(T, spl, counts, key=0, sc=0, sv=None):
+        keep, bucket = OracleOps._keep(T, key, sc, sv, spl)
+        return torch.from_numpy(keep[np.argsort(bucket, kind="stable")].copy())
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, R, S, cfg, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "pim-sort-merge-join_amd"), os.path.join(repo, "oracle"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smj import dist as sdist
+    from test_dist_gloo import OracleOps as Ops
+    # contiguous, uneven slices in input order
+    cuts_r = np.linspace(0, len(R), world + 1).astype(int)
+    cuts_s = np.sqrt(np.linspace(0, 1, world + 1)) * len(S)
+    cuts_s = cuts_s.astype(int)
+    r = torch.from_numpy(R[cuts_r[rank]:cuts_r[rank + 1]].copy())
+    s = torch.from_numpy(S[cuts_s[rank]:cuts_s[rank + 1]].copy())
+    out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=Ops, samples=cfg["samples"])
+    np.save(os.path.join(outdir, f"rank{rank}.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def make_tables(kind, n):
+    rng = np.random.default_rng(42)
+    if kind == "uniform":
+        return oracle.gen_uniform(n, 0, 1, 3 * n), oracle.gen_uniform(n, 0, 2, 3 * n)
+    if kind == "dups":  # heavy duplicates, 3 columns, key in column 1
+        R = rng.integers(0, 40, size=(n, 3)).astype(np.int64)
+        S = rng.integers(0, 40, size=(n // 2, 3)).astype(np.int64)
+        R[:, 0], S[:, 2] = np.arange(n), np.arange(n // 2) + 10 ** 6
+        return R, S
+    if kind == "skew":  # one key carries most rows, negative keys too
+        R = rng.integers(-1000, 1000, size=(n, 2)).astype(np.int64)
+        S = rng.integers(-1000, 1000, size=(n, 2)).astype(np.int64)
+        R[rng.random(n) < 0.6, 0] = 17
+        S[rng.random(n) < 0.5, 0] = 17
+        R[:, 1], S[:, 1] = np.arange(n), -np.arange(n)
+        return R, S
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("world,kind,cfg", [
+    (2, "uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 64}),
+    (3, "uniform", {"select": (0, 100, 0, 20000), "keys": (0, 0), "samples": 16}),
+    (2, "dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 32}),
+    (3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8}),
+])
+def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
+    R, S = make_tables(kind, 30_000)
+    mp.spawn(_worker, args=(world, free_port(), R, S, cfg, str(tmp_path)), nprocs=world, join=True)
+    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    sc1, sv1, sc2, sv2 = cfg["select"]
+    k1, k2 = cfg["keys"]
+    ref = oracle.join(oracle.select_sort(R, k1, sc1, sv1), oracle.select_sort(S, k2, sc2, sv2), k1, k2)
+    assert len(ref) > 0
+    np.testing.assert_array_equal(got, ref)
