@@ -102,7 +102,7 @@ struct ProfScope {
 
 extern "C" void smj_prof_enable(int on) { g_prof_on = on != 0; }
 
-extern "C" int smj_prof_report(char *buf, size_t buflen) {
+static std::string prof_json() {
     struct Agg { long launches = 0; double ms = 0, bytes = 0; };
     std::map<std::string, Agg> agg;
     for (auto &r : g_prof) {
@@ -113,10 +113,7 @@ extern "C" int smj_prof_report(char *buf, size_t buflen) {
         a.launches++;
         a.ms += ms;
         a.bytes += r.bytes;
-        g_event_pool.push_back(r.a);
-        g_event_pool.push_back(r.b);
     }
-    g_prof.clear();
     std::string out = "{";
     bool first = true;
     for (auto &kv : agg) {
@@ -126,10 +123,21 @@ extern "C" int smj_prof_report(char *buf, size_t buflen) {
         out += tmp;
         first = false;
     }
-    out += "}";
-    if (!buf || buflen == 0) return (int)out.size() + 1;
-    snprintf(buf, buflen, "%s", out.c_str());
-    return out.size() + 1 <= buflen ? SMJ_OK : (int)out.size() + 1;
+    return out + "}";
+}
+
+// Returns SMJ_OK after filling buf (and resetting the records), or the
+// buffer size needed (records kept) when buf is NULL / too small.
+extern "C" int smj_prof_report(char *buf, size_t buflen) {
+    const std::string out = prof_json();
+    if (!buf || buflen < out.size() + 1) return (int)out.size() + 1;
+    memcpy(buf, out.c_str(), out.size() + 1);
+    for (auto &r : g_prof) {
+        g_event_pool.push_back(r.a);
+        g_event_pool.push_back(r.b);
+    }
+    g_prof.clear();
+    return SMJ_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -139,7 +147,8 @@ namespace {
 struct DevScratch {
     int dev = -1;
     void *tmp = nullptr;  size_t tmp_bytes = 0;     // ping-pong rows
-    void *status = nullptr; size_t status_bytes = 0; // look-back words
+    void *status = nullptr; size_t status_bytes = 0; // pass chunk tables / join look-back words
+    uint32_t *segsum = nullptr;                      // kScanSegs * kRadix
     void *apart = nullptr; size_t apart_bytes = 0;   // merge-path partition
     uint32_t *hist = nullptr;                        // kNumPos * kRadix
     SortPlan *plan = nullptr;                        // device
@@ -173,6 +182,7 @@ int scratch(DevScratch **out) {
         HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
         HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
         HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 32));
+        HIP_TRY(hipMalloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
         HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 64, hipHostMallocDefault));
     }
@@ -195,6 +205,32 @@ int check_err(DevScratch *sc, int slot, hipStream_t s) {
     return err ? SMJ_ERR_TIMEOUT : SMJ_OK;
 }
 }  // namespace
+
+// One scatter pass (chunk_hist -> chunk_scan -> chunk_scatter).  rows_out:
+// rows the pass writes (for the profiler's algorithmic byte count).
+static int run_pass(DevScratch *sc, const PassSpec &ps, const uint32_t *base, Counters *ctr, const char *tag,
+                    int64_t rows_out, hipStream_t s) {
+    static const char *names[3][3] = {{"radix_hist", "radix_scan", "radix_scatter"},
+                                      {"select_hist", "select_scan", "select_scatter"},
+                                      {"partition_hist", "partition_scan", "partition_scatter"}};
+    (void)tag;
+    const int k = ps.kind == DIGIT_RADIX ? 0 : ps.kind == DIGIT_ZERO ? 1 : 2;
+    const double rowb = 8.0 * ps.cols;
+    const size_t tbytes = (size_t)pass_chunks(ps) * pass_radix(ps) * sizeof(uint32_t);
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, tbytes));
+    uint32_t *table = (uint32_t *)sc->status;
+    {
+        ProfScope p1(names[k][0], rowb * ps.nsrc, s);
+        HIP_TRY(launch_chunk_hist(ps, table, s));
+    }
+    {
+        ProfScope p2(names[k][1], 0, s);
+        HIP_TRY(launch_chunk_scan(ps, table, sc->segsum, base, s));
+    }
+    ProfScope p3(names[k][2], rowb * (ps.nsrc + rows_out), s);
+    HIP_TRY(launch_chunk_scatter(ps, table, ctr, s));
+    return SMJ_OK;
+}
 
 // ---------------------------------------------------------------------------
 // select + sort
@@ -227,20 +263,22 @@ static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int
     if (m == 0) return SMJ_OK;
     const int P = plan.npasses;
     if (P > 1) SMJ_TRY(grow(&sc->tmp, &sc->tmp_bytes, (size_t)m * cols * 8));
-    const int64_t tile_rows = sort_tile_rows(cols);
-    const size_t max_tiles = (size_t)((n + tile_rows - 1) / tile_rows);
-    SMJ_TRY(grow(&sc->status, &sc->status_bytes, max_tiles * kRadix * sizeof(uint32_t)));
     const T *src = in;
     for (int k = 0; k < P; k++) {
-        const int64_t nsrc = k == 0 ? n : m;
         T *dst = ((P - 1 - k) % 2 == 0) ? out : (T *)sc->tmp;
-        const size_t tiles = (size_t)((nsrc + tile_rows - 1) / tile_rows);
-        HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * kRadix * sizeof(uint32_t), s));
-        HIP_TRY(hipMemsetAsync(&sc->ctr[0], 0, 8, s));
-        ProfScope ps("radix_pass", rowb * (nsrc + m), s);
-        HIP_TRY(launch_radix_pass(src, nsrc, dst, cols, k == 0 ? use_select : 0, sel_col, sel_val, key_col,
-                                  key_base, plan.pos[k] * kRadixBits, sc->hist + plan.pos[k] * kRadix,
-                                  (uint32_t *)sc->status, &sc->ctr[0], s));
+        PassSpec ps{};
+        ps.src = src;
+        ps.nsrc = k == 0 ? n : m;
+        ps.dst = dst;
+        ps.cols = cols;
+        ps.use_select = k == 0 ? use_select : 0;
+        ps.sel_col = sel_col;
+        ps.key_col = key_col;
+        ps.sel_val = sel_val;
+        ps.kind = DIGIT_RADIX;
+        ps.key_base = key_base;
+        ps.shift = plan.pos[k] * kRadixBits;
+        SMJ_TRY(run_pass(sc, ps, sc->hist + plan.pos[k] * kRadix, &sc->ctr[0], "radix", m, s));
         src = dst;
     }
     *out_rows = m;
@@ -264,15 +302,17 @@ extern "C" int smj_dev_select(const T *in, int64_t n, int cols, int sel_col, T s
     if (!in || !out || in == out) return SMJ_ERR_INVALID;
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
-    const int64_t tile_rows = sort_tile_rows(cols);
-    const size_t tiles = (size_t)((n + tile_rows - 1) / tile_rows);
-    SMJ_TRY(grow(&sc->status, &sc->status_bytes, tiles * sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(&sc->ctr[1], 0, sizeof(Counters), s));
-    {
-        ProfScope ps("select_compact", 8.0 * cols * n, s);
-        HIP_TRY(launch_compact_pass(in, n, out, cols, sel_col, sel_val, (uint32_t *)sc->status, &sc->ctr[1], s));
-    }
+    PassSpec ps{};
+    ps.src = in;
+    ps.nsrc = n;
+    ps.dst = out;
+    ps.cols = cols;
+    ps.use_select = 1;
+    ps.sel_col = sel_col;
+    ps.sel_val = sel_val;
+    ps.kind = DIGIT_ZERO;
+    SMJ_TRY(run_pass(sc, ps, nullptr, &sc->ctr[1], "select", n, s));
     Counters c;
     HIP_TRY(hipMemcpyAsync(&c, &sc->ctr[1], sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -319,25 +359,36 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
     } else {
         if (!R || !S || !out) return SMJ_ERR_INVALID;
         const int64_t ntiles = (nr + ns + kJoinTile - 1) / kJoinTile;
-        SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(ntiles + 1) * sizeof(int64_t)));
-        SMJ_TRY(grow(&sc->status, &sc->status_bytes, (size_t)ntiles * sizeof(uint32_t)));
-        HIP_TRY(hipMemsetAsync(sc->status, 0, (size_t)ntiles * sizeof(uint32_t), s));
-        HIP_TRY(hipMemsetAsync(&sc->ctr[2], 0, sizeof(Counters), s));
+        const int tc = c1 + c2 - 1;
+        // apart (ntiles+1) | offs (ntiles) | counts (ntiles u32), slots (nr rows)
+        SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(3 * ntiles + 2) * sizeof(int64_t)));
+        SMJ_TRY(grow(&sc->tmp, &sc->tmp_bytes, (size_t)nr * tc * sizeof(int64_t)));
+        int64_t *apart = (int64_t *)sc->apart;
+        int64_t *offs = apart + ntiles + 1;
+        uint32_t *counts = (uint32_t *)(offs + ntiles);
+        int64_t *slots = (int64_t *)sc->tmp;
         {
             ProfScope ps("join_partition", 0, s);
-            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, (int64_t *)sc->apart, ntiles, s));
+            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, s));
         }
-        // algorithmic bytes: read R and S once; the output bytes are added by
-        // the caller-visible row count in smj_prof_report consumers (bench.py)
-        ProfScope ps("join_tiles", 8.0 * (c1 * nr + c2 * ns), s);
-        HIP_TRY(launch_join_tiles(R, nr, c1, key1, S, ns, c2, key2, (const int64_t *)sc->apart, ntiles, out,
-                                  d_out_rows, (uint32_t *)sc->status, &sc->ctr[2], s));
+        {
+            ProfScope ps("join_tiles", 8.0 * (c1 * nr + c2 * ns), s);
+            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out,
+                                d_out_rows, 0, s));
+        }
+        {
+            ProfScope ps("join_scan", 0, s);
+            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out,
+                                d_out_rows, 1, s));
+        }
+        ProfScope ps("join_compact", 0, s);
+        HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out, d_out_rows,
+                            2, s));
     }
     if (h_out_rows) {
         HIP_TRY(hipMemcpyAsync(sc->h_small, d_out_rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         *h_out_rows = sc->h_small[0];
-        if (nr && ns) SMJ_TRY(check_err(sc, 2, s));
     }
     return SMJ_OK;
 }
@@ -402,14 +453,20 @@ extern "C" int smj_dev_partition_scatter(const T *in, int64_t n, int cols, int u
     if (total >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     uint32_t *d_base = (uint32_t *)(sc->dcount);
     HIP_TRY(hipMemcpyAsync(d_base, h_base, sizeof(uint32_t) * (1 << kBucketBits), hipMemcpyHostToDevice, s));
-    const int64_t tile_rows = sort_tile_rows(cols);
-    const size_t tiles = (size_t)((n + tile_rows - 1) / tile_rows);
-    SMJ_TRY(grow(&sc->status, &sc->status_bytes, tiles * (1 << kBucketBits) * sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(sc->status, 0, tiles * (1 << kBucketBits) * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(&sc->ctr[3], 0, sizeof(Counters), s));
-    ProfScope ps("partition_scatter", 8.0 * cols * (n + total), s);
-    HIP_TRY(launch_bucket_pass(in, n, out, cols, use_select, sel_col, sel_val, key_col, spl, n_split, d_base,
-                               (uint32_t *)sc->status, &sc->ctr[3], s));
+    PassSpec ps{};
+    ps.src = in;
+    ps.nsrc = n;
+    ps.dst = out;
+    ps.cols = cols;
+    ps.use_select = use_select;
+    ps.sel_col = sel_col;
+    ps.key_col = key_col;
+    ps.sel_val = sel_val;
+    ps.kind = DIGIT_BUCKET;
+    ps.spl = spl;
+    ps.nspl = n_split;
+    SMJ_TRY(run_pass(sc, ps, d_base, &sc->ctr[3], "partition", total, s));
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_TRY(hipStreamSynchronize(s));
     return SMJ_OK;
@@ -476,6 +533,7 @@ extern "C" void smj_finalize(void) {
         hipFree(s.plan);
         hipFree(s.ctr);
         hipFree(s.dcount);
+        hipFree(s.segsum);
         hipHostFree(s.h_plan);
         hipHostFree(s.h_small);
     }

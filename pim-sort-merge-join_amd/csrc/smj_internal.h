@@ -28,6 +28,13 @@ constexpr int kMaxSplitters = (1 << kBucketBits) - 1;
 __host__ __device__ constexpr int sort_items(int cols) { return cols >= 8 ? 2 : (16 / cols); }
 __host__ __device__ constexpr int sort_tile_rows(int cols) { return sort_items(cols) * kSortThreads; }
 
+// A pass is processed in chunks of kChunkTiles consecutive tiles (one
+// workgroup per chunk in the scatter kernel); the [chunk][digit] count table
+// is scanned in kScanSegs segments.
+constexpr int kChunkTiles = 8;
+__host__ __device__ constexpr int64_t chunk_rows(int cols) { return (int64_t)kChunkTiles * sort_tile_rows(cols); }
+constexpr int kScanSegs = 16;
+
 // Join / merge geometry: one workgroup per merge-path tile of kJoinTile
 // merged elements (R-piece + S-piece).
 constexpr int kJoinThreads = 512;
@@ -64,27 +71,40 @@ hipError_t launch_hist_radix(const int64_t *src, int64_t n, int cols, int use_se
                              int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist,
                              hipStream_t s);
 hipError_t launch_plan(uint32_t *ghist, SortPlan *plan, hipStream_t s);
-hipError_t launch_radix_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols,
-                             int use_select, int sel_col, int64_t sel_val, int key_col,
-                             uint64_t key_base, int shift, const uint32_t *bin_base,
-                             uint32_t *status, Counters *ctr, hipStream_t s);
-hipError_t launch_compact_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols,
-                               int sel_col, int64_t sel_val, uint32_t *status, Counters *ctr,
-                               hipStream_t s);
+enum DigitKind { DIGIT_RADIX = 0, DIGIT_ZERO = 1, DIGIT_BUCKET = 2 };
+// One scatter pass: rows of src (with the WHERE predicate when use_select)
+// are moved stably into dst in the order of their digit.
+struct PassSpec {
+    const int64_t *src;
+    int64_t nsrc;
+    int64_t *dst;
+    int cols, use_select, sel_col, key_col;
+    int64_t sel_val;
+    DigitKind kind;
+    uint64_t key_base;    // DIGIT_RADIX: digit = ((key ^ 2^63) - key_base) >> shift
+    int shift;
+    const int64_t *spl;   // DIGIT_BUCKET: host array of nspl sorted splitters
+    int nspl;
+};
+int pass_radix(const PassSpec &ps);
+int64_t pass_chunks(const PassSpec &ps);
+// table: pass_chunks * pass_radix u32; segsum: kScanSegs * pass_radix u32;
+// base: pass_radix global exclusive digit starts (nullptr = 0).
+hipError_t launch_chunk_hist(const PassSpec &ps, uint32_t *table, hipStream_t s);
+hipError_t launch_chunk_scan(const PassSpec &ps, uint32_t *table, uint32_t *segsum, const uint32_t *base,
+                             hipStream_t s);
+hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *ctr, hipStream_t s);
 hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
                               int64_t sel_val, int key_col, const int64_t *spl, int nspl,
                               unsigned long long *gcount, long long *gminmax, hipStream_t s);
-hipError_t launch_bucket_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols,
-                              int use_select, int sel_col, int64_t sel_val, int key_col,
-                              const int64_t *spl, int nspl, const uint32_t *bin_base,
-                              uint32_t *status, Counters *ctr, hipStream_t s);
 hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
                                   int64_t nb, int cb, int kb, int64_t *apart, int64_t ntiles,
                                   hipStream_t s);
-hipError_t launch_join_tiles(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S,
-                             int64_t ns, int c2, int key2, const int64_t *apart, int64_t ntiles,
-                             int64_t *out, int64_t *out_rows, uint32_t *status, Counters *ctr,
-                             hipStream_t s);
+// join phases: 0 = tiles (slots + counts), 1 = scan counts (offs, *out_rows),
+// 2 = compact slots into out
+hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns, int c2,
+                       int key2, const int64_t *apart, int64_t ntiles, int64_t *slots, uint32_t *counts,
+                       int64_t *offs, int64_t *out, int64_t *out_rows, int phase, hipStream_t s);
 hipError_t launch_merge_tiles(const int64_t *a, int64_t na, const int64_t *b, int64_t nb, int cols,
                               int key_col, const int64_t *apart, int64_t ntiles, int64_t *out,
                               hipStream_t s);

@@ -19,6 +19,8 @@
 
 #include <math.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 namespace smj {
@@ -148,7 +150,15 @@ struct BucketDigit {  // multi-GPU range partition: #splitters < key
 };
 
 // ---------------------------------------------------------------------------
-// onesweep pass
+// one radix / bucket / compaction pass = chunk_hist -> chunk_scan -> chunk_scatter
+//
+// A pass is cut into chunks of kChunkTiles tiles.  chunk_hist counts each
+// chunk's digits (the WHERE predicate of pass 0 applied), chunk_scan turns
+// the [chunk][digit] table into exclusive global offsets in place, and
+// chunk_scatter moves every chunk with one workgroup that walks its tiles in
+// order, carrying running digit offsets in LDS.  No workgroup ever waits on
+// another: on MI355X a cross-XCD status round trip under full streaming load
+// costs microseconds, which made a decoupled look-back the bottleneck.
 // ---------------------------------------------------------------------------
 template <class DigitF>
 struct PassParams {
@@ -156,11 +166,10 @@ struct PassParams {
     int64_t *dst;
     int64_t nsrc;
     int64_t sel_val;
-    int use_select, sel_col, key_col, pad;
+    int use_select, sel_col, key_col, dbg;  // dbg: ablation bits (SMJ_DEBUG_PASS), 0 in production
     DigitF digit;
-    const uint32_t *bin_base;  // global exclusive digit prefix (nullptr = 0)
-    uint32_t *status;          // [tiles][RADIX] look-back words, zeroed
-    Counters *ctr;             // zeroed
+    uint32_t *table;  // [nchunks][RADIX]: counts (chunk_hist) -> exclusive offsets (chunk_scan)
+    Counters *ctr;
 };
 
 template <int COLS, int DBITS>
@@ -170,173 +179,290 @@ struct PassLds {
     static constexpr int ROW_BYTES = TILE * COLS * 8;
     static constexpr int CNT_BYTES = kSortWaves * RADIX * 4;
     static constexpr int A = ROW_BYTES > CNT_BYTES ? ROW_BYTES : CNT_BYTES;
-    static constexpr int OFF_BIN = A;
-    static constexpr int OFF_ADJ = OFF_BIN + ((RADIX * 4 + 15) / 16) * 16;
-    static constexpr int OFF_MISC = OFF_ADJ + ((RADIX * 8 + 15) / 16) * 16;
-    static constexpr int BYTES = OFF_MISC + 64;
+    static constexpr int R16 = ((RADIX * 4 + 15) / 16) * 16;
+    static constexpr int OFF_BIN = A;              // u32 tile-local digit starts
+    static constexpr int OFF_ADJ = OFF_BIN + R16;  // i32 global - local offset per digit
+    static constexpr int OFF_RUN = OFF_ADJ + R16;  // i32 running global offset per digit
+    static constexpr int OFF_MISC = OFF_RUN + R16;
+    static constexpr int BYTES = OFF_MISC + 128;
 };
 
-// One tile per workgroup; tiles are claimed in launch order through an
-// atomic counter so a tile's predecessors are always running or done when
-// it looks back (forward progress of the spin waits).
-template <int COLS, int DBITS, class DigitF>
-__global__ __launch_bounds__(kSortThreads, 4) void onesweep_kernel(const PassParams<DigitF> p) {
-    using L = PassLds<COLS, DBITS>;
-    constexpr int RADIX = L::RADIX;
-    constexpr int ITEMS = sort_items(COLS);
-    constexpr int TILE = L::TILE;
-    constexpr uint32_t MASK = RADIX - 1;
-    constexpr int BPT = RADIX >= kSortThreads ? RADIX / kSortThreads : 1;
-
-    __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
-    int64_t *s_rows = reinterpret_cast<int64_t *>(smem);          // after ranking
-    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(smem);        // during ranking
-    uint32_t *s_binstart = reinterpret_cast<uint32_t *>(smem + L::OFF_BIN);
-    int64_t *s_adj = reinterpret_cast<int64_t *>(smem + L::OFF_ADJ);
-    uint32_t *s_misc = reinterpret_cast<uint32_t *>(smem + L::OFF_MISC);
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_misc[0] = atomicAdd(&p.ctr->tile, 1u);
-    for (int i = tid; i < kSortWaves * RADIX; i += kSortThreads) s_wcnt[i] = 0;
-    __syncthreads();
-    const uint32_t tile = s_misc[0];
-
-    // ---- load: wave w owns rows [w*ITEMS*64, (w+1)*ITEMS*64) of the tile,
-    //      item i is 64 consecutive rows -> 64 x (8*COLS) B per instruction.
-    const int64_t row0 = (int64_t)tile * TILE + (int64_t)wave * (ITEMS * 64) + lane;
-    int64_t rows[ITEMS][COLS];
+template <int COLS, int ITEMS>
+__device__ __forceinline__ void load_tile(const int64_t *__restrict__ src, int64_t end, int64_t row0,
+                                          int64_t (&rows)[ITEMS][COLS]) {
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
         const int64_t r = row0 + it * 64;
-        if (r < p.nsrc) load_row<COLS>(p.src + r * COLS, rows[it]);
+        if (r < end) load_row<COLS>(src + r * COLS, rows[it]);
         else {
 #pragma unroll
             for (int c = 0; c < COLS; c++) rows[it][c] = 0;
         }
     }
-    uint32_t dig[ITEMS];
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const int64_t r = row0 + it * 64;
-        bool v = r < p.nsrc;
-        if (p.use_select) v = v && (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
-        dig[it] = v ? (p.digit(pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
-        vmask |= v ? (1u << it) : 0u;
-    }
+}
 
-    // ---- rank: stable within the tile.  Peers with the same digit in one
-    //      64-row item are found with DBITS ballots; per-wave running digit
-    //      counters in LDS order items within the wave.
-    uint32_t rank[ITEMS];
-    uint32_t *wc = s_wcnt + wave * RADIX;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const bool v = (vmask >> it) & 1u;
-        uint64_t peers = __ballot(v);
-#pragma unroll
-        for (int b = 0; b < DBITS; b++) {
-            const bool bit = (dig[it] >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        rank[it] = 0;
-        if (v) {
-            const uint32_t base = wc[dig[it]];
-            rank[it] = base + (uint32_t)__popcll(peers & lt_mask);
-            if ((peers >> lane) == 1ull) wc[dig[it]] = base + (uint32_t)__popcll(peers);
-        }
-    }
+// ---- chunk_hist: digit counts of every chunk ------------------------------
+template <int COLS, int DBITS, class DigitF>
+__global__ __launch_bounds__(512) void chunk_hist_kernel(const PassParams<DigitF> p) {
+    constexpr int RADIX = 1 << DBITS;
+    constexpr uint32_t MASK = RADIX - 1;
+    constexpr int64_t CH = chunk_rows(COLS);
+    constexpr int U = 8;
+    __shared__ uint32_t sh[RADIX];
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int i = tid; i < RADIX; i += 512) sh[i] = 0;
     __syncthreads();
-
-    // ---- per-digit totals and cross-wave exclusive prefix (in place)
-    uint32_t tot[BPT];
-    uint32_t tsum = 0;
+    const int64_t begin = (int64_t)blockIdx.x * CH;
+    const int64_t end = min(begin + CH, p.nsrc);
+    for (int64_t r0 = begin; r0 < end; r0 += 512 * U) {
+        int64_t key[U], sv[U];
 #pragma unroll
-    for (int j = 0; j < BPT; j++) {
-        const int d = tid * BPT + j;
-        uint32_t run = 0;
-        if (d < RADIX) {
+        for (int u = 0; u < U; u++) {
+            const int64_t r = r0 + u * 512 + tid;
+            key[u] = r < end ? p.src[r * COLS + p.key_col] : 0;
+            sv[u] = (r < end && p.use_select) ? p.src[r * COLS + p.sel_col] : 0;
+        }
 #pragma unroll
-            for (int w = 0; w < kSortWaves; w++) {
-                const uint32_t c = s_wcnt[w * RADIX + d];
-                s_wcnt[w * RADIX + d] = run;
-                run += c;
+        for (int u = 0; u < U; u++) {
+            const int64_t r = r0 + u * 512 + tid;
+            const bool ok = r < end && (!p.use_select || sv[u] > p.sel_val);
+            const uint64_t act = __ballot(ok);
+            if (act == 0) continue;
+            const uint32_t d = p.digit(key[u]) & MASK;
+            const int leader = __ffsll((unsigned long long)act) - 1;
+            const uint32_t dl = __shfl(d, leader, 64);
+            if (__ballot(ok && d == dl) == act) {
+                if (lane == leader) atomicAdd(&sh[dl], (uint32_t)__popcll(act));
+            } else if (ok) {
+                atomicAdd(&sh[d], 1u);
             }
         }
-        tot[j] = run;
-        tsum += run;
     }
-    // publish this tile's digit counts at once (unblocks successors)
-    uint32_t *st = p.status + (size_t)tile * RADIX;
+    __syncthreads();
+    for (int i = tid; i < RADIX; i += 512) p.table[(size_t)blockIdx.x * RADIX + i] = sh[i];
+}
+
+// ---- chunk_scan: table[c][d] <- base[d] + sum_{c' < c} table[c'][d] ---------
+// grid (ceil(radix/64), kScanSegs) x 256 threads; lane = digit, the chunks of
+// a segment are split into 4 contiguous runs, one per wave.
+__device__ __forceinline__ void scan_seg_range(int64_t nchunks, int64_t &c0, int64_t &c1) {
+    const int64_t L = (nchunks + kScanSegs - 1) / kScanSegs;
+    c0 = min((int64_t)blockIdx.y * L, nchunks);
+    c1 = min(c0 + L, nchunks);
+    const int64_t L4 = (c1 - c0 + 3) / 4;
+    const int w = threadIdx.x >> 6;
+    const int64_t s0 = min(c0 + w * L4, c1);
+    c1 = min(s0 + L4, c1);
+    c0 = s0;
+}
+
+__global__ __launch_bounds__(256) void chunk_scan_seg_kernel(const uint32_t *__restrict__ table, int64_t nchunks,
+                                                             int radix, uint32_t *__restrict__ segsum) {
+    __shared__ uint32_t part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int bin = blockIdx.x * 64 + lane;
+    int64_t c0, c1;
+    scan_seg_range(nchunks, c0, c1);
+    uint32_t sum = 0;
+    if (bin < radix) {
+#pragma unroll 8
+        for (int64_t c = c0; c < c1; c++) sum += table[c * radix + bin];
+    }
+    part[w][lane] = sum;
+    __syncthreads();
+    if (w == 0 && bin < radix)
+        segsum[(size_t)blockIdx.y * radix + bin] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+}
+
+__global__ __launch_bounds__(256) void chunk_scan_apply_kernel(uint32_t *__restrict__ table, int64_t nchunks,
+                                                               int radix, const uint32_t *__restrict__ segsum,
+                                                               const uint32_t *__restrict__ base) {
+    __shared__ uint32_t part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int bin = blockIdx.x * 64 + lane;
+    int64_t c0, c1;
+    scan_seg_range(nchunks, c0, c1);
+    uint32_t sum = 0;
+    if (bin < radix) {
+#pragma unroll 8
+        for (int64_t c = c0; c < c1; c++) sum += table[c * radix + bin];
+    }
+    part[w][lane] = sum;
+    __syncthreads();
+    if (bin >= radix) return;
+    uint32_t off = base ? base[bin] : 0u;
+    for (int s = 0; s < (int)blockIdx.y; s++) off += segsum[(size_t)s * radix + bin];
+    for (int v = 0; v < w; v++) off += part[v][lane];
+#pragma unroll 8
+    for (int64_t c = c0; c < c1; c++) {
+        const uint32_t x = table[c * radix + bin];
+        table[c * radix + bin] = off;
+        off += x;
+    }
+}
+
+// ---- chunk_scatter: stable scatter of one chunk per workgroup ---------------
+// Tiles of the chunk are taken in order; the next tile's rows are loaded into
+// registers while the current one is ranked and scattered.  Per tile:
+//   rank     stable digit ranks: DBITS ballots per 64-row item find the lanes
+//            with the same digit; per-wave running counters in LDS order the
+//            items of a wave; a cross-wave prefix orders the waves;
+//   stage    rows are written to LDS in digit order (block scan of the digit
+//            totals gives each digit's local start);
+//   scatter  consecutive LDS rows of one digit leave as one contiguous run at
+//            the digit's running global offset.
+template <int COLS, int DBITS, class DigitF>
+__global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const PassParams<DigitF> p) {
+    using L = PassLds<COLS, DBITS>;
+    constexpr int RADIX = L::RADIX;
+    constexpr int ITEMS = sort_items(COLS);
+    constexpr int TILE = L::TILE;
+    constexpr int64_t CH = chunk_rows(COLS);
+    constexpr uint32_t MASK = RADIX - 1;
+    constexpr int BPT = RADIX > kSortThreads ? RADIX / kSortThreads : 1;  // digits d = tid + j*512
+
+    __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
+    int64_t *s_rows = reinterpret_cast<int64_t *>(smem);          // staging tile (after ranking)
+    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(smem);        // [wave][digit] counters (ranking)
+    uint32_t *s_binstart = reinterpret_cast<uint32_t *>(smem + L::OFF_BIN);
+    int32_t *s_adj = reinterpret_cast<int32_t *>(smem + L::OFF_ADJ);
+    int32_t *s_run = reinterpret_cast<int32_t *>(smem + L::OFF_RUN);
+    uint32_t *s_misc = reinterpret_cast<uint32_t *>(smem + L::OFF_MISC);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t begin = (int64_t)blockIdx.x * CH;
+    const int64_t end = min(begin + CH, p.nsrc);
+    const int64_t lane_row = (int64_t)wave * (ITEMS * 64) + lane;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    uint32_t *wc = s_wcnt + wave * RADIX;
+
 #pragma unroll
     for (int j = 0; j < BPT; j++) {
-        const int d = tid * BPT + j;
-        if (d < RADIX) st_status(st + d, (tile == 0 ? kFlagInc : kFlagAgg) | tot[j]);
+        const int d = tid + j * kSortThreads;
+        if (d < RADIX) s_run[d] = (int32_t)p.table[(size_t)blockIdx.x * RADIX + d];
     }
-    // block exclusive scan of digit totals -> tile-local digit starts
-    const uint32_t incl = wave_incl_scan(tsum, lane);
-    if (lane == 63) s_misc[4 + wave] = incl;
-    __syncthreads();
-    uint32_t woff = 0, tile_total = 0;
+    int64_t rows[ITEMS][COLS];
+    load_tile<COLS, ITEMS>(p.src, end, begin + lane_row, rows);
+    uint32_t chunk_total = 0;
+
+    for (int64_t tile0 = begin;;) {
+        for (int i = tid; i < kSortWaves * RADIX; i += kSortThreads) s_wcnt[i] = 0;
+        __syncthreads();  // B1 (also publishes s_run on the first tile)
+
+        // ---- digits (select predicate fused into pass 0)
+        const int64_t row0 = tile0 + lane_row;
+        uint32_t dig[ITEMS];
+        uint32_t vmask = 0;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) {
-        const uint32_t x = s_misc[4 + w];
-        woff += (w < wave) ? x : 0u;
-        tile_total += x;
-    }
-    {
-        uint32_t run = woff + incl - tsum;
+        for (int it = 0; it < ITEMS; it++) {
+            bool v = row0 + it * 64 < end;
+            if (p.use_select) v = v && (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+            dig[it] = v ? (p.digit(pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
+            vmask |= v ? (1u << it) : 0u;
+        }
+        // ---- stable rank within the tile; dig[it] becomes (rank << 16) | digit
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const bool v = (vmask >> it) & 1u;
+            uint64_t peers = __ballot(v);
+#pragma unroll
+            for (int b = 0; b < DBITS; b++) {
+                const bool bit = (dig[it] >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            if (v) {
+                const uint32_t base = wc[dig[it]];
+                const uint32_t rank = base + (uint32_t)__popcll(peers & lt_mask);
+                if ((peers >> lane) == 1ull) wc[dig[it]] = base + (uint32_t)__popcll(peers);
+                dig[it] |= rank << 16;
+            }
+        }
+        __syncthreads();  // B2
+
+        // ---- per-digit totals, cross-wave exclusive prefix in place
+        uint32_t tot[BPT], incl[BPT];
 #pragma unroll
         for (int j = 0; j < BPT; j++) {
-            const int d = tid * BPT + j;
-            if (d < RADIX) s_binstart[d] = run;
-            run += tot[j];
-        }
-    }
-    __syncthreads();
-
-    // ---- tile-local destination of every row
-    uint32_t pos[ITEMS];
+            const int d = tid + j * kSortThreads;
+            uint32_t run = 0;
+            if (d < RADIX) {
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++)
-        pos[it] = ((vmask >> it) & 1u) ? s_binstart[dig[it]] + wc[dig[it]] + rank[it] : 0u;
-    __syncthreads();  // counters dead from here: the region becomes the row tile
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++)
-        if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)pos[it] * COLS, rows[it]);
-
-    // ---- decoupled look-back: global start of each digit's run of this tile
-#pragma unroll
-    for (int j = 0; j < BPT; j++) {
-        const int d = tid * BPT + j;
-        if (d < RADIX) {
-            uint32_t excl = 0;
-            if (tile > 0) {
-                int64_t t = (int64_t)tile - 1;
-                while (true) {
-                    const uint32_t w = spin_status(p.status + (size_t)t * RADIX + d, &p.ctr->err);
-                    excl += w & kValueMask;
-                    if ((w & kFlagInc) || t == 0) break;
-                    --t;
+                for (int w = 0; w < kSortWaves; w++) {
+                    const uint32_t c = s_wcnt[w * RADIX + d];
+                    s_wcnt[w * RADIX + d] = run;
+                    run += c;
                 }
-                st_status(st + d, kFlagInc | (excl + tot[j]));
             }
-            const int64_t gbase = p.bin_base ? (int64_t)p.bin_base[d] : 0;
-            s_adj[d] = gbase + (int64_t)excl - (int64_t)s_binstart[d];
+            tot[j] = run;
+            incl[j] = wave_incl_scan(run, lane);
+            if (lane == 63) s_misc[4 + j * kSortWaves + wave] = incl[j];
         }
-    }
-    if (tid == 0 && tile_total) atomicAdd(&p.ctr->count, tile_total);
-    __syncthreads();
+        __syncthreads();  // B3
+        // ---- block exclusive scan of the totals in digit order -> local starts
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < BPT; j++) {
+            uint32_t before = 0, all = 0;
+#pragma unroll
+            for (int w = 0; w < kSortWaves; w++) {
+                const uint32_t x = s_misc[4 + j * kSortWaves + w];
+                before += (w < wave) ? x : 0u;
+                all += x;
+            }
+            const int d = tid + j * kSortThreads;
+            if (d < RADIX) s_binstart[d] = run + before + incl[j] - tot[j];
+            run += all;
+        }
+        const uint32_t tile_total = run;
+        chunk_total += tile_total;
+        __syncthreads();  // B4
 
-    // ---- scatter: consecutive LDS rows of one digit -> consecutive HBM rows
-    for (uint32_t i = tid; i < tile_total; i += kSortThreads) {
-        int64_t r[COLS];
-        load_row<COLS>(s_rows + (size_t)i * COLS, r);
-        const uint32_t d = p.digit(pick<COLS>(r, p.key_col)) & MASK;
-        store_row<COLS>(p.dst + (s_adj[d] + (int64_t)i) * COLS, r);
+        // ---- tile-local destinations; prefetch the next tile behind them
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {  // dig[it] becomes the LDS slot
+            const uint32_t d = dig[it] & 0xffffu;
+            dig[it] = ((vmask >> it) & 1u) ? s_binstart[d] + wc[d] + (dig[it] >> 16) : 0u;
+        }
+        const int64_t next0 = tile0 + TILE;
+        int64_t nrows[ITEMS][COLS];
+        if (next0 < end) load_tile<COLS, ITEMS>(p.src, end, next0 + lane_row, nrows);
+        __syncthreads();  // B5: counters dead, the region becomes the staging tile
+        if (!(p.dbg & 4)) {
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+        }
+#pragma unroll
+        for (int j = 0; j < BPT; j++) {
+            const int d = tid + j * kSortThreads;
+            if (d < RADIX) {
+                const int32_t r = s_run[d];
+                s_adj[d] = r - (int32_t)s_binstart[d];
+                s_run[d] = r + (int32_t)tot[j];
+            }
+        }
+        __syncthreads();  // B6
+
+        // ---- scatter: consecutive LDS rows of one digit -> consecutive HBM rows
+        if (!(p.dbg & 4)) {
+            for (uint32_t i = tid; i < tile_total; i += kSortThreads) {
+                int64_t r[COLS];
+                load_row<COLS>(s_rows + (size_t)i * COLS, r);
+                const uint32_t d = p.digit(pick<COLS>(r, p.key_col)) & MASK;
+                if (!(p.dbg & 2)) store_row<COLS>(p.dst + ((int64_t)s_adj[d] + (int64_t)i) * COLS, r);
+                else if (r[0] == 0x7fffffffffffffffll && d == 12345u) p.dst[0] = r[COLS - 1];  // keep live
+            }
+        }
+        if (next0 >= end) break;
+        __syncthreads();  // B0: staging tile read before it is zeroed again
+        tile0 = next0;
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+#pragma unroll
+            for (int c = 0; c < COLS; c++) rows[it][c] = nrows[it][c];
     }
+    if (tid == 0 && chunk_total) atomicAdd(&p.ctr->count, chunk_total);
 }
 
 // ---------------------------------------------------------------------------
@@ -519,41 +645,44 @@ __global__ void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na
 }
 
 // ---------------------------------------------------------------------------
-// join: one merge-path tile per workgroup.  For every R row i (key k):
-//   lbS(k) = b0 + #{S-piece keys < k}      (merge path: S[<b0] < k <= S[>=b1])
-//   lbR(k) = first R row with key k        (local, or galloped for the tile's first key)
+// join: one merge-path tile per workgroup (kJoinTile merged elements of R
+// and S, R first on equal keys).  For an R row i with key k:
+//   lbS(k) = first S row with key k   (merge path: S[<b0] < k <= S[>=b1], so
+//            lbS = b0 + #S-piece rows merged before i)
+//   lbR(k) = first R row with key k   (local, or galloped for the tile's first key)
 //   occ = i - lbR(k);  partner p = lbS(k) + occ;  match iff S[p].key == k
-// which is exactly cpu_app.c's zip (:211-227): the occ-th R occurrence of k
-// pairs with the occ-th S occurrence.  Output rows in R order; tile offsets
-// by single-word decoupled look-back.
+// i.e. exactly cpu_app.c's zip (:211-227): the occ-th R occurrence of k pairs
+// with the occ-th S occurrence.  Every thread walks kJoinPer consecutive
+// merged elements.  Matches of tile t are written, in R order, to rows
+// [a0_t, a0_t + cnt_t) of a slot buffer (a tile holds at most a1_t - a0_t
+// matches) and counted; join_scan + join_compact then pack the slots.  No
+// workgroup waits on another.
 // ---------------------------------------------------------------------------
 struct JoinParams {
     const int64_t *R;
     const int64_t *S;
     const int64_t *apart;
-    int64_t *out;
-    int64_t *out_rows;
-    uint32_t *status;
-    Counters *ctr;
+    int64_t *slots;      // [nr][c1 + c2 - 1]
+    uint32_t *counts;    // [ntiles]
     int64_t nr, ns, ntiles;
     int c1, key1, c2, key2;
 };
 
+constexpr int kJoinStageCols = 3;  // output rows up to 3 columns are staged in LDS
+
 __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParams p) {
     __shared__ int64_t s_keys[kJoinTile];
+    __shared__ int64_t s_out[(kJoinTile / 2) * kJoinStageCols];
     __shared__ uint32_t s_scan[kJoinThreads / 64];
     __shared__ int64_t s_lbr0;
-    __shared__ uint32_t s_tile, s_excl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(&p.ctr->tile, 1u);
-    __syncthreads();
-    const int64_t tile = s_tile;
+    const int64_t tile = blockIdx.x;
     const int64_t L = p.nr + p.ns;
     const int64_t d0 = tile * kJoinTile, d1 = min(d0 + kJoinTile, L);
     const int64_t a0 = p.apart[tile], a1 = p.apart[tile + 1];
     const int64_t b0 = d0 - a0, b1 = d1 - a1;
-    const int nR = (int)(a1 - a0), nS = (int)(b1 - b0);
-    for (int j = tid; j < nR + nS; j += kJoinThreads)
+    const int nR = (int)(a1 - a0), nS = (int)(b1 - b0), nM = nR + nS;
+    for (int j = tid; j < nM; j += kJoinThreads)
         s_keys[j] = j < nR ? p.R[(a0 + j) * p.c1 + p.key1] : p.S[(b0 + j - nR) * p.c2 + p.key2];
     if (tid == 0 && nR > 0) {
         // first R row carrying R[a0].key: gallop backwards, then bisect
@@ -575,35 +704,63 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
             }
             first = l;
         }
-        const int64_t hi = first;
-        s_lbr0 = hi;
+        s_lbr0 = first;
     }
     __syncthreads();
 
+    const int64_t *rk = s_keys;
     const int64_t *sk = s_keys + nR;
-    uint32_t mmask = 0;
-    int64_t part[kJoinPer];
-    uint32_t cnt = 0;
+    // this thread's merged elements [m0, m1): merge-path split inside the tile
+    const int m0 = min(tid * kJoinPer, nM), m1 = min(m0 + kJoinPer, nM);
+    int ai, bi;
+    {
+        int lo = max(0, m0 - nS), hi = min(m0, nR);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (rk[mid] <= sk[m0 - 1 - mid]) lo = mid + 1; else hi = mid;
+        }
+        ai = lo;
+        bi = m0 - lo;
+    }
+    int64_t lbr = 0, prev = 0;
+    bool have_prev = false;
+    uint32_t mmask = 0, cnt = 0;
+    int32_t mrow[kJoinPer];   // R row (tile-local) of the q-th match
+    int64_t mpart[kJoinPer];  // its S partner
 #pragma unroll
     for (int q = 0; q < kJoinPer; q++) {
-        const int j = tid * kJoinPer + q;
-        part[q] = 0;
-        if (j < nR) {
-            const int64_t k = s_keys[j];
-            const int lb_loc = lds_lower_bound(s_keys, j, k);
-            const int64_t lbr = lb_loc == 0 ? s_lbr0 : a0 + lb_loc;
-            const int64_t lbs = b0 + lds_lower_bound(sk, nS, k);
-            const int64_t pidx = lbs + (a0 + j - lbr);
-            if (pidx < p.ns) {
-                const int64_t skey = pidx < b1 ? sk[pidx - b0] : p.S[pidx * p.c2 + p.key2];
-                if (skey == k) {
-                    mmask |= 1u << q;
-                    part[q] = pidx;
-                    cnt++;
+        mrow[q] = 0;
+        mpart[q] = 0;
+        if (m0 + q < m1) {
+            const bool takeR = ai < nR && (bi >= nS || rk[ai] <= sk[bi]);
+            if (takeR) {
+                const int64_t k = rk[ai];
+                if (!have_prev || k != prev) {
+                    if (have_prev) {
+                        lbr = a0 + ai;  // a new run starts here
+                    } else {        // first R row of this thread: search the run start
+                        const int lb = lds_lower_bound(rk, ai, k);
+                        lbr = lb == 0 ? s_lbr0 : a0 + lb;
+                    }
+                    prev = k;
+                    have_prev = true;
                 }
+                const int64_t pidx = b0 + bi + (a0 + ai - lbr);
+                if (pidx < p.ns) {
+                    const int64_t skey = pidx < b1 ? sk[pidx - b0] : p.S[pidx * p.c2 + p.key2];
+                    if (skey == k) {
+                        mrow[q] = ai;
+                        mpart[q] = pidx;
+                        mmask |= 1u << q;
+                    }
+                }
+                ai++;
+            } else {
+                bi++;
             }
         }
     }
+    cnt = __popc(mmask);
     // block exclusive scan of match counts
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (lane == 63) s_scan[wave] = incl;
@@ -616,41 +773,77 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
         total += x;
     }
     off += incl - cnt;
-    if (tid == 0) {
-        uint32_t excl = 0;
-        if (tile == 0) {
-            st_status(p.status, kFlagInc | total);
-        } else {
-            st_status(p.status + tile, kFlagAgg | total);
-            int64_t t = tile - 1;
-            while (true) {
-                const uint32_t w = spin_status(p.status + t, &p.ctr->err);
-                excl += w & kValueMask;
-                if ((w & kFlagInc) || t == 0) break;
-                --t;
-            }
-            st_status(p.status + tile, kFlagInc | (excl + total));
-        }
-        s_excl = excl;
-        if (tile == p.ntiles - 1) *p.out_rows = (int64_t)excl + total;
-    }
-    __syncthreads();
-    if (!mmask) return;
+    if (tid == 0) p.counts[tile] = total;
     const int tc = p.c1 + p.c2 - 1;
-    int64_t o = (int64_t)s_excl + off;
+    if (tc <= kJoinStageCols) {
+        // stage the tile's output rows in LDS, then one coalesced copy
 #pragma unroll
-    for (int q = 0; q < kJoinPer; q++) {
-        if ((mmask >> q) & 1u) {
-            const int64_t i = a0 + tid * kJoinPer + q;
-            int64_t *dst = p.out + o * tc;
-            const int64_t *rr = p.R + i * p.c1;
-            const int64_t *ss = p.S + part[q] * p.c2;
-            for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
-            for (int c = 0, k = p.c1; c < p.c2; c++)
-                if (c != p.key2) dst[k++] = ss[c];
-            ++o;
+        for (int q = 0; q < kJoinPer; q++) {
+            if ((mmask >> q) & 1u) {
+                int64_t *dst = s_out + (size_t)(off + __popc(mmask & ((1u << q) - 1u))) * tc;
+                const int64_t *rr = p.R + (a0 + mrow[q]) * p.c1;
+                const int64_t *ss = p.S + mpart[q] * p.c2;
+                for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
+                for (int c = 0, k = p.c1; c < p.c2; c++)
+                    if (c != p.key2) dst[k++] = ss[c];
+            }
+        }
+        __syncthreads();
+        int64_t *out = p.slots + a0 * tc;
+        for (uint32_t i = tid; i < total * tc; i += kJoinThreads) out[i] = s_out[i];
+    } else {
+#pragma unroll
+        for (int q = 0; q < kJoinPer; q++) {
+            if ((mmask >> q) & 1u) {
+                int64_t *dst = p.slots + (a0 + off + __popc(mmask & ((1u << q) - 1u))) * tc;
+                const int64_t *rr = p.R + (a0 + mrow[q]) * p.c1;
+                const int64_t *ss = p.S + mpart[q] * p.c2;
+                for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
+                for (int c = 0, k = p.c1; c < p.c2; c++)
+                    if (c != p.key2) dst[k++] = ss[c];
+            }
         }
     }
+}
+
+// exclusive scan of the per-tile match counts (one workgroup); writes the
+// joined row count to *out_rows
+__global__ __launch_bounds__(1024) void join_scan_kernel(const uint32_t *__restrict__ counts, int64_t ntiles,
+                                                         int64_t *__restrict__ offs, int64_t *out_rows) {
+    __shared__ int64_t s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t c0 = min((int64_t)tid * per, ntiles), c1 = min(c0 + per, ntiles);
+    int64_t sum = 0;
+    for (int64_t c = c0; c < c1; c++) sum += counts[c];
+    int64_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int64_t run = incl - sum;
+    for (int w = 0; w < wave; w++) run += s_w[w];
+    for (int64_t c = c0; c < c1; c++) {
+        offs[c] = run;
+        run += counts[c];
+    }
+    if (tid == 1023) *out_rows = run;
+}
+
+// pack the slots: tile t's cnt_t rows at slot row a0_t -> output row offs_t
+__global__ __launch_bounds__(256) void join_compact_kernel(const int64_t *__restrict__ slots,
+                                                           const int64_t *__restrict__ apart,
+                                                           const uint32_t *__restrict__ counts,
+                                                           const int64_t *__restrict__ offs, int tc,
+                                                           int64_t *__restrict__ out) {
+    const int64_t t = blockIdx.x;
+    const int64_t n = (int64_t)counts[t] * tc;
+    const int64_t *src = slots + apart[t] * tc;
+    int64_t *dst = out + offs[t] * tc;
+    for (int64_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -754,6 +947,21 @@ __global__ void gen_zipf_kernel(int64_t *out, int64_t row0, int64_t rows, uint64
 
 static inline unsigned blocks_for(int64_t n, int64_t per) { return (unsigned)((n + per - 1) / per); }
 
+// Ablation switches for profiling builds of the bench tools only (unset in
+// production): SMJ_DEBUG_PASS bit0 = no look-back, bit1 = no HBM stores,
+// bit2 = no LDS staging / scatter; SMJ_DEBUG_JOIN bit0 = no look-back.
+static int debug_bits(const char *name) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : 0;
+}
+
+static BucketDigit make_bucket(const int64_t *spl, int nspl) {
+    BucketDigit d{};
+    for (int i = 0; i < kMaxSplitters; i++) d.spl[i] = i < nspl ? spl[i] : INT64_MAX;
+    d.nspl = nspl;
+    return d;
+}
+
 hipError_t launch_hist_radix(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
                              int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist,
                              hipStream_t s) {
@@ -768,33 +976,6 @@ hipError_t launch_plan(uint32_t *ghist, SortPlan *plan, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_radix_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int use_select,
-                             int sel_col, int64_t sel_val, int key_col, uint64_t key_base, int shift,
-                             const uint32_t *bin_base, uint32_t *status, Counters *ctr, hipStream_t s) {
-    PassParams<RadixDigit> p{src, dst, nsrc, sel_val, use_select, sel_col, key_col, 0,
-                             RadixDigit{key_base, shift}, bin_base, status, ctr};
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, kRadixBits, RadixDigit>),
-                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
-                                             dim3(kSortThreads), 0, s, p));
-    return hipGetLastError();
-}
-
-hipError_t launch_compact_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int sel_col,
-                               int64_t sel_val, uint32_t *status, Counters *ctr, hipStream_t s) {
-    PassParams<ZeroDigit> p{src, dst, nsrc, sel_val, 1, sel_col, 0, 0, ZeroDigit{}, nullptr, status, ctr};
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, 0, ZeroDigit>),
-                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
-                                             dim3(kSortThreads), 0, s, p));
-    return hipGetLastError();
-}
-
-static BucketDigit make_bucket(const int64_t *spl, int nspl) {
-    BucketDigit d{};
-    for (int i = 0; i < kMaxSplitters; i++) d.spl[i] = i < nspl ? spl[i] : INT64_MAX;
-    d.nspl = nspl;
-    return d;
-}
-
 hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
                               int64_t sel_val, int key_col, const int64_t *spl, int nspl,
                               unsigned long long *gcount, long long *gminmax, hipStream_t s) {
@@ -805,14 +986,53 @@ hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_s
     return hipGetLastError();
 }
 
-hipError_t launch_bucket_pass(const int64_t *src, int64_t nsrc, int64_t *dst, int cols, int use_select,
-                              int sel_col, int64_t sel_val, int key_col, const int64_t *spl, int nspl,
-                              const uint32_t *bin_base, uint32_t *status, Counters *ctr, hipStream_t s) {
-    PassParams<BucketDigit> p{src, dst, nsrc, sel_val, use_select, sel_col, key_col, 0,
-                              make_bucket(spl, nspl), bin_base, status, ctr};
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((onesweep_kernel<C, kBucketBits, BucketDigit>),
-                                             dim3(blocks_for(nsrc, sort_tile_rows(C))),
-                                             dim3(kSortThreads), 0, s, p));
+int pass_radix(const PassSpec &ps) {
+    return ps.kind == DIGIT_RADIX ? kRadix : ps.kind == DIGIT_BUCKET ? (1 << kBucketBits) : 1;
+}
+
+int64_t pass_chunks(const PassSpec &ps) { return (ps.nsrc + chunk_rows(ps.cols) - 1) / chunk_rows(ps.cols); }
+
+// dispatch a pass kernel over (cols, digit kind)
+#define SMJ_PASS_DISPATCH(KERNEL, BLOCK)                                                                   \
+    do {                                                                                                   \
+        const unsigned grid = (unsigned)pass_chunks(ps);                                                   \
+        const int dbg = debug_bits("SMJ_DEBUG_PASS");                                                      \
+        if (ps.kind == DIGIT_RADIX) {                                                                      \
+            PassParams<RadixDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,        \
+                                     ps.key_col, dbg, RadixDigit{ps.key_base, ps.shift}, table, ctr};      \
+            SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, kRadixBits, RadixDigit>), dim3(grid),    \
+                                                        dim3(BLOCK), 0, s, p));                           \
+        } else if (ps.kind == DIGIT_BUCKET) {                                                              \
+            PassParams<BucketDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,       \
+                                      ps.key_col, dbg, make_bucket(ps.spl, ps.nspl), table, ctr};          \
+            SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, kBucketBits, BucketDigit>), dim3(grid),  \
+                                                        dim3(BLOCK), 0, s, p));                           \
+        } else {                                                                                           \
+            PassParams<ZeroDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,         \
+                                    ps.key_col, dbg, ZeroDigit{}, table, ctr};                             \
+            SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, 0, ZeroDigit>), dim3(grid), dim3(BLOCK), \
+                                                        0, s, p));                                         \
+        }                                                                                                  \
+    } while (0)
+
+hipError_t launch_chunk_hist(const PassSpec &ps, uint32_t *table, hipStream_t s) {
+    Counters *ctr = nullptr;
+    SMJ_PASS_DISPATCH(chunk_hist_kernel, 512);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_scan(const PassSpec &ps, uint32_t *table, uint32_t *segsum, const uint32_t *base,
+                             hipStream_t s) {
+    const int radix = pass_radix(ps);
+    const int64_t nch = pass_chunks(ps);
+    const dim3 grid((radix + 63) / 64, kScanSegs);
+    hipLaunchKernelGGL(chunk_scan_seg_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum);
+    hipLaunchKernelGGL(chunk_scan_apply_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *ctr, hipStream_t s) {
+    SMJ_PASS_DISPATCH(chunk_scatter_kernel, kSortThreads);
     return hipGetLastError();
 }
 
@@ -824,11 +1044,18 @@ hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, 
     return hipGetLastError();
 }
 
-hipError_t launch_join_tiles(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns,
-                             int c2, int key2, const int64_t *apart, int64_t ntiles, int64_t *out,
-                             int64_t *out_rows, uint32_t *status, Counters *ctr, hipStream_t s) {
-    JoinParams p{R, S, apart, out, out_rows, status, ctr, nr, ns, ntiles, c1, key1, c2, key2};
-    hipLaunchKernelGGL(join_tile_kernel, dim3((unsigned)ntiles), dim3(kJoinThreads), 0, s, p);
+hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns, int c2,
+                       int key2, const int64_t *apart, int64_t ntiles, int64_t *slots, uint32_t *counts,
+                       int64_t *offs, int64_t *out, int64_t *out_rows, int phase, hipStream_t s) {
+    if (phase == 0) {
+        JoinParams p{R, S, apart, slots, counts, nr, ns, ntiles, c1, key1, c2, key2};
+        hipLaunchKernelGGL(join_tile_kernel, dim3((unsigned)ntiles), dim3(kJoinThreads), 0, s, p);
+    } else if (phase == 1) {
+        hipLaunchKernelGGL(join_scan_kernel, dim3(1), dim3(1024), 0, s, counts, ntiles, offs, out_rows);
+    } else {
+        hipLaunchKernelGGL(join_compact_kernel, dim3((unsigned)ntiles), dim3(256), 0, s, slots, apart, counts, offs,
+                           c1 + c2 - 1, out);
+    }
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ import threading
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libsmj_hip.so")
+LIB_PATH = os.environ.get("SMJ_LIB") or os.path.join(PKG_DIR, "lib", "libsmj_hip.so")
 CSV_LIB_PATH = os.path.join(PKG_DIR, "lib", "libsmj_csv.so")
 APP_PATH = os.path.join(PKG_DIR, "bin", "smj_app")
 
