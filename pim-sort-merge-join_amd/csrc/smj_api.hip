@@ -102,6 +102,13 @@ struct ProfScope {
 
 extern "C" void smj_prof_enable(int on) { g_prof_on = on != 0; }
 
+// Diagnostic only (not part of smj.h): chunk_scatter phase cycles collected
+// under SMJ_DEBUG_PASS bit 3; out[0..6] cycles per phase, out[7] tiles.
+extern "C" int smj_debug_phase_cycles(unsigned long long *out16) {
+    hipDeviceSynchronize();
+    return read_phase_cycles(out16) == hipSuccess ? SMJ_OK : SMJ_ERR_HIP;
+}
+
 static std::string prof_json() {
     struct Agg { long launches = 0; double ms = 0, bytes = 0; };
     std::map<std::string, Agg> agg;
@@ -338,7 +345,8 @@ extern "C" int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int
     SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(ntiles + 1) * sizeof(int64_t)));
     {
         ProfScope ps("merge_partition", 0, s);
-        HIP_TRY(launch_merge_partition(a, na, cols, key_col, b, nb, cols, key_col, (int64_t *)sc->apart, ntiles, s));
+        HIP_TRY(launch_merge_partition(a, na, cols, key_col, b, nb, cols, key_col, (int64_t *)sc->apart, nullptr,
+                                       ntiles, s));
     }
     ProfScope ps("merge_tiles", 2.0 * 8 * cols * (na + nb), s);
     HIP_TRY(launch_merge_tiles(a, na, b, nb, cols, key_col, (const int64_t *)sc->apart, ntiles, out, s));
@@ -360,30 +368,31 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
         if (!R || !S || !out) return SMJ_ERR_INVALID;
         const int64_t ntiles = (nr + ns + kJoinTile - 1) / kJoinTile;
         const int tc = c1 + c2 - 1;
-        // apart (ntiles+1) | offs (ntiles) | counts (ntiles u32), slots (nr rows)
+        // apart (ntiles+1) | run_start (ntiles) | offs (ntiles u32) | counts (ntiles u32); slots (nr rows)
         SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(3 * ntiles + 2) * sizeof(int64_t)));
         SMJ_TRY(grow(&sc->tmp, &sc->tmp_bytes, (size_t)nr * tc * sizeof(int64_t)));
         int64_t *apart = (int64_t *)sc->apart;
-        int64_t *offs = apart + ntiles + 1;
-        uint32_t *counts = (uint32_t *)(offs + ntiles);
+        int64_t *run_start = apart + ntiles + 1;
+        uint32_t *offs = (uint32_t *)(run_start + ntiles);
+        uint32_t *counts = offs + ntiles;
         int64_t *slots = (int64_t *)sc->tmp;
         {
             ProfScope ps("join_partition", 0, s);
-            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, s));
+            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, s));
         }
         {
             ProfScope ps("join_tiles", 8.0 * (c1 * nr + c2 * ns), s);
-            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out,
-                                d_out_rows, 0, s));
+            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, slots, counts, offs,
+                                out, d_out_rows, 0, s));
         }
         {
             ProfScope ps("join_scan", 0, s);
-            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out,
-                                d_out_rows, 1, s));
+            HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, slots, counts, offs,
+                                out, d_out_rows, 1, s));
         }
         ProfScope ps("join_compact", 0, s);
-        HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, ntiles, slots, counts, offs, out, d_out_rows,
-                            2, s));
+        HIP_TRY(launch_join(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, slots, counts, offs, out,
+                            d_out_rows, 2, s));
     }
     if (h_out_rows) {
         HIP_TRY(hipMemcpyAsync(sc->h_small, d_out_rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));

@@ -97,17 +97,21 @@ hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *c
 hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
                               int64_t sel_val, int key_col, const int64_t *spl, int nspl,
                               unsigned long long *gcount, long long *gminmax, hipStream_t s);
+// run_start may be nullptr (merge); for the join it gets, per tile, the first
+// A row carrying the key of A[apart[t]]
 hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
-                                  int64_t nb, int cb, int kb, int64_t *apart, int64_t ntiles,
+                                  int64_t nb, int cb, int kb, int64_t *apart, int64_t *run_start, int64_t ntiles,
                                   hipStream_t s);
 // join phases: 0 = tiles (slots + counts), 1 = scan counts (offs, *out_rows),
 // 2 = compact slots into out
 hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns, int c2,
-                       int key2, const int64_t *apart, int64_t ntiles, int64_t *slots, uint32_t *counts,
-                       int64_t *offs, int64_t *out, int64_t *out_rows, int phase, hipStream_t s);
+                       int key2, const int64_t *apart, const int64_t *run_start, int64_t ntiles, int64_t *slots,
+                       uint32_t *counts, uint32_t *offs, int64_t *out, int64_t *out_rows, int phase,
+                       hipStream_t s);
 hipError_t launch_merge_tiles(const int64_t *a, int64_t na, const int64_t *b, int64_t nb, int cols,
                               int key_col, const int64_t *apart, int64_t ntiles, int64_t *out,
                               hipStream_t s);
+hipError_t read_phase_cycles(unsigned long long *out16);
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed,
                               uint64_t key_range, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,

@@ -311,6 +311,18 @@ __global__ __launch_bounds__(256) void chunk_scan_apply_kernel(uint32_t *__restr
 //            totals gives each digit's local start);
 //   scatter  consecutive LDS rows of one digit leave as one contiguous run at
 //            the digit's running global offset.
+// Diagnostic phase stamps (SMJ_DEBUG_PASS bit 3): cycles between the
+// barriers of chunk_scatter, summed over workgroups (thread 0's view).
+__device__ unsigned long long g_phase_cycles[16];
+#define SMJ_STAMP(k)                                                       \
+    if (p.dbg & 8) {                                                       \
+        if (tid == 0) {                                                    \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+            ph[k] += t_ - t_last;                                          \
+            t_last = t_;                                                   \
+        }                                                                  \
+    }
+
 template <int COLS, int DBITS, class DigitF>
 __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const PassParams<DigitF> p) {
     using L = PassLds<COLS, DBITS>;
@@ -344,10 +356,13 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
     int64_t rows[ITEMS][COLS];
     load_tile<COLS, ITEMS>(p.src, end, begin + lane_row, rows);
     uint32_t chunk_total = 0;
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_last = (p.dbg & 8) ? __builtin_amdgcn_s_memtime() : 0;
 
     for (int64_t tile0 = begin;;) {
         for (int i = tid; i < kSortWaves * RADIX; i += kSortThreads) s_wcnt[i] = 0;
         __syncthreads();  // B1 (also publishes s_run on the first tile)
+        SMJ_STAMP(0);
 
         // ---- digits (select predicate fused into pass 0)
         const int64_t row0 = tile0 + lane_row;
@@ -379,6 +394,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
             }
         }
         __syncthreads();  // B2
+        SMJ_STAMP(1);
 
         // ---- per-digit totals, cross-wave exclusive prefix in place
         uint32_t tot[BPT], incl[BPT];
@@ -399,6 +415,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
             if (lane == 63) s_misc[4 + j * kSortWaves + wave] = incl[j];
         }
         __syncthreads();  // B3
+        SMJ_STAMP(2);
         // ---- block exclusive scan of the totals in digit order -> local starts
         uint32_t run = 0;
 #pragma unroll
@@ -417,6 +434,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         const uint32_t tile_total = run;
         chunk_total += tile_total;
         __syncthreads();  // B4
+        SMJ_STAMP(3);
 
         // ---- tile-local destinations; prefetch the next tile behind them
 #pragma unroll
@@ -428,6 +446,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         int64_t nrows[ITEMS][COLS];
         if (next0 < end) load_tile<COLS, ITEMS>(p.src, end, next0 + lane_row, nrows);
         __syncthreads();  // B5: counters dead, the region becomes the staging tile
+        SMJ_STAMP(4);
         if (!(p.dbg & 4)) {
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
@@ -443,6 +462,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
             }
         }
         __syncthreads();  // B6
+        SMJ_STAMP(5);
 
         // ---- scatter: consecutive LDS rows of one digit -> consecutive HBM rows
         if (!(p.dbg & 4)) {
@@ -454,6 +474,8 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
                 else if (r[0] == 0x7fffffffffffffffll && d == 12345u) p.dst[0] = r[COLS - 1];  // keep live
             }
         }
+        SMJ_STAMP(6);
+        ph[7]++;
         if (next0 >= end) break;
         __syncthreads();  // B0: staging tile read before it is zeroed again
         tile0 = next0;
@@ -463,6 +485,8 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
             for (int c = 0; c < COLS; c++) rows[it][c] = nrows[it][c];
     }
     if (tid == 0 && chunk_total) atomicAdd(&p.ctr->count, chunk_total);
+    if ((p.dbg & 8) && tid == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], ph[k]);
 }
 
 // ---------------------------------------------------------------------------
@@ -627,11 +651,16 @@ __global__ __launch_bounds__(512) void hist_bucket_kernel(const int64_t *__restr
 
 // ---------------------------------------------------------------------------
 // merge path: a_t = #rows of A among the first min(t*kJoinTile, na+nb) rows
-// of the stable merge (A first on equal keys).
+// of the stable merge (A first on equal keys); one thread per diagonal,
+// binary search.  With run_start != nullptr the thread also finds the first
+// A row carrying A[a_t].key (the join needs the start of the key run that a
+// tile begins in): gallop backwards, then bisect -- one probe when keys are
+// distinct, O(log run) under skew.
 // ---------------------------------------------------------------------------
-__global__ void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na, int ca, int ka,
-                                       const int64_t *__restrict__ b, int64_t nb, int cb, int kb,
-                                       int64_t *apart, int64_t ntiles) {
+__global__ __launch_bounds__(256) void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na, int ca,
+                                                              int ka, const int64_t *__restrict__ b, int64_t nb,
+                                                              int cb, int kb, int64_t *apart, int64_t *run_start,
+                                                              int64_t ntiles) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
     const int64_t d = min(t * (int64_t)kJoinTile, na + nb);
@@ -642,6 +671,28 @@ __global__ void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na
         if (a[mid * ca + ka] <= b[(d - 1 - mid) * cb + kb]) lo = mid + 1; else hi = mid;
     }
     apart[t] = lo;
+    if (!run_start || t == ntiles) return;
+    int64_t first = lo;
+    if (lo < na && lo > 0) {
+        const int64_t k = a[lo * ca + ka];
+        if (a[(lo - 1) * ca + ka] == k) {
+            int64_t h = lo - 1, l = -1, step = 1;  // a[h] == k; first equal lies in (l, h]
+            while (true) {
+                const int64_t c = h - step;
+                if (c < 0) { l = -1; break; }
+                if (a[c * ca + ka] != k) { l = c; break; }
+                h = c;
+                step <<= 1;
+            }
+            int64_t x = l + 1;
+            while (x < h) {
+                const int64_t mid = (x + h) >> 1;
+                if (a[mid * ca + ka] == k) h = mid; else x = mid + 1;
+            }
+            first = x;
+        }
+    }
+    run_start[t] = first;
 }
 
 // ---------------------------------------------------------------------------
@@ -662,17 +713,15 @@ struct JoinParams {
     const int64_t *R;
     const int64_t *S;
     const int64_t *apart;
+    const int64_t *run_start;  // first R row with the key of R[apart[t]]
     int64_t *slots;      // [nr][c1 + c2 - 1]
     uint32_t *counts;    // [ntiles]
     int64_t nr, ns, ntiles;
     int c1, key1, c2, key2;
 };
 
-constexpr int kJoinStageCols = 3;  // output rows up to 3 columns are staged in LDS
-
 __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParams p) {
-    __shared__ int64_t s_keys[kJoinTile];
-    __shared__ int64_t s_out[(kJoinTile / 2) * kJoinStageCols];
+    __shared__ int64_t s_keys[kJoinTile];  // tile keys; then the staged output rows
     __shared__ uint32_t s_scan[kJoinThreads / 64];
     __shared__ int64_t s_lbr0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -684,28 +733,7 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     const int nR = (int)(a1 - a0), nS = (int)(b1 - b0), nM = nR + nS;
     for (int j = tid; j < nM; j += kJoinThreads)
         s_keys[j] = j < nR ? p.R[(a0 + j) * p.c1 + p.key1] : p.S[(b0 + j - nR) * p.c2 + p.key2];
-    if (tid == 0 && nR > 0) {
-        // first R row carrying R[a0].key: gallop backwards, then bisect
-        const int64_t k = p.R[a0 * p.c1 + p.key1];
-        int64_t first = a0;
-        if (a0 > 0 && p.R[(a0 - 1) * p.c1 + p.key1] == k) {
-            int64_t hi = a0 - 1, lo = -1, step = 1;  // R[hi] == k
-            while (true) {
-                const int64_t c = hi - step;
-                if (c < 0) { lo = -1; break; }
-                if (p.R[c * p.c1 + p.key1] != k) { lo = c; break; }
-                hi = c;
-                step <<= 1;
-            }
-            int64_t l = lo + 1, h = hi;  // first equal lies in (lo, hi]
-            while (l < h) {
-                const int64_t mid = (l + h) >> 1;
-                if (p.R[mid * p.c1 + p.key1] == k) h = mid; else l = mid + 1;
-            }
-            first = l;
-        }
-        s_lbr0 = first;
-    }
+    if (tid == 0) s_lbr0 = p.run_start[tile];
     __syncthreads();
 
     const int64_t *rk = s_keys;
@@ -775,12 +803,13 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     off += incl - cnt;
     if (tid == 0) p.counts[tile] = total;
     const int tc = p.c1 + p.c2 - 1;
-    if (tc <= kJoinStageCols) {
-        // stage the tile's output rows in LDS, then one coalesced copy
+    if ((int64_t)total * tc <= kJoinTile) {
+        // stage the tile's output rows in LDS (the keys are dead: every read of
+        // them happened before the scan barrier above), then one coalesced copy
 #pragma unroll
         for (int q = 0; q < kJoinPer; q++) {
             if ((mmask >> q) & 1u) {
-                int64_t *dst = s_out + (size_t)(off + __popc(mmask & ((1u << q) - 1u))) * tc;
+                int64_t *dst = s_keys + (size_t)(off + __popc(mmask & ((1u << q) - 1u))) * tc;
                 const int64_t *rr = p.R + (a0 + mrow[q]) * p.c1;
                 const int64_t *ss = p.S + mpart[q] * p.c2;
                 for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
@@ -790,7 +819,7 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
         }
         __syncthreads();
         int64_t *out = p.slots + a0 * tc;
-        for (uint32_t i = tid; i < total * tc; i += kJoinThreads) out[i] = s_out[i];
+        for (uint32_t i = tid; i < total * tc; i += kJoinThreads) out[i] = s_keys[i];
     } else {
 #pragma unroll
         for (int q = 0; q < kJoinPer; q++) {
@@ -806,43 +835,58 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     }
 }
 
-// exclusive scan of the per-tile match counts (one workgroup); writes the
-// joined row count to *out_rows
+// exclusive scan of the per-tile match counts (one workgroup of 1024): rounds
+// of 16 Ki counts staged through LDS (coalesced in and out), 16 per thread.
+// Writes the joined row count to *out_rows.
 __global__ __launch_bounds__(1024) void join_scan_kernel(const uint32_t *__restrict__ counts, int64_t ntiles,
-                                                         int64_t *__restrict__ offs, int64_t *out_rows) {
-    __shared__ int64_t s_w[16];
+                                                         uint32_t *__restrict__ offs, int64_t *out_rows) {
+    constexpr int PER = 16, ROUND = 1024 * PER;
+    __shared__ uint32_t s_c[ROUND];
+    __shared__ uint32_t s_w[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t per = (ntiles + 1023) / 1024;
-    const int64_t c0 = min((int64_t)tid * per, ntiles), c1 = min(c0 + per, ntiles);
-    int64_t sum = 0;
-    for (int64_t c = c0; c < c1; c++) sum += counts[c];
-    int64_t incl = sum;
+    uint32_t carry = 0;
+    for (int64_t base = 0; base < ntiles; base += ROUND) {
+        const int64_t n = min((int64_t)ROUND, ntiles - base);
+        for (int i = tid; i < ROUND; i += 1024) s_c[i] = i < n ? counts[base + i] : 0u;
+        __syncthreads();
+        uint32_t v[PER], sum = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+        for (int k = 0; k < PER; k++) {
+            v[k] = s_c[tid * PER + k];
+            sum += v[k];
+        }
+        const uint32_t incl = wave_incl_scan(sum, lane);
+        if (lane == 63) s_w[wave] = incl;
+        __syncthreads();
+        uint32_t run = carry + incl - sum, all = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            run += (w < wave) ? s_w[w] : 0u;
+            all += s_w[w];
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            s_c[tid * PER + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        for (int i = tid; i < n; i += 1024) offs[base + i] = s_c[i];
+        carry += all;
+        __syncthreads();
     }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    int64_t run = incl - sum;
-    for (int w = 0; w < wave; w++) run += s_w[w];
-    for (int64_t c = c0; c < c1; c++) {
-        offs[c] = run;
-        run += counts[c];
-    }
-    if (tid == 1023) *out_rows = run;
+    if (tid == 0) *out_rows = (int64_t)carry;
 }
 
 // pack the slots: tile t's cnt_t rows at slot row a0_t -> output row offs_t
 __global__ __launch_bounds__(256) void join_compact_kernel(const int64_t *__restrict__ slots,
                                                            const int64_t *__restrict__ apart,
                                                            const uint32_t *__restrict__ counts,
-                                                           const int64_t *__restrict__ offs, int tc,
+                                                           const uint32_t *__restrict__ offs, int tc,
                                                            int64_t *__restrict__ out) {
     const int64_t t = blockIdx.x;
     const int64_t n = (int64_t)counts[t] * tc;
     const int64_t *src = slots + apart[t] * tc;
-    int64_t *dst = out + offs[t] * tc;
+    int64_t *dst = out + (int64_t)offs[t] * tc;
     for (int64_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
 }
 
@@ -1037,18 +1081,19 @@ hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *c
 }
 
 hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
-                                  int64_t nb, int cb, int kb, int64_t *apart, int64_t ntiles,
+                                  int64_t nb, int cb, int kb, int64_t *apart, int64_t *run_start, int64_t ntiles,
                                   hipStream_t s) {
-    hipLaunchKernelGGL(merge_partition_kernel, dim3(blocks_for(ntiles + 1, 256)), dim3(256), 0, s, a, na,
-                       ca, ka, b, nb, cb, kb, apart, ntiles);
+    hipLaunchKernelGGL(merge_partition_kernel, dim3(blocks_for(ntiles + 1, 256)), dim3(256), 0, s, a, na, ca, ka, b,
+                       nb, cb, kb, apart, run_start, ntiles);
     return hipGetLastError();
 }
 
 hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns, int c2,
-                       int key2, const int64_t *apart, int64_t ntiles, int64_t *slots, uint32_t *counts,
-                       int64_t *offs, int64_t *out, int64_t *out_rows, int phase, hipStream_t s) {
+                       int key2, const int64_t *apart, const int64_t *run_start, int64_t ntiles, int64_t *slots,
+                       uint32_t *counts, uint32_t *offs, int64_t *out, int64_t *out_rows, int phase,
+                       hipStream_t s) {
     if (phase == 0) {
-        JoinParams p{R, S, apart, slots, counts, nr, ns, ntiles, c1, key1, c2, key2};
+        JoinParams p{R, S, apart, run_start, slots, counts, nr, ns, ntiles, c1, key1, c2, key2};
         hipLaunchKernelGGL(join_tile_kernel, dim3((unsigned)ntiles), dim3(kJoinThreads), 0, s, p);
     } else if (phase == 1) {
         hipLaunchKernelGGL(join_scan_kernel, dim3(1), dim3(1024), 0, s, counts, ntiles, offs, out_rows);
@@ -1065,6 +1110,14 @@ hipError_t launch_merge_tiles(const int64_t *a, int64_t na, const int64_t *b, in
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((merge_tile_kernel<C>), dim3((unsigned)ntiles),
                                              dim3(kJoinThreads), 0, s, a, na, b, nb, key_col, apart, out));
     return hipGetLastError();
+}
+
+// diagnostic: read and clear the chunk_scatter phase cycle sums
+hipError_t read_phase_cycles(unsigned long long *out16) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 16);
+    if (e != hipSuccess) return e;
+    static const unsigned long long zero[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero));
 }
 
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
