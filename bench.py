@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per table per GPU")
-    p.add_argument("--cpu-sample", type=int, default=131072,
+    p.add_argument("--cpu-sample", type=int, default=196608,
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
     p.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field")

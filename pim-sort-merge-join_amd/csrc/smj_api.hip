@@ -156,6 +156,7 @@ struct DevScratch {
     void *tmp = nullptr;  size_t tmp_bytes = 0;     // ping-pong rows
     void *status = nullptr; size_t status_bytes = 0; // pass chunk tables / join look-back words
     uint32_t *segsum = nullptr;                      // kScanSegs * kRadix
+    int64_t *trash = nullptr;                        // kSortThreads * 16 int64 write sink
     void *apart = nullptr; size_t apart_bytes = 0;   // merge-path partition
     uint32_t *hist = nullptr;                        // kNumPos * kRadix
     SortPlan *plan = nullptr;                        // device
@@ -190,6 +191,7 @@ int scratch(DevScratch **out) {
         HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
         HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 32));
         HIP_TRY(hipMalloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
+        HIP_TRY(hipMalloc(&s.trash, sizeof(int64_t) * kSortThreads * 16));
         HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 64, hipHostMallocDefault));
     }
@@ -215,18 +217,18 @@ int check_err(DevScratch *sc, int slot, hipStream_t s) {
 
 // One scatter pass (chunk_hist -> chunk_scan -> chunk_scatter).  rows_out:
 // rows the pass writes (for the profiler's algorithmic byte count).
-static int run_pass(DevScratch *sc, const PassSpec &ps, const uint32_t *base, Counters *ctr, const char *tag,
+static int run_pass(DevScratch *sc, const PassSpec &ps, const uint32_t *base, Counters *ctr, bool have_table,
                     int64_t rows_out, hipStream_t s) {
     static const char *names[3][3] = {{"radix_hist", "radix_scan", "radix_scatter"},
                                       {"select_hist", "select_scan", "select_scatter"},
                                       {"partition_hist", "partition_scan", "partition_scatter"}};
-    (void)tag;
     const int k = ps.kind == DIGIT_RADIX ? 0 : ps.kind == DIGIT_ZERO ? 1 : 2;
     const double rowb = 8.0 * ps.cols;
+    const_cast<PassSpec &>(ps).trash = sc->trash;
     const size_t tbytes = (size_t)pass_chunks(ps) * pass_radix(ps) * sizeof(uint32_t);
     SMJ_TRY(grow(&sc->status, &sc->status_bytes, tbytes));
     uint32_t *table = (uint32_t *)sc->status;
-    {
+    if (!have_table) {
         ProfScope p1(names[k][0], rowb * ps.nsrc, s);
         HIP_TRY(launch_chunk_hist(ps, table, s));
     }
@@ -255,9 +257,12 @@ static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int
 
     HIP_TRY(hipMemsetAsync(sc->hist, 0, sizeof(uint32_t) * kNumPos * kRadix, s));
     HIP_TRY(hipMemsetAsync(&sc->ctr[0], 0, sizeof(Counters), s));
+    // chunk table of the first pass (digit 0), filled by hist_radix
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, (size_t)((n + chunk_rows(cols) - 1) / chunk_rows(cols)) * kRadix * 4));
     {
         ProfScope ps("hist_radix", rowb * n, s);
-        HIP_TRY(launch_hist_radix(in, n, cols, use_select, sel_col, sel_val, key_col, key_base, sc->hist, s));
+        HIP_TRY(launch_hist_radix(in, n, cols, use_select, sel_col, sel_val, key_col, key_base, sc->hist,
+                                  (uint32_t *)sc->status, s));
     }
     {
         ProfScope ps("plan", 0, s);
@@ -285,7 +290,8 @@ static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int
         ps.kind = DIGIT_RADIX;
         ps.key_base = key_base;
         ps.shift = plan.pos[k] * kRadixBits;
-        SMJ_TRY(run_pass(sc, ps, sc->hist + plan.pos[k] * kRadix, &sc->ctr[0], "radix", m, s));
+        // pass 0 on digit 0 reuses the chunk counts hist_radix already wrote
+        SMJ_TRY(run_pass(sc, ps, sc->hist + plan.pos[k] * kRadix, &sc->ctr[0], k == 0 && plan.pos[0] == 0, m, s));
         src = dst;
     }
     *out_rows = m;
@@ -319,7 +325,7 @@ extern "C" int smj_dev_select(const T *in, int64_t n, int cols, int sel_col, T s
     ps.sel_col = sel_col;
     ps.sel_val = sel_val;
     ps.kind = DIGIT_ZERO;
-    SMJ_TRY(run_pass(sc, ps, nullptr, &sc->ctr[1], "select", n, s));
+    SMJ_TRY(run_pass(sc, ps, nullptr, &sc->ctr[1], false, n, s));
     Counters c;
     HIP_TRY(hipMemcpyAsync(&c, &sc->ctr[1], sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -346,7 +352,7 @@ extern "C" int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int
     {
         ProfScope ps("merge_partition", 0, s);
         HIP_TRY(launch_merge_partition(a, na, cols, key_col, b, nb, cols, key_col, (int64_t *)sc->apart, nullptr,
-                                       ntiles, s));
+                                       ntiles, kJoinTile, s));
     }
     ProfScope ps("merge_tiles", 2.0 * 8 * cols * (na + nb), s);
     HIP_TRY(launch_merge_tiles(a, na, b, nb, cols, key_col, (const int64_t *)sc->apart, ntiles, out, s));
@@ -366,7 +372,8 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
         HIP_TRY(hipMemsetAsync(d_out_rows, 0, sizeof(int64_t), s));
     } else {
         if (!R || !S || !out) return SMJ_ERR_INVALID;
-        const int64_t ntiles = (nr + ns + kJoinTile - 1) / kJoinTile;
+        const int jt = join_tile_size(c1, c2);
+        const int64_t ntiles = (nr + ns + jt - 1) / jt;
         const int tc = c1 + c2 - 1;
         // apart (ntiles+1) | run_start (ntiles) | offs (ntiles u32) | counts (ntiles u32); slots (nr rows)
         SMJ_TRY(grow(&sc->apart, &sc->apart_bytes, (size_t)(3 * ntiles + 2) * sizeof(int64_t)));
@@ -378,7 +385,7 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
         int64_t *slots = (int64_t *)sc->tmp;
         {
             ProfScope ps("join_partition", 0, s);
-            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, s));
+            HIP_TRY(launch_merge_partition(R, nr, c1, key1, S, ns, c2, key2, apart, run_start, ntiles, jt, s));
         }
         {
             ProfScope ps("join_tiles", 8.0 * (c1 * nr + c2 * ns), s);
@@ -475,7 +482,7 @@ extern "C" int smj_dev_partition_scatter(const T *in, int64_t n, int cols, int u
     ps.kind = DIGIT_BUCKET;
     ps.spl = spl;
     ps.nspl = n_split;
-    SMJ_TRY(run_pass(sc, ps, d_base, &sc->ctr[3], "partition", total, s));
+    SMJ_TRY(run_pass(sc, ps, d_base, &sc->ctr[3], false, total, s));
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_TRY(hipStreamSynchronize(s));
     return SMJ_OK;
@@ -543,6 +550,7 @@ extern "C" void smj_finalize(void) {
         hipFree(s.ctr);
         hipFree(s.dcount);
         hipFree(s.segsum);
+        hipFree(s.trash);
         hipHostFree(s.h_plan);
         hipHostFree(s.h_small);
     }

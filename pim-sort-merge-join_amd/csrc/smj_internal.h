@@ -16,16 +16,22 @@ namespace smj {
 // scatters the tile through LDS so that each digit's run leaves as coalesced
 // 16-B-per-lane stores.
 // ---------------------------------------------------------------------------
-constexpr int kSortThreads = 512;
+#ifndef SMJ_SORT_THREADS
+#define SMJ_SORT_THREADS 1024
+#endif
+#ifndef SMJ_RADIX_BITS
+#define SMJ_RADIX_BITS 10
+#endif
+constexpr int kSortThreads = SMJ_SORT_THREADS;
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kRadixBits = 10;                   // digit width of the radix passes
+constexpr int kRadixBits = SMJ_RADIX_BITS;       // digit width of the radix passes
 constexpr int kRadix = 1 << kRadixBits;          // 1024 bins
 constexpr int kNumPos = (64 + kRadixBits - 1) / kRadixBits;  // 7 digit positions
 constexpr int kBucketBits = 4;                   // multi-GPU partition: <= 16 buckets
 constexpr int kMaxSplitters = (1 << kBucketBits) - 1;
 
 // rows per thread per tile: a tile is 64 KiB of rows whatever the row width
-__host__ __device__ constexpr int sort_items(int cols) { return cols >= 8 ? 2 : (16 / cols); }
+__host__ __device__ constexpr int sort_items(int cols) { return cols == 1 ? 8 : cols >= 8 ? 2 : (16 / cols); }
 __host__ __device__ constexpr int sort_tile_rows(int cols) { return sort_items(cols) * kSortThreads; }
 
 // A pass is processed in chunks of kChunkTiles consecutive tiles (one
@@ -39,7 +45,11 @@ constexpr int kScanSegs = 16;
 // merged elements (R-piece + S-piece).
 constexpr int kJoinThreads = 512;
 constexpr int kJoinPer = 8;
-constexpr int kJoinTile = kJoinThreads * kJoinPer;  // 4096
+constexpr int kJoinTile = kJoinThreads * kJoinPer;  // 4096 (merge); the join adapts:
+// merged elements per join tile: both pieces must fit in 64 KiB of LDS as rows
+__host__ __device__ constexpr int join_tile_size(int c1, int c2) {
+    return (c1 > c2 ? c1 : c2) <= 2 ? 4096 : (c1 > c2 ? c1 : c2) <= 4 ? 2048 : 1024;
+}
 
 // Look-back status word: [31:30] flag, [29:0] count.
 constexpr uint32_t kFlagAgg = 1u << 30;
@@ -67,8 +77,10 @@ struct Counters {
 // All return hipSuccess or the launch error.  `prof` tags are recorded by
 // the caller.
 
+// all-digit histograms (ghist[kNumPos][kRadix]) + digit-0 counts per chunk of
+// the first pass (table0[chunks][kRadix])
 hipError_t launch_hist_radix(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
-                             int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist,
+                             int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist, uint32_t *table0,
                              hipStream_t s);
 hipError_t launch_plan(uint32_t *ghist, SortPlan *plan, hipStream_t s);
 enum DigitKind { DIGIT_RADIX = 0, DIGIT_ZERO = 1, DIGIT_BUCKET = 2 };
@@ -85,6 +97,7 @@ struct PassSpec {
     int shift;
     const int64_t *spl;   // DIGIT_BUCKET: host array of nspl sorted splitters
     int nspl;
+    int64_t *trash;       // device scratch, kSortThreads * 16 int64 (ITEMS * COLS <= 16)
 };
 int pass_radix(const PassSpec &ps);
 int64_t pass_chunks(const PassSpec &ps);
@@ -101,7 +114,7 @@ hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_s
 // A row carrying the key of A[apart[t]]
 hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
                                   int64_t nb, int cb, int kb, int64_t *apart, int64_t *run_start, int64_t ntiles,
-                                  hipStream_t s);
+                                  int tile, hipStream_t s);
 // join phases: 0 = tiles (slots + counts), 1 = scan counts (offs, *out_rows),
 // 2 = compact slots into out
 hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int64_t *S, int64_t ns, int c2,

@@ -65,12 +65,14 @@ __device__ __forceinline__ void store_row(int64_t *__restrict__ p, const int64_t
     }
 }
 
-// r[col] with a run-time col, compile-time indexing only (no scratch).
+// r[col] with a run-time col.  Written as an and/or of per-column masks:
+// the equivalent select chain is pattern-matched by hipcc into an indexed
+// access, which demotes the whole row array to scratch memory.
 template <int COLS>
 __device__ __forceinline__ int64_t pick(const int64_t (&r)[COLS], int col) {
-    int64_t v = r[0];
+    int64_t v = 0;
 #pragma unroll
-    for (int c = 1; c < COLS; c++) v = (col == c) ? r[c] : v;
+    for (int c = 0; c < COLS; c++) v |= r[c] & -(int64_t)(col == c);
     return v;
 }
 
@@ -98,12 +100,17 @@ __device__ __forceinline__ uint32_t spin_status(const uint32_t *p, uint32_t *err
     return w;
 }
 
+// Inclusive wave64 scan on DPP (row_shr 1/2/4/8 inside each row of 16
+// lanes, then row_bcast:15 / row_bcast:31 across rows): VALU-only, no LDS
+// permutes.  `lane` is unused; kept for call-site symmetry.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    (void)lane;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
 }
 
@@ -166,10 +173,11 @@ struct PassParams {
     int64_t *dst;
     int64_t nsrc;
     int64_t sel_val;
-    int use_select, sel_col, key_col, dbg;  // dbg: ablation bits (SMJ_DEBUG_PASS), 0 in production
+    int use_select, sel_col, key_col, dbg;  // dbg bit 3: phase stamps (SMJ_DEBUG_PASS), 0 in production
     DigitF digit;
     uint32_t *table;  // [nchunks][RADIX]: counts (chunk_hist) -> exclusive offsets (chunk_scan)
     Counters *ctr;
+    int64_t *trash;   // kSortThreads * 16 int64 scratch: dummy / empty-tile stores
 };
 
 template <int COLS, int DBITS>
@@ -187,17 +195,16 @@ struct PassLds {
     static constexpr int BYTES = OFF_MISC + 128;
 };
 
+// Rows past `end` are loaded from row end-1 instead (and masked out by the
+// caller): no branches around the loads, so the compiler can count them in
+// s_waitcnt vmcnt(N) instead of draining every outstanding store (vmcnt(0)).
 template <int COLS, int ITEMS>
 __device__ __forceinline__ void load_tile(const int64_t *__restrict__ src, int64_t end, int64_t row0,
                                           int64_t (&rows)[ITEMS][COLS]) {
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
-        const int64_t r = row0 + it * 64;
-        if (r < end) load_row<COLS>(src + r * COLS, rows[it]);
-        else {
-#pragma unroll
-            for (int c = 0; c < COLS; c++) rows[it][c] = 0;
-        }
+        const int64_t r = min(row0 + it * 64, end - 1);
+        load_row<COLS>(src + r * COLS, rows[it]);
     }
 }
 
@@ -218,9 +225,9 @@ __global__ __launch_bounds__(512) void chunk_hist_kernel(const PassParams<DigitF
         int64_t key[U], sv[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int64_t r = r0 + u * 512 + tid;
-            key[u] = r < end ? p.src[r * COLS + p.key_col] : 0;
-            sv[u] = (r < end && p.use_select) ? p.src[r * COLS + p.sel_col] : 0;
+            const int64_t r = min(r0 + u * 512 + tid, end - 1);  // clamped: no branches around loads
+            key[u] = p.src[r * COLS + p.key_col];
+            sv[u] = p.src[r * COLS + p.sel_col];
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -355,12 +362,23 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
     }
     int64_t rows[ITEMS][COLS];
     load_tile<COLS, ITEMS>(p.src, end, begin + lane_row, rows);
+    // ITEMS dummy stores behind the first loads: the loop is then always
+    // entered with (loads, then ITEMS stores) in flight, exactly as from its
+    // back edge, so hipcc's vmcnt waits for the rows skip the stores
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        int64_t z[COLS];
+#pragma unroll
+        for (int c = 0; c < COLS; c++) z[c] = 0;
+        store_row<COLS>(p.trash + ((size_t)it * kSortThreads + tid) * COLS, z);
+    }
     uint32_t chunk_total = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long t_last = (p.dbg & 8) ? __builtin_amdgcn_s_memtime() : 0;
 
     for (int64_t tile0 = begin;;) {
-        for (int i = tid; i < kSortWaves * RADIX; i += kSortThreads) s_wcnt[i] = 0;
+        for (int i = tid; i < kSortWaves * RADIX / 4; i += kSortThreads)
+            reinterpret_cast<uint4 *>(s_wcnt)[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();  // B1 (also publishes s_run on the first tile)
         SMJ_STAMP(0);
 
@@ -436,22 +454,22 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         __syncthreads();  // B4
         SMJ_STAMP(3);
 
-        // ---- tile-local destinations; prefetch the next tile behind them
+        // ---- tile-local destinations
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {  // dig[it] becomes the LDS slot
             const uint32_t d = dig[it] & 0xffffu;
             dig[it] = ((vmask >> it) & 1u) ? s_binstart[d] + wc[d] + (dig[it] >> 16) : 0u;
         }
         const int64_t next0 = tile0 + TILE;
-        int64_t nrows[ITEMS][COLS];
-        if (next0 < end) load_tile<COLS, ITEMS>(p.src, end, next0 + lane_row, nrows);
         __syncthreads();  // B5: counters dead, the region becomes the staging tile
         SMJ_STAMP(4);
-        if (!(p.dbg & 4)) {
-#pragma unroll
-            for (int it = 0; it < ITEMS; it++)
-                if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-        }
+    #pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+        // the rows are staged: their registers now take the next tile's rows,
+        // in flight while this tile is scattered (after the last tile: an
+        // L2-hot reload of this one -- unconditional, so vmcnt stays exact)
+        load_tile<COLS, ITEMS>(p.src, end, (next0 < end ? next0 : tile0) + lane_row, rows);
 #pragma unroll
         for (int j = 0; j < BPT; j++) {
             const int d = tid + j * kSortThreads;
@@ -465,13 +483,21 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         SMJ_STAMP(5);
 
         // ---- scatter: consecutive LDS rows of one digit -> consecutive HBM rows
-        if (!(p.dbg & 4)) {
-            for (uint32_t i = tid; i < tile_total; i += kSortThreads) {
+        // exactly ITEMS unconditional stores per thread (a static count keeps
+        // the compiler's vmcnt waits for the prefetch exact): slots past
+        // tile_total rewrite the last row with its own value; an empty tile
+        // writes its (garbage) slots to the trash buffer
+        {
+            const bool any = tile_total > 0;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const uint32_t i = any ? min((uint32_t)(tid + it * kSortThreads), tile_total - 1u) : 0u;
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)i * COLS, r);
                 const uint32_t d = p.digit(pick<COLS>(r, p.key_col)) & MASK;
-                if (!(p.dbg & 2)) store_row<COLS>(p.dst + ((int64_t)s_adj[d] + (int64_t)i) * COLS, r);
-                else if (r[0] == 0x7fffffffffffffffll && d == 12345u) p.dst[0] = r[COLS - 1];  // keep live
+                int64_t *q = any ? p.dst + ((int64_t)s_adj[d] + (int64_t)i) * COLS
+                                 : p.trash + ((size_t)it * kSortThreads + tid) * COLS;
+                store_row<COLS>(q, r);
             }
         }
         SMJ_STAMP(6);
@@ -479,10 +505,6 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         if (next0 >= end) break;
         __syncthreads();  // B0: staging tile read before it is zeroed again
         tile0 = next0;
-#pragma unroll
-        for (int it = 0; it < ITEMS; it++)
-#pragma unroll
-            for (int c = 0; c < COLS; c++) rows[it][c] = nrows[it][c];
     }
     if (tid == 0 && chunk_total) atomicAdd(&p.ctr->count, chunk_total);
     if ((p.dbg & 8) && tid == 0)
@@ -492,50 +514,67 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
 // ---------------------------------------------------------------------------
 // histogram (upsweep) of all digit positions of the selected rows
 // ---------------------------------------------------------------------------
+// Histograms of every digit position of the selected rows, chunk by chunk
+// (the chunks of the first radix pass): the digit-0 counts of each chunk are
+// also written to table0[chunk][*], so the first pass needs no chunk_hist of
+// its own when digit 0 is not trivial (the usual case).
 template <int COLS>
 __global__ __launch_bounds__(512) void hist_radix_kernel(const int64_t *__restrict__ src, int64_t n,
                                                          int use_select, int sel_col, int64_t sel_val,
                                                          int key_col, uint64_t base,
-                                                         uint32_t *__restrict__ ghist) {
+                                                         uint32_t *__restrict__ ghist,
+                                                         uint32_t *__restrict__ table0) {
     __shared__ uint32_t sh[kNumPos * kRadix];
+    __shared__ uint32_t sh0[kRadix];  // this block's digit-0 totals over its chunks
+    constexpr int64_t CH = chunk_rows(COLS);
+    constexpr int U = 8;
     const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < kNumPos * kRadix; i += 512) sh[i] = 0;
+    for (int i = tid; i < kRadix; i += 512) sh0[i] = 0;
     __syncthreads();
-    constexpr int U = 4;
-    const int64_t stride = (int64_t)gridDim.x * 512 * U;
-    for (int64_t r0 = (int64_t)blockIdx.x * 512 * U; r0 < n; r0 += stride) {
-        int64_t key[U], sv[U];
-        bool v[U];
+    const int64_t nchunks = (n + CH - 1) / CH;
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const int64_t begin = chunk * CH, end = min(begin + CH, n);
+        for (int64_t r0 = begin; r0 < end; r0 += 512 * U) {
+            int64_t key[U], sv[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int64_t r = r0 + u * 512 + tid;
-            v[u] = r < n;
-            key[u] = v[u] ? src[r * COLS + key_col] : 0;
-            sv[u] = (v[u] && use_select) ? src[r * COLS + sel_col] : 0;
-        }
+            for (int u = 0; u < U; u++) {
+                const int64_t r = min(r0 + u * 512 + tid, end - 1);  // clamped: no branches around loads
+                key[u] = src[r * COLS + key_col];
+                sv[u] = src[r * COLS + sel_col];
+            }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool ok = v[u] && (!use_select || sv[u] > sel_val);
-            const uint64_t act = __ballot(ok);
-            if (act == 0) continue;
-            const int leader = __ffsll((unsigned long long)act) - 1;
-            const uint64_t x = biased(key[u]) - base;
+            for (int u = 0; u < U; u++) {
+                const int64_t r = r0 + u * 512 + tid;
+                const bool ok = r < end && (!use_select || sv[u] > sel_val);
+                const uint64_t act = __ballot(ok);
+                if (act == 0) continue;
+                const int leader = __ffsll((unsigned long long)act) - 1;
+                const uint64_t x = biased(key[u]) - base;
 #pragma unroll
-            for (int ps = 0; ps < kNumPos; ps++) {
-                const uint32_t d = (uint32_t)(x >> (ps * kRadixBits)) & (kRadix - 1);
-                const uint32_t dl = __shfl(d, leader, 64);
-                const uint64_t same = __ballot(ok && d == dl);
-                if (same == act) {
-                    if (lane == leader) atomicAdd(&sh[ps * kRadix + dl], (uint32_t)__popcll(act));
-                } else if (ok) {
-                    atomicAdd(&sh[ps * kRadix + d], 1u);
+                for (int ps = 0; ps < kNumPos; ps++) {
+                    const uint32_t d = (uint32_t)(x >> (ps * kRadixBits)) & (kRadix - 1);
+                    const uint32_t dl = __shfl(d, leader, 64);
+                    const uint64_t same = __ballot(ok && d == dl);
+                    if (same == act) {
+                        if (lane == leader) atomicAdd(&sh[ps * kRadix + dl], (uint32_t)__popcll(act));
+                    } else if (ok) {
+                        atomicAdd(&sh[ps * kRadix + d], 1u);
+                    }
                 }
             }
         }
+        __syncthreads();
+        for (int i = tid; i < kRadix; i += 512) {
+            const uint32_t c = sh[i];
+            table0[chunk * kRadix + i] = c;
+            sh0[i] += c;
+            sh[i] = 0;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     for (int i = tid; i < kNumPos * kRadix; i += 512) {
-        const uint32_t c = sh[i];
+        const uint32_t c = i < kRadix ? sh0[i] : sh[i];
         if (c) atomicAdd(&ghist[i], c);
     }
 }
@@ -581,16 +620,18 @@ __device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t *s
 }
 
 __global__ __launch_bounds__(1024) void plan_kernel(uint32_t *ghist, SortPlan *plan) {
+    static_assert(kRadix <= 1024, "plan_kernel: one thread per digit");
     __shared__ uint32_t scratch[16];
     __shared__ int s_np;
     __shared__ int s_pos[8];
     const int tid = threadIdx.x;
-    const uint32_t m = block_sum_1024(ghist[tid], scratch);
+    const bool mine = tid < kRadix;
+    const uint32_t m = block_sum_1024(mine ? ghist[tid] : 0u, scratch);
     if (tid == 0) s_np = 0;
     __syncthreads();
     for (int ps = 0; ps < kNumPos; ps++) {
-        const uint32_t mx = block_max_1024(ghist[ps * kRadix + tid], scratch);
-        if (tid == 0 && m > 0 && mx < m) s_pos[s_np++] = ps;
+        const uint32_t mx = block_max_1024(mine ? ghist[ps * kRadix + tid] : 0u, scratch);
+        if (tid == 0 && m > 0 && mx < m && s_np < 8) s_pos[s_np++] = ps;
         __syncthreads();
     }
     if (tid == 0 && s_np == 0) { s_pos[0] = 0; s_np = 1; }  // still one pass: it compacts
@@ -598,8 +639,8 @@ __global__ __launch_bounds__(1024) void plan_kernel(uint32_t *ghist, SortPlan *p
     const int np = s_np;
     for (int k = 0; k < np; k++) {
         uint32_t *h = ghist + s_pos[k] * kRadix;
-        const uint32_t e = block_excl_scan_1024(h[tid], scratch);
-        h[tid] = e;
+        const uint32_t e = block_excl_scan_1024(mine ? h[tid] : 0u, scratch);
+        if (mine) h[tid] = e;
     }
     if (tid == 0) {
         plan->m = m;
@@ -660,10 +701,10 @@ __global__ __launch_bounds__(512) void hist_bucket_kernel(const int64_t *__restr
 __global__ __launch_bounds__(256) void merge_partition_kernel(const int64_t *__restrict__ a, int64_t na, int ca,
                                                               int ka, const int64_t *__restrict__ b, int64_t nb,
                                                               int cb, int kb, int64_t *apart, int64_t *run_start,
-                                                              int64_t ntiles) {
+                                                              int64_t ntiles, int tile) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
-    const int64_t d = min(t * (int64_t)kJoinTile, na + nb);
+    const int64_t d = min(t * (int64_t)tile, na + nb);
     int64_t lo = max((int64_t)0, d - nb), hi = min(d, na);
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
@@ -718,65 +759,80 @@ struct JoinParams {
     uint32_t *counts;    // [ntiles]
     int64_t nr, ns, ntiles;
     int c1, key1, c2, key2;
+    int jt;              // merged elements per tile (join_tile_size)
 };
 
+// Both pieces of a tile are staged in LDS as whole rows (one coalesced read
+// of R and S; the output gathers then never go back to HBM).
+constexpr int kJoinLdsWords = 8192;  // 64 KiB
+
 __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParams p) {
-    __shared__ int64_t s_keys[kJoinTile];  // tile keys; then the staged output rows
+    __shared__ __attribute__((aligned(16))) int64_t s_rows[kJoinLdsWords];
     __shared__ uint32_t s_scan[kJoinThreads / 64];
-    __shared__ int64_t s_lbr0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t tile = blockIdx.x;
     const int64_t L = p.nr + p.ns;
-    const int64_t d0 = tile * kJoinTile, d1 = min(d0 + kJoinTile, L);
+    const int64_t d0 = tile * p.jt, d1 = min(d0 + p.jt, L);
     const int64_t a0 = p.apart[tile], a1 = p.apart[tile + 1];
     const int64_t b0 = d0 - a0, b1 = d1 - a1;
     const int nR = (int)(a1 - a0), nS = (int)(b1 - b0), nM = nR + nS;
-    for (int j = tid; j < nM; j += kJoinThreads)
-        s_keys[j] = j < nR ? p.R[(a0 + j) * p.c1 + p.key1] : p.S[(b0 + j - nR) * p.c2 + p.key2];
-    if (tid == 0) s_lbr0 = p.run_start[tile];
+    const int c1 = p.c1, c2 = p.c2, k1 = p.key1, k2 = p.key2;
+    const int sbase = nR * c1;  // S piece starts here in s_rows
+    {
+        const int64_t *rs = p.R + a0 * c1;
+        const int64_t *ss = p.S + b0 * c2;
+        for (int j = tid; j < sbase; j += kJoinThreads) s_rows[j] = rs[j];
+        for (int j = tid; j < nS * c2; j += kJoinThreads) s_rows[sbase + j] = ss[j];
+    }
+    const int64_t lbr0 = p.run_start[tile];
     __syncthreads();
 
-    const int64_t *rk = s_keys;
-    const int64_t *sk = s_keys + nR;
     // this thread's merged elements [m0, m1): merge-path split inside the tile
-    const int m0 = min(tid * kJoinPer, nM), m1 = min(m0 + kJoinPer, nM);
+    const int per = p.jt / kJoinThreads;
+    const int m0 = min(tid * per, nM), m1 = min(m0 + per, nM);
     int ai, bi;
     {
         int lo = max(0, m0 - nS), hi = min(m0, nR);
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (rk[mid] <= sk[m0 - 1 - mid]) lo = mid + 1; else hi = mid;
+            if (s_rows[mid * c1 + k1] <= s_rows[sbase + (m0 - 1 - mid) * c2 + k2]) lo = mid + 1; else hi = mid;
         }
         ai = lo;
         bi = m0 - lo;
     }
     int64_t lbr = 0, prev = 0;
     bool have_prev = false;
-    uint32_t mmask = 0, cnt = 0;
-    int32_t mrow[kJoinPer];   // R row (tile-local) of the q-th match
-    int64_t mpart[kJoinPer];  // its S partner
+    uint32_t mmask = 0;
+    int32_t mrow[kJoinPer];   // R row (tile-local) of the q-th element if it matched
+    int64_t mpart[kJoinPer];  // its S partner (global row)
 #pragma unroll
     for (int q = 0; q < kJoinPer; q++) {
         mrow[q] = 0;
         mpart[q] = 0;
         if (m0 + q < m1) {
-            const bool takeR = ai < nR && (bi >= nS || rk[ai] <= sk[bi]);
+            const int64_t rkey = ai < nR ? s_rows[ai * c1 + k1] : 0;
+            const bool takeR = ai < nR && (bi >= nS || rkey <= s_rows[sbase + bi * c2 + k2]);
             if (takeR) {
-                const int64_t k = rk[ai];
-                if (!have_prev || k != prev) {
+                if (!have_prev || rkey != prev) {
                     if (have_prev) {
                         lbr = a0 + ai;  // a new run starts here
-                    } else {        // first R row of this thread: search the run start
-                        const int lb = lds_lower_bound(rk, ai, k);
-                        lbr = lb == 0 ? s_lbr0 : a0 + lb;
+                    } else {        // first R row of this thread: find the run start
+                        int lo = 0, hi = ai;
+                        while (lo < hi) {
+                            const int mid = (lo + hi) >> 1;
+                            if (s_rows[mid * c1 + k1] < rkey) lo = mid + 1; else hi = mid;
+                        }
+                        lbr = lo == 0 ? lbr0 : a0 + lo;
                     }
-                    prev = k;
+                    prev = rkey;
                     have_prev = true;
                 }
+                // S rows merged before this R row are exactly those with a smaller key
                 const int64_t pidx = b0 + bi + (a0 + ai - lbr);
                 if (pidx < p.ns) {
-                    const int64_t skey = pidx < b1 ? sk[pidx - b0] : p.S[pidx * p.c2 + p.key2];
-                    if (skey == k) {
+                    const int64_t skey = pidx < b1 ? s_rows[sbase + (int)(pidx - b0) * c2 + k2]
+                                                   : p.S[pidx * c2 + k2];
+                    if (skey == rkey) {
                         mrow[q] = ai;
                         mpart[q] = pidx;
                         mmask |= 1u << q;
@@ -788,7 +844,7 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
             }
         }
     }
-    cnt = __popc(mmask);
+    const uint32_t cnt = __popc(mmask);
     // block exclusive scan of match counts
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (lane == 63) s_scan[wave] = incl;
@@ -802,35 +858,18 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     }
     off += incl - cnt;
     if (tid == 0) p.counts[tile] = total;
-    const int tc = p.c1 + p.c2 - 1;
-    if ((int64_t)total * tc <= kJoinTile) {
-        // stage the tile's output rows in LDS (the keys are dead: every read of
-        // them happened before the scan barrier above), then one coalesced copy
+    // output rows: consecutive threads own consecutive slot rows
+    const int tc = c1 + c2 - 1;
 #pragma unroll
-        for (int q = 0; q < kJoinPer; q++) {
-            if ((mmask >> q) & 1u) {
-                int64_t *dst = s_keys + (size_t)(off + __popc(mmask & ((1u << q) - 1u))) * tc;
-                const int64_t *rr = p.R + (a0 + mrow[q]) * p.c1;
-                const int64_t *ss = p.S + mpart[q] * p.c2;
-                for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
-                for (int c = 0, k = p.c1; c < p.c2; c++)
-                    if (c != p.key2) dst[k++] = ss[c];
-            }
-        }
-        __syncthreads();
-        int64_t *out = p.slots + a0 * tc;
-        for (uint32_t i = tid; i < total * tc; i += kJoinThreads) out[i] = s_keys[i];
-    } else {
-#pragma unroll
-        for (int q = 0; q < kJoinPer; q++) {
-            if ((mmask >> q) & 1u) {
-                int64_t *dst = p.slots + (a0 + off + __popc(mmask & ((1u << q) - 1u))) * tc;
-                const int64_t *rr = p.R + (a0 + mrow[q]) * p.c1;
-                const int64_t *ss = p.S + mpart[q] * p.c2;
-                for (int c = 0; c < p.c1; c++) dst[c] = rr[c];
-                for (int c = 0, k = p.c1; c < p.c2; c++)
-                    if (c != p.key2) dst[k++] = ss[c];
-            }
+    for (int q = 0; q < kJoinPer; q++) {
+        if ((mmask >> q) & 1u) {
+            int64_t *dst = p.slots + (a0 + off + __popc(mmask & ((1u << q) - 1u))) * tc;
+            const int64_t *rr = s_rows + mrow[q] * c1;
+            const int64_t pl = mpart[q] - b0;
+            const bool local = mpart[q] < b1;
+            for (int c = 0; c < c1; c++) dst[c] = rr[c];
+            for (int c = 0, k = c1; c < c2; c++)
+                if (c != k2) dst[k++] = local ? s_rows[sbase + (int)pl * c2 + c] : p.S[mpart[q] * c2 + c];
         }
     }
 }
@@ -1007,11 +1046,11 @@ static BucketDigit make_bucket(const int64_t *spl, int nspl) {
 }
 
 hipError_t launch_hist_radix(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
-                             int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist,
+                             int64_t sel_val, int key_col, uint64_t key_base, uint32_t *ghist, uint32_t *table0,
                              hipStream_t s) {
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, 2048), 1024));
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, chunk_rows(cols)), 1024));
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((hist_radix_kernel<C>), dim3(grid), dim3(512), 0, s, src, n,
-                                             use_select, sel_col, sel_val, key_col, key_base, ghist));
+                                             use_select, sel_col, sel_val, key_col, key_base, ghist, table0));
     return hipGetLastError();
 }
 
@@ -1043,17 +1082,18 @@ int64_t pass_chunks(const PassSpec &ps) { return (ps.nsrc + chunk_rows(ps.cols) 
         const int dbg = debug_bits("SMJ_DEBUG_PASS");                                                      \
         if (ps.kind == DIGIT_RADIX) {                                                                      \
             PassParams<RadixDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,        \
-                                     ps.key_col, dbg, RadixDigit{ps.key_base, ps.shift}, table, ctr};      \
+                                     ps.key_col, dbg, RadixDigit{ps.key_base, ps.shift}, table, ctr,       \
+                                     ps.trash};                                                            \
             SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, kRadixBits, RadixDigit>), dim3(grid),    \
                                                         dim3(BLOCK), 0, s, p));                           \
         } else if (ps.kind == DIGIT_BUCKET) {                                                              \
             PassParams<BucketDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,       \
-                                      ps.key_col, dbg, make_bucket(ps.spl, ps.nspl), table, ctr};          \
+                                      ps.key_col, dbg, make_bucket(ps.spl, ps.nspl), table, ctr, ps.trash}; \
             SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, kBucketBits, BucketDigit>), dim3(grid),  \
                                                         dim3(BLOCK), 0, s, p));                           \
         } else {                                                                                           \
             PassParams<ZeroDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,         \
-                                    ps.key_col, dbg, ZeroDigit{}, table, ctr};                             \
+                                    ps.key_col, dbg, ZeroDigit{}, table, ctr, ps.trash};                   \
             SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, 0, ZeroDigit>), dim3(grid), dim3(BLOCK), \
                                                         0, s, p));                                         \
         }                                                                                                  \
@@ -1082,9 +1122,9 @@ hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *c
 
 hipError_t launch_merge_partition(const int64_t *a, int64_t na, int ca, int ka, const int64_t *b,
                                   int64_t nb, int cb, int kb, int64_t *apart, int64_t *run_start, int64_t ntiles,
-                                  hipStream_t s) {
+                                  int tile, hipStream_t s) {
     hipLaunchKernelGGL(merge_partition_kernel, dim3(blocks_for(ntiles + 1, 256)), dim3(256), 0, s, a, na, ca, ka, b,
-                       nb, cb, kb, apart, run_start, ntiles);
+                       nb, cb, kb, apart, run_start, ntiles, tile);
     return hipGetLastError();
 }
 
@@ -1093,7 +1133,7 @@ hipError_t launch_join(const int64_t *R, int64_t nr, int c1, int key1, const int
                        uint32_t *counts, uint32_t *offs, int64_t *out, int64_t *out_rows, int phase,
                        hipStream_t s) {
     if (phase == 0) {
-        JoinParams p{R, S, apart, run_start, slots, counts, nr, ns, ntiles, c1, key1, c2, key2};
+        JoinParams p{R, S, apart, run_start, slots, counts, nr, ns, ntiles, c1, key1, c2, key2, join_tile_size(c1, c2)};
         hipLaunchKernelGGL(join_tile_kernel, dim3((unsigned)ntiles), dim3(kJoinThreads), 0, s, p);
     } else if (phase == 1) {
         hipLaunchKernelGGL(join_scan_kernel, dim3(1), dim3(1024), 0, s, counts, ntiles, offs, out_rows);

@@ -17,7 +17,14 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
         ops.join(Rs, Ss, out=J, count=c, sync=False)
     torch.cuda.synchronize()
     rep = ops.prof_report()
-    print(json.dumps({k: round(v["ms"] / v["launches"], 4) for k, v in rep.items()}))
+    k, pay = Rs[:, 0], Rs[:, 1]
+    ok = bool((k[1:] >= k[:-1]).all()) and bool(((k[1:] > k[:-1]) | (pay[1:] > pay[:-1])).all())
+    jn = int(c.item())
+    res = {k2: round(v["ms"] / v["launches"], 4) for k2, v in rep.items()}
+    res["_sorted_stable"] = ok
+    res["_joined"] = jn
+    res["_ms_step"] = round(sum(v["ms"] for v in rep.values()) / 3, 3)
+    print(json.dumps(res))
     sys.exit(0)
 CONFIGS = [{}, {"SMJ_DEBUG_PASS": "1", "SMJ_DEBUG_JOIN": "1"}, {"SMJ_DEBUG_PASS": "2"}, {"SMJ_DEBUG_PASS": "3"},
            {"SMJ_DEBUG_PASS": "4"}, {"SMJ_DEBUG_PASS": "5"}]
