@@ -70,10 +70,16 @@ __device__ __forceinline__ void store_row(int64_t *__restrict__ p, const int64_t
 // access, which demotes the whole row array to scratch memory.
 template <int COLS>
 __device__ __forceinline__ int64_t pick(const int64_t (&r)[COLS], int col) {
-    int64_t v = 0;
+    if constexpr (COLS == 1) {
+        return r[0];
+    } else if constexpr (COLS == 2) {
+        return col ? r[1] : r[0];  // one uniform select: two v_cndmask
+    } else {
+        int64_t v = 0;
 #pragma unroll
-    for (int c = 0; c < COLS; c++) v |= r[c] & -(int64_t)(col == c);
-    return v;
+        for (int c = 0; c < COLS; c++) v |= r[c] & -(int64_t)(col == c);
+        return v;
+    }
 }
 
 __device__ __forceinline__ uint32_t ld_status(const uint32_t *p) {
@@ -135,11 +141,11 @@ __device__ __forceinline__ int lds_upper_bound(const int64_t *a, int n, int64_t 
 // ---------------------------------------------------------------------------
 // digit functors
 // ---------------------------------------------------------------------------
-struct RadixDigit {   // digit of the biased key, relative to a base
-    uint64_t base;
+struct RadixDigit {   // digit of the biased key relative to a base: ((key ^ 2^63) - base) >> shift
+    uint64_t kbase;   // base ^ 2^63, so that the digit is (key - kbase) >> shift (mod 2^64)
     int shift;
     __device__ __forceinline__ uint32_t operator()(int64_t key) const {
-        return (uint32_t)((biased(key) - base) >> shift);
+        return (uint32_t)(((uint64_t)key - kbase) >> shift);
     }
 };
 struct ZeroDigit {    // select-only compaction: one bin
@@ -188,11 +194,13 @@ struct PassLds {
     static constexpr int CNT_BYTES = kSortWaves * RADIX * 4;
     static constexpr int A = ROW_BYTES > CNT_BYTES ? ROW_BYTES : CNT_BYTES;
     static constexpr int R16 = ((RADIX * 4 + 15) / 16) * 16;
-    static constexpr int OFF_BIN = A;              // u32 tile-local digit starts
+    static constexpr int OFF_DIG = A;              // u16 digit of every staged row (slot order)
+    static constexpr int OFF_BIN = OFF_DIG + ((TILE * 2 + 15) / 16) * 16;  // u32 tile-local digit starts
     static constexpr int OFF_ADJ = OFF_BIN + R16;  // i32 global - local offset per digit
     static constexpr int OFF_RUN = OFF_ADJ + R16;  // i32 running global offset per digit
     static constexpr int OFF_MISC = OFF_RUN + R16;
-    static constexpr int BYTES = OFF_MISC + 128;
+    static constexpr int OFF_PH = OFF_MISC + 128;  // u64[16] phase stamps (SMJ_DEBUG_PASS bit 3)
+    static constexpr int BYTES = OFF_PH + 128;
 };
 
 // Rows past `end` are loaded from row end-1 instead (and masked out by the
@@ -312,12 +320,15 @@ __global__ __launch_bounds__(256) void chunk_scan_apply_kernel(uint32_t *__restr
 // Tiles of the chunk are taken in order; the next tile's rows are loaded into
 // registers while the current one is ranked and scattered.  Per tile:
 //   rank     stable digit ranks: DBITS ballots per 64-row item find the lanes
-//            with the same digit; per-wave running counters in LDS order the
+//            with the same digit (one v_bitop3 per ballot half folds each bit
+//            into the peer mask); per-wave running counters in LDS order the
 //            items of a wave; a cross-wave prefix orders the waves;
-//   stage    rows are written to LDS in digit order (block scan of the digit
-//            totals gives each digit's local start);
+//   stage    rows (and their digits, u16) are written to LDS in digit order
+//            (block scan of the digit totals gives each digit's local start);
 //   scatter  consecutive LDS rows of one digit leave as one contiguous run at
 //            the digit's running global offset.
+// Every wave zeroes only its own counter row, so no barrier separates the
+// zeroing from the ranking.  Row offsets inside a chunk are 32-bit.
 // Diagnostic phase stamps (SMJ_DEBUG_PASS bit 3): cycles between the
 // barriers of chunk_scatter, summed over workgroups (thread 0's view).
 __device__ unsigned long long g_phase_cycles[16];
@@ -325,34 +336,51 @@ __device__ unsigned long long g_phase_cycles[16];
     if (p.dbg & 8) {                                                       \
         if (tid == 0) {                                                    \
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
-            ph[k] += t_ - t_last;                                          \
-            t_last = t_;                                                   \
+            s_ph[k] += t_ - s_ph[15];                                      \
+            s_ph[15] = t_;                                                 \
         }                                                                  \
     }
+
+// a wave zeroes its own row of digit counters
+template <int RADIX>
+__device__ __forceinline__ void zero_counters(uint32_t *wc, int lane) {
+    if constexpr (RADIX % 4 == 0) {
+        for (int i = lane; i < RADIX / 4; i += 64) reinterpret_cast<uint4 *>(wc)[i] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int i = lane; i < RADIX; i += 64) wc[i] = 0;
+    }
+}
+
+// p &= ~(ballot ^ s) on one 32-bit half (s = 0 or ~0: this lane's bit)
+__device__ __forceinline__ uint32_t peer_fold(uint32_t p, uint32_t ballot_half, uint32_t s) {
+    return __builtin_amdgcn_bitop3_b32(p, ballot_half, s, 0x90);
+}
 
 template <int COLS, int DBITS, class DigitF>
 __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const PassParams<DigitF> p) {
     using L = PassLds<COLS, DBITS>;
     constexpr int RADIX = L::RADIX;
     constexpr int ITEMS = sort_items(COLS);
-    constexpr int TILE = L::TILE;
+    constexpr uint32_t TILE = L::TILE;
     constexpr int64_t CH = chunk_rows(COLS);
     constexpr uint32_t MASK = RADIX - 1;
-    constexpr int BPT = RADIX > kSortThreads ? RADIX / kSortThreads : 1;  // digits d = tid + j*512
+    constexpr int BPT = RADIX > kSortThreads ? RADIX / kSortThreads : 1;  // digits d = tid + j*kSortThreads
 
     __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
     int64_t *s_rows = reinterpret_cast<int64_t *>(smem);          // staging tile (after ranking)
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(smem);        // [wave][digit] counters (ranking)
+    uint16_t *s_dig = reinterpret_cast<uint16_t *>(smem + L::OFF_DIG);
     uint32_t *s_binstart = reinterpret_cast<uint32_t *>(smem + L::OFF_BIN);
     int32_t *s_adj = reinterpret_cast<int32_t *>(smem + L::OFF_ADJ);
     int32_t *s_run = reinterpret_cast<int32_t *>(smem + L::OFF_RUN);
     uint32_t *s_misc = reinterpret_cast<uint32_t *>(smem + L::OFF_MISC);
+    unsigned long long *s_ph = reinterpret_cast<unsigned long long *>(smem + L::OFF_PH);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t begin = (int64_t)blockIdx.x * CH;
-    const int64_t end = min(begin + CH, p.nsrc);
-    const int64_t lane_row = (int64_t)wave * (ITEMS * 64) + lane;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t clen = (uint32_t)min(CH, p.nsrc - begin);  // rows of this chunk (>= 1)
+    const int64_t *src = p.src + begin * COLS;
+    const uint32_t lane_row = (uint32_t)wave * (ITEMS * 64) + lane;
     uint32_t *wc = s_wcnt + wave * RADIX;
 
 #pragma unroll
@@ -360,8 +388,10 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         const int d = tid + j * kSortThreads;
         if (d < RADIX) s_run[d] = (int32_t)p.table[(size_t)blockIdx.x * RADIX + d];
     }
+    zero_counters<RADIX>(wc, lane);
     int64_t rows[ITEMS][COLS];
-    load_tile<COLS, ITEMS>(p.src, end, begin + lane_row, rows);
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) load_row<COLS>(src + (int64_t)min(lane_row + it * 64, clen - 1) * COLS, rows[it]);
     // ITEMS dummy stores behind the first loads: the loop is then always
     // entered with (loads, then ITEMS stores) in flight, exactly as from its
     // back edge, so hipcc's vmcnt waits for the rows skip the stores
@@ -373,23 +403,23 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         store_row<COLS>(p.trash + ((size_t)it * kSortThreads + tid) * COLS, z);
     }
     uint32_t chunk_total = 0;
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long t_last = (p.dbg & 8) ? __builtin_amdgcn_s_memtime() : 0;
+    if ((p.dbg & 8) && tid == 0) {
+        for (int k = 0; k < 15; k++) s_ph[k] = 0;
+        s_ph[15] = __builtin_amdgcn_s_memtime();
+    }
+    __syncthreads();  // s_run published
 
-    for (int64_t tile0 = begin;;) {
-        for (int i = tid; i < kSortWaves * RADIX / 4; i += kSortThreads)
-            reinterpret_cast<uint4 *>(s_wcnt)[i] = make_uint4(0, 0, 0, 0);
-        __syncthreads();  // B1 (also publishes s_run on the first tile)
+    for (uint32_t tile0 = 0;;) {
         SMJ_STAMP(0);
-
         // ---- digits (select predicate fused into pass 0)
-        const int64_t row0 = tile0 + lane_row;
+        const uint32_t row0 = tile0 + lane_row;
         uint32_t dig[ITEMS];
         uint32_t vmask = 0;
 #pragma unroll
-        for (int it = 0; it < ITEMS; it++) {
-            bool v = row0 + it * 64 < end;
-            if (p.use_select) v = v && (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+        for (int it = 0; it < ITEMS; it++) {  // branch-free: every term is computed
+            const bool inb = row0 + it * 64 < clen;
+            const bool pass = !p.use_select | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+            const bool v = inb & pass;
             dig[it] = v ? (p.digit(pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
@@ -397,18 +427,23 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const bool v = (vmask >> it) & 1u;
-            uint64_t peers = __ballot(v);
+            const uint64_t act = __ballot(v);
+            uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
+            const uint32_t dd = dig[it];
 #pragma unroll
             for (int b = 0; b < DBITS; b++) {
-                const bool bit = (dig[it] >> b) & 1u;
-                const uint64_t bb = __ballot(bit);
-                peers &= bit ? bb : ~bb;
+                const uint32_t sb = (uint32_t)((int32_t)(dd << (31 - b)) >> 31);  // ~0 iff bit b
+                const uint64_t bb = __ballot(sb != 0u);
+                plo = peer_fold(plo, (uint32_t)bb, sb);
+                phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
             }
             if (v) {
-                const uint32_t base = wc[dig[it]];
-                const uint32_t rank = base + (uint32_t)__popcll(peers & lt_mask);
-                if ((peers >> lane) == 1ull) wc[dig[it]] = base + (uint32_t)__popcll(peers);
-                dig[it] |= rank << 16;
+                const uint32_t base = wc[dd];
+                // lanes below this one with the same digit (mbcnt), and the last of them
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, base));
+                const uint64_t peers = ((uint64_t)phi << 32) | plo;
+                if ((peers >> lane) == 1ull) wc[dd] = base + (uint32_t)__popcll(peers);
+                dig[it] = dd | (rank << 16);
             }
         }
         __syncthreads();  // B2
@@ -454,22 +489,33 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         __syncthreads();  // B4
         SMJ_STAMP(3);
 
-        // ---- tile-local destinations
+        // ---- tile-local slots: dig[it] becomes (digit << 16) | slot
 #pragma unroll
-        for (int it = 0; it < ITEMS; it++) {  // dig[it] becomes the LDS slot
+        for (int it = 0; it < ITEMS; it++) {
             const uint32_t d = dig[it] & 0xffffu;
-            dig[it] = ((vmask >> it) & 1u) ? s_binstart[d] + wc[d] + (dig[it] >> 16) : 0u;
+            const uint32_t slot = s_binstart[d] + wc[d] + (dig[it] >> 16);
+            dig[it] = (d << 16) | slot;
         }
-        const int64_t next0 = tile0 + TILE;
+        const uint32_t next0 = tile0 + TILE;
         __syncthreads();  // B5: counters dead, the region becomes the staging tile
         SMJ_STAMP(4);
-    #pragma unroll
-        for (int it = 0; it < ITEMS; it++)
-            if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            if ((vmask >> it) & 1u) {
+                const uint32_t slot = dig[it] & 0xffffu;
+                store_row<COLS>(s_rows + (size_t)slot * COLS, rows[it]);
+                s_dig[slot] = (uint16_t)(dig[it] >> 16);
+            }
+        }
         // the rows are staged: their registers now take the next tile's rows,
         // in flight while this tile is scattered (after the last tile: an
         // L2-hot reload of this one -- unconditional, so vmcnt stays exact)
-        load_tile<COLS, ITEMS>(p.src, end, (next0 < end ? next0 : tile0) + lane_row, rows);
+        {
+            const uint32_t nrow0 = (next0 < clen ? next0 : tile0) + lane_row;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                load_row<COLS>(src + (int64_t)min(nrow0 + it * 64, clen - 1) * COLS, rows[it]);
+        }
 #pragma unroll
         for (int j = 0; j < BPT; j++) {
             const int d = tid + j * kSortThreads;
@@ -489,26 +535,31 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         // writes its (garbage) slots to the trash buffer
         {
             const bool any = tile_total > 0;
+            uint32_t slot[ITEMS], d[ITEMS];
 #pragma unroll
             for (int it = 0; it < ITEMS; it++) {
-                const uint32_t i = any ? min((uint32_t)(tid + it * kSortThreads), tile_total - 1u) : 0u;
+                slot[it] = any ? min((uint32_t)(tid + it * kSortThreads), tile_total - 1u) : 0u;
+                d[it] = s_dig[slot[it]];
+            }
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
                 int64_t r[COLS];
-                load_row<COLS>(s_rows + (size_t)i * COLS, r);
-                const uint32_t d = p.digit(pick<COLS>(r, p.key_col)) & MASK;
-                int64_t *q = any ? p.dst + ((int64_t)s_adj[d] + (int64_t)i) * COLS
-                                 : p.trash + ((size_t)it * kSortThreads + tid) * COLS;
+                load_row<COLS>(s_rows + (size_t)slot[it] * COLS, r);
+                const int64_t g = (int64_t)s_adj[d[it]] + (int64_t)slot[it];
+                int64_t *q = any ? p.dst + g * COLS : p.trash + ((size_t)it * kSortThreads + tid) * COLS;
                 store_row<COLS>(q, r);
             }
         }
         SMJ_STAMP(6);
-        ph[7]++;
-        if (next0 >= end) break;
-        __syncthreads();  // B0: staging tile read before it is zeroed again
+        if ((p.dbg & 8) && tid == 0) s_ph[7]++;
+        if (next0 >= clen) break;
+        __syncthreads();  // B0: staging tile read before it becomes counters again
+        zero_counters<RADIX>(wc, lane);
         tile0 = next0;
     }
     if (tid == 0 && chunk_total) atomicAdd(&p.ctr->count, chunk_total);
     if ((p.dbg & 8) && tid == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], ph[k]);
+        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], s_ph[k]);
 }
 
 // ---------------------------------------------------------------------------
@@ -762,13 +813,29 @@ struct JoinParams {
     int jt;              // merged elements per tile (join_tile_size)
 };
 
-// Both pieces of a tile are staged in LDS as whole rows (one coalesced read
-// of R and S; the output gathers then never go back to HBM).
-constexpr int kJoinLdsWords = 8192;  // 64 KiB
+// Both pieces of a tile are staged in LDS as whole rows: one read of R and S
+// whose loads are all in flight together (kJoinLoads unrolled, clamped, no
+// branches around them).  The matches are then listed in LDS in output order
+// and the slot rows leave as consecutive 8-B words, every lane of a store
+// instruction on the next address.  LDS: 64 KiB of rows + 16 KiB of match list
+// = 80 KiB, so two workgroups share a CU (one loads while the other walks).
+constexpr int kJoinLdsWords = 8192;                       // 64 KiB
+constexpr int kJoinLoads = kJoinLdsWords / kJoinThreads;  // 16 words per thread
+constexpr uint32_t kMatchFar = 0xFFFFFu;  // list entry: (R row << 20) | (partner - b0), or this escape
+
+// first row of a strided LDS piece whose word `col` is >= k
+__device__ __forceinline__ int lds_lower_bound_rows(const int64_t *a, int stride, int col, int n, int64_t k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid * stride + col] < k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
 
 __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParams p) {
     __shared__ __attribute__((aligned(16))) int64_t s_rows[kJoinLdsWords];
-    __shared__ uint32_t s_scan[kJoinThreads / 64];
+    __shared__ uint32_t s_match[kJoinLdsWords / 2];  // first holds the wave sums of the count scan
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t tile = blockIdx.x;
     const int64_t L = p.nr + p.ns;
@@ -777,12 +844,22 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     const int64_t b0 = d0 - a0, b1 = d1 - a1;
     const int nR = (int)(a1 - a0), nS = (int)(b1 - b0), nM = nR + nS;
     const int c1 = p.c1, c2 = p.c2, k1 = p.key1, k2 = p.key2;
-    const int sbase = nR * c1;  // S piece starts here in s_rows
+    const int sbase = nR * c1;            // S piece starts here in s_rows
+    const int nwords = sbase + nS * c2;   // >= 1: a tile is never empty
     {
         const int64_t *rs = p.R + a0 * c1;
         const int64_t *ss = p.S + b0 * c2;
-        for (int j = tid; j < sbase; j += kJoinThreads) s_rows[j] = rs[j];
-        for (int j = tid; j < nS * c2; j += kJoinThreads) s_rows[sbase + j] = ss[j];
+        int64_t v[kJoinLoads];
+#pragma unroll
+        for (int u = 0; u < kJoinLoads; u++) {
+            const int j = min(tid + u * kJoinThreads, nwords - 1);
+            v[u] = j < sbase ? rs[j] : ss[j - sbase];
+        }
+#pragma unroll
+        for (int u = 0; u < kJoinLoads; u++) {
+            const int j = tid + u * kJoinThreads;
+            if (j < nwords) s_rows[j] = v[u];
+        }
     }
     const int64_t lbr0 = p.run_start[tile];
     __syncthreads();
@@ -803,12 +880,10 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
     int64_t lbr = 0, prev = 0;
     bool have_prev = false;
     uint32_t mmask = 0;
-    int32_t mrow[kJoinPer];   // R row (tile-local) of the q-th element if it matched
-    int64_t mpart[kJoinPer];  // its S partner (global row)
+    uint32_t ment[kJoinPer];  // list entry of the q-th element if it matched
 #pragma unroll
     for (int q = 0; q < kJoinPer; q++) {
-        mrow[q] = 0;
-        mpart[q] = 0;
+        ment[q] = 0;
         if (m0 + q < m1) {
             const int64_t rkey = ai < nR ? s_rows[ai * c1 + k1] : 0;
             const bool takeR = ai < nR && (bi >= nS || rkey <= s_rows[sbase + bi * c2 + k2]);
@@ -817,11 +892,7 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
                     if (have_prev) {
                         lbr = a0 + ai;  // a new run starts here
                     } else {        // first R row of this thread: find the run start
-                        int lo = 0, hi = ai;
-                        while (lo < hi) {
-                            const int mid = (lo + hi) >> 1;
-                            if (s_rows[mid * c1 + k1] < rkey) lo = mid + 1; else hi = mid;
-                        }
+                        const int lo = lds_lower_bound_rows(s_rows, c1, k1, ai, rkey);
                         lbr = lo == 0 ? lbr0 : a0 + lo;
                     }
                     prev = rkey;
@@ -833,8 +904,8 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
                     const int64_t skey = pidx < b1 ? s_rows[sbase + (int)(pidx - b0) * c2 + k2]
                                                    : p.S[pidx * c2 + k2];
                     if (skey == rkey) {
-                        mrow[q] = ai;
-                        mpart[q] = pidx;
+                        const int64_t rel = pidx - b0;
+                        ment[q] = ((uint32_t)ai << 20) | (rel < (int64_t)kMatchFar ? (uint32_t)rel : kMatchFar);
                         mmask |= 1u << q;
                     }
                 }
@@ -844,33 +915,56 @@ __global__ __launch_bounds__(kJoinThreads) void join_tile_kernel(const JoinParam
             }
         }
     }
+    // block exclusive scan of the match counts -> this thread's list offset
     const uint32_t cnt = __popc(mmask);
-    // block exclusive scan of match counts
     const uint32_t incl = wave_incl_scan(cnt, lane);
-    if (lane == 63) s_scan[wave] = incl;
+    if (lane == 63) s_match[wave] = incl;
     __syncthreads();
     uint32_t off = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < kJoinThreads / 64; w++) {
-        const uint32_t x = s_scan[w];
+        const uint32_t x = s_match[w];
         off += (w < wave) ? x : 0u;
         total += x;
     }
     off += incl - cnt;
-    if (tid == 0) p.counts[tile] = total;
-    // output rows: consecutive threads own consecutive slot rows
-    const int tc = c1 + c2 - 1;
+    __syncthreads();  // wave sums read before the list overwrites them
 #pragma unroll
-    for (int q = 0; q < kJoinPer; q++) {
-        if ((mmask >> q) & 1u) {
-            int64_t *dst = p.slots + (a0 + off + __popc(mmask & ((1u << q) - 1u))) * tc;
-            const int64_t *rr = s_rows + mrow[q] * c1;
-            const int64_t pl = mpart[q] - b0;
-            const bool local = mpart[q] < b1;
-            for (int c = 0; c < c1; c++) dst[c] = rr[c];
-            for (int c = 0, k = c1; c < c2; c++)
-                if (c != k2) dst[k++] = local ? s_rows[sbase + (int)pl * c2 + c] : p.S[mpart[q] * c2 + c];
+    for (int q = 0; q < kJoinPer; q++)
+        if ((mmask >> q) & 1u) s_match[off + __popc(mmask & ((1u << q) - 1u))] = ment[q];
+    if (tid == 0) p.counts[tile] = total;
+    __syncthreads();
+
+    // slot rows [a0, a0 + total): word w = (row o, column c), c < c1 from R,
+    // then the S columns without key2
+    const int tc = c1 + c2 - 1;
+    const uint32_t W = total * (uint32_t)tc;  // <= 4096 * 15 < 2^16: the reciprocal below is exact
+    const uint32_t magic = tc > 1 ? (uint32_t)((0x100000000ull + tc - 1) / tc) : 0u;
+    int64_t *dst = p.slots + a0 * tc;
+    for (uint32_t w = tid; w < W; w += kJoinThreads) {
+        const uint32_t o = tc > 1 ? __umulhi(w, magic) : w;
+        const int c = (int)(w - o * (uint32_t)tc);
+        const uint32_t m = s_match[o];
+        const int r = (int)(m >> 20);
+        int64_t val;
+        if (c < c1) {
+            val = s_rows[r * c1 + c];
+        } else {
+            const int j = c - c1;
+            const int sc = j + (j >= k2 ? 1 : 0);
+            int64_t part;
+            if ((m & kMatchFar) != kMatchFar) {
+                part = b0 + (m & kMatchFar);
+            } else {  // partner far past the tile (long duplicate runs): recompute it
+                const int64_t k = s_rows[r * c1 + k1];
+                const int lbs = lds_lower_bound_rows(s_rows + sbase, c2, k2, nS, k);
+                const int lo = lds_lower_bound_rows(s_rows, c1, k1, r, k);
+                const int64_t lr = lo == 0 ? lbr0 : a0 + lo;
+                part = b0 + lbs + (a0 + r - lr);
+            }
+            val = part < b1 ? s_rows[sbase + (int)(part - b0) * c2 + sc] : p.S[part * c2 + sc];
         }
+        dst[w] = val;
     }
 }
 
@@ -1082,7 +1176,7 @@ int64_t pass_chunks(const PassSpec &ps) { return (ps.nsrc + chunk_rows(ps.cols) 
         const int dbg = debug_bits("SMJ_DEBUG_PASS");                                                      \
         if (ps.kind == DIGIT_RADIX) {                                                                      \
             PassParams<RadixDigit> p{ps.src, ps.dst, ps.nsrc, ps.sel_val, ps.use_select, ps.sel_col,        \
-                                     ps.key_col, dbg, RadixDigit{ps.key_base, ps.shift}, table, ctr,       \
+                                     ps.key_col, dbg, RadixDigit{ps.key_base ^ 0x8000000000000000ull, ps.shift}, table, ctr,       \
                                      ps.trash};                                                            \
             SMJ_COLS_SWITCH(ps.cols, hipLaunchKernelGGL((KERNEL<C, kRadixBits, RadixDigit>), dim3(grid),    \
                                                         dim3(BLOCK), 0, s, p));                           \
