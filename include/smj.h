@@ -130,14 +130,31 @@ int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, 
  * on one stream).  Buffers must be distinct unless stated. */
 
 /* Stable select + sort (fused): out <- sort_stable(select(in)).  When
- * use_select == 0 every row is kept.  key_base: keys are radix-sorted on
- * (key ^ 2^63) - key_base; pass 0 unless every key is known to be >= the
- * signed value whose biased form is key_base (the multi-GPU driver passes
- * its partition's lower bound).  Blocks until the row count is known
- * (one small device->host read); *out_rows gets it. */
+ * use_select == 0 every row is kept.  Runs the MSD sample-sort pipeline
+ * (sample splitters -> two tile-local partition passes -> LDS sort of final
+ * groups); key_base is accepted for ABI stability and only used by the LSD
+ * variant below.  Blocks until the row count is known; *out_rows gets it. */
 int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
                         T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
                         void *stream);
+
+/* The same select + sort on the LSD radix path (hist -> 10-bit chunk passes);
+ * kept as the fallback of the MSD pipeline for groups it cannot sort in LDS
+ * and for comparison.  Same contract as smj_dev_select_sort. */
+int smj_dev_select_sort_lsd(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                            T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                            void *stream);
+
+/* The whole hot path on device-resident tables in one pipeline (app.c
+ * :172-692 / cpu_app.c main :303-364): select (row[sel_col] > sel_val when
+ * use_sel), stable sort on the key, and the 1:1 zip join.  R_sorted / S_sorted
+ * get the sorted selected rows (nr x c1 / ns x c2 capacity), out the joined
+ * rows (min(nr, ns) x (c1 + c2 - 1) capacity).  Synchronises once at the end
+ * (twice when oversized single-key or multi-key groups need the fallback);
+ * h_rows[0..2] = selected rows of R, of S, joined rows. */
+int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1, int key1,
+                            const T *S, int64_t ns, int c2, int use_sel2, int sel_col2, T sel_val2, int key2,
+                            T *R_sorted, T *S_sorted, T *out, int64_t *h_rows, void *stream);
 
 /* Stable select alone (a stable compaction). *out_rows is written after a
  * stream synchronisation. */
@@ -188,6 +205,12 @@ int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t 
                      double theta, double zeta_n, void *stream);
 /* sum_{i=1..n} i^-theta (host). */
 double smj_zipf_zeta(int64_t n, double theta);
+
+/* ---- diagnostics ------------------------------------------------------- */
+/* Counters of the last MSD pipeline call: out4[0] = single-key groups
+ * streamed without a sort, out4[1] = groups sorted / joined by the LSD
+ * fallback, out4[2] / out4[3] = selected rows of R / S. */
+void smj_debug_msd_stats(int64_t *out4);
 
 /* ---- profiling ---------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by hipEvents recorded on

@@ -244,7 +244,7 @@ static int run_pass(DevScratch *sc, const PassSpec &ps, const uint32_t *base, Co
 // ---------------------------------------------------------------------------
 // select + sort
 // ---------------------------------------------------------------------------
-static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+static int lsd_select_sort(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
                            int key_col, uint64_t key_base, T *out, int64_t *out_rows, hipStream_t s) {
     SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
     if (!out_rows) return SMJ_ERR_INVALID;
@@ -298,10 +298,10 @@ static int dev_select_sort(const T *in, int64_t n, int cols, int use_select, int
     return SMJ_OK;
 }
 
-extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
-                                   T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
-                                   void *stream) {
-    return dev_select_sort(in, n_rows, col_num, use_select, select_col, select_val, key_col, key_base, out,
+extern "C" int smj_dev_select_sort_lsd(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                                       T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                                       void *stream) {
+    return lsd_select_sort(in, n_rows, col_num, use_select, select_col, select_val, key_col, key_base, out,
                            out_rows, (hipStream_t)stream);
 }
 
@@ -407,6 +407,349 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
         *h_out_rows = sc->h_small[0];
     }
     return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// MSD sample-sort pipeline (smj_msd.hip): select + stable sort
+// of one or two tables and, for two, their zip join, in one pass structure
+// ---------------------------------------------------------------------------
+namespace {
+struct MsdTabScratch {
+    void *tempA = nullptr, *tempB = nullptr, *offsA = nullptr, *tmm = nullptr, *list = nullptr,
+         *tinfo = nullptr, *offsB = nullptr, *seg = nullptr, *bk = nullptr, *fb = nullptr;
+    size_t c_tempA = 0, c_tempB = 0, c_offsA = 0, c_tmm = 0, c_list = 0, c_tinfo = 0, c_offsB = 0, c_seg = 0,
+           c_bk = 0, c_fb = 0;
+};
+struct MsdScratch {
+    int dev = -1;
+    MsdTabScratch t[2];
+    int64_t *spl = nullptr;
+    MsdGroup *groups = nullptr, *slot_groups = nullptr;
+    uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr;
+    MsdPlan *plan = nullptr, *h_plan = nullptr;
+    void *slots = nullptr;
+    size_t c_slots = 0;
+    void *work = nullptr;
+    size_t c_work = 0;
+    int64_t *d_tmp = nullptr;
+};
+std::map<int, MsdScratch> g_msd;
+int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
+
+int msd_scratch(MsdScratch **out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    MsdScratch &m = g_msd[dev];
+    if (m.dev < 0) {
+        m.dev = dev;
+        HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
+        HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
+        HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
+        HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * 256));
+        HIP_TRY(hipMalloc(&m.counts, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.single_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.big_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
+        HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
+        HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
+    }
+    *out = &m;
+    return SMJ_OK;
+}
+
+void msd_free_all() {
+    for (auto &kv : g_msd) {
+        MsdScratch &m = kv.second;
+        hipSetDevice(kv.first);
+        for (auto &t : m.t)
+            for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
+                hipFree(p);
+        for (void *p : {(void *)m.spl, (void *)m.groups, (void *)m.slot_groups, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+                        (void *)m.big_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
+            hipFree(p);
+        hipHostFree(m.h_plan);
+    }
+    g_msd.clear();
+}
+
+struct MsdIn {            // one input table of the pipeline
+    const T *src;
+    int64_t n;
+    int cols, use_sel, sel_col, key;
+    T sel_val;
+    T *out;               // sorted selected rows
+};
+
+// Records the index of the last profiling record (to patch its byte count
+// once the row counts are known).
+size_t prof_last() { return g_prof.empty() ? (size_t)-1 : g_prof.size() - 1; }
+void prof_set_bytes(size_t i, double bytes) {
+    if (g_prof_on && i < g_prof.size()) g_prof[i].bytes = bytes;
+}
+
+// Oversized groups after the main pass: single-key ones stream through
+// msd_single_kernel; multi-key ones (and groups whose key range does not fit
+// the LDS sort word) are gathered and sorted / joined by the LSD path.
+int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdFinalParams &fp, int64_t *out_j,
+                 hipStream_t s, bool *redo_compact) {
+    const MsdPlan &pl = *ms->h_plan;
+    *redo_compact = false;
+    if (pl.nsingle == 0 && pl.nbig == 0) return SMJ_OK;
+    std::vector<MsdGroup> groups(std::max<uint32_t>(pl.ngroups, 1));
+    HIP_TRY(hipMemcpyAsync(groups.data(), ms->groups, sizeof(MsdGroup) * pl.ngroups, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> singles(pl.nsingle), bigs(pl.nbig);
+    if (pl.nsingle)
+        HIP_TRY(hipMemcpyAsync(singles.data(), ms->single_list, 4 * pl.nsingle, hipMemcpyDeviceToHost, s));
+    if (pl.nbig) HIP_TRY(hipMemcpyAsync(bigs.data(), ms->big_list, 4 * pl.nbig, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (pl.nsingle) {
+        std::vector<uint2> work;
+        for (uint32_t slot : singles) {
+            const MsdGroup &g = groups[slot];
+            const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
+            for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work.push_back(make_uint2(slot, c));
+        }
+        SMJ_TRY(grow(&ms->work, &ms->c_work, work.size() * sizeof(uint2)));
+        HIP_TRY(hipMemcpyAsync(ms->work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+        ProfScope ps("msd_single", 0, s);
+        HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
+    }
+    for (uint32_t slot : bigs) {
+        const MsdGroup &g = groups[slot];
+        const uint32_t nx[2] = {g.nR, ntab > 1 ? g.nS : 0u};
+        const uint32_t ox[2] = {g.outR, g.outS};
+        for (int x = 0; x < ntab; x++) {
+            if (nx[x] == 0) continue;
+            MsdTabScratch &ts = ms->t[x];
+            SMJ_TRY(grow(&ts.fb, &ts.c_fb, (size_t)nx[x] * in[x].cols * 8));
+            HIP_TRY(launch_msd_gather(fp.tab[x], ms->groups, slot, nx[x], (int64_t *)ts.fb, s));
+            int64_t m = 0;
+            SMJ_TRY(lsd_select_sort((const T *)ts.fb, nx[x], in[x].cols, 0, 0, 0, in[x].key, 0,
+                                    in[x].out + (int64_t)ox[x] * in[x].cols, &m, s));
+        }
+        if (join && nx[0] && nx[1]) {
+            const int tc = in[0].cols + in[1].cols - 1;
+            SMJ_TRY(smj_dev_join(in[0].out + (int64_t)g.outR * in[0].cols, nx[0], in[0].cols,
+                                 in[1].out + (int64_t)g.outS * in[1].cols, nx[1], in[1].cols, in[0].key, in[1].key,
+                                 (T *)ms->slots + (int64_t)g.outR * tc, ms->d_tmp, nullptr, s));
+            HIP_TRY(hipMemcpyAsync(ms->counts + slot, ms->d_tmp, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    (void)out_j;
+    *redo_compact = join != 0;
+    return SMJ_OK;
+}
+
+// The pipeline.  h_rows[x] gets the selected row count of table x and, with
+// join, h_rows[2] the joined row count.  One stream synchronisation at the
+// end (plus one more round when oversized groups need the fallback).
+int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+    MsdScratch *ms;
+    SMJ_TRY(msd_scratch(&ms));
+    int T_[2] = {1, 1};
+    int64_t tilesA[2] = {0, 0}, maxB[2] = {0, 0};
+    for (int x = 0; x < ntab; x++) {
+        const MsdIn &t = in[x];
+        MsdTabScratch &ts = ms->t[x];
+        T_[x] = msd_tile(t.cols);
+        tilesA[x] = (t.n + T_[x] - 1) / T_[x];
+        maxB[x] = tilesA[x] + kBucketsA;
+        const size_t W = (size_t)t.cols * 8;
+        SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, std::max<size_t>(1, t.n) * W));
+        SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * T_[x] * W));
+        SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsA * 4));
+        SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
+        SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
+        SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
+        SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * 4));
+        SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4));
+        SMJ_TRY(grow(&ts.bk, &ts.c_bk, 256 * sizeof(MsdBucket)));
+    }
+    const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
+    if (join) SMJ_TRY(grow(&ms->slots, &ms->c_slots, std::max<size_t>(1, in[0].n) * tc * 8));
+    HIP_TRY(hipMemsetAsync(ms->plan, 0, sizeof(MsdPlan), s));
+    auto segL = [&](int x) { return (uint32_t *)ms->t[x].seg; };
+    auto segC = [&](int x) { return (uint32_t *)ms->t[x].seg + kMsdSegs * kOffsA; };
+    {
+        MsdSampleParams sp{};
+        for (int x = 0; x < ntab; x++)
+            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val};
+        sp.ntab = ntab;
+        sp.spl = ms->spl;
+        ProfScope ps("msd_sample", 0, s);
+        HIP_TRY(launch_msd_sample(sp, s));
+    }
+    size_t pa[2] = {(size_t)-1, (size_t)-1};
+    for (int x = 0; x < ntab; x++) {
+        MsdPartAParams p{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
+                         (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
+        {
+            ProfScope ps("msd_part_a", 0, s);
+            HIP_TRY(launch_msd_part_a(p, in[x].cols, s));
+        }
+        pa[x] = prof_last();
+    }
+    {
+        ProfScope ps("msd_runs", 0, s);
+        for (int x = 0; x < ntab; x++)
+            HIP_TRY(launch_msd_runs_seg((const uint32_t *)ms->t[x].offsA, tilesA[x], segL(x), segC(x), s));
+        MsdBasesParams bp{};
+        for (int x = 0; x < ntab; x++) {
+            bp.segL[x] = segL(x);
+            bp.segC[x] = segC(x);
+            bp.tmm[x] = (const int64_t *)ms->t[x].tmm;
+            bp.ntiles[x] = tilesA[x];
+            bp.tile[x] = T_[x];
+            bp.bk[x] = (MsdBucket *)ms->t[x].bk;
+        }
+        bp.ntab = ntab;
+        bp.spl = ms->spl;
+        bp.plan = ms->plan;
+        HIP_TRY(launch_msd_bases(bp, s));
+        for (int x = 0; x < ntab; x++)
+            HIP_TRY(launch_msd_runs_apply((const uint32_t *)ms->t[x].offsA, tilesA[x], T_[x], segL(x), segC(x),
+                                          (const MsdBucket *)ms->t[x].bk, (uint2 *)ms->t[x].list,
+                                          (uint2 *)ms->t[x].tinfo, s));
+    }
+    size_t pb[2] = {(size_t)-1, (size_t)-1};
+    for (int x = 0; x < ntab; x++) {
+        MsdPartBParams p{(const int64_t *)ms->t[x].tempA, (int64_t *)ms->t[x].tempB, (const uint2 *)ms->t[x].list,
+                         (const uint2 *)ms->t[x].tinfo, (const MsdBucket *)ms->t[x].bk, ms->plan,
+                         (uint32_t *)ms->t[x].offsB, in[x].key, x};
+        {
+            ProfScope ps("msd_part_b", 0, s);
+            HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s));
+        }
+        pb[x] = prof_last();
+    }
+    {
+        MsdGroupParams gp{};
+        for (int x = 0; x < ntab; x++) {
+            gp.offs[x] = (const uint32_t *)ms->t[x].offsB;
+            gp.bk[x] = (const MsdBucket *)ms->t[x].bk;
+            gp.tile[x] = T_[x];
+        }
+        gp.ntab = ntab;
+        gp.slot_groups = ms->slot_groups;
+        gp.ngrp = ms->ngrp;
+        gp.groups = ms->groups;
+        gp.counts = ms->counts;
+        gp.plan = ms->plan;
+        gp.single_list = ms->single_list;
+        gp.big_list = ms->big_list;
+        ProfScope ps("msd_group", 0, s);
+        HIP_TRY(launch_msd_group(gp, s));
+    }
+    MsdFinalParams fp{};
+    for (int x = 0; x < ntab; x++)
+        fp.tab[x] = MsdTab{(const int64_t *)ms->t[x].tempB, (const uint32_t *)ms->t[x].offsB,
+                           (const MsdBucket *)ms->t[x].bk, in[x].out, T_[x], in[x].cols, in[x].key, x};
+    fp.groups = ms->groups;
+    fp.slots = (int64_t *)ms->slots;
+    fp.counts = ms->counts;
+    fp.plan = ms->plan;
+    fp.big_list = ms->big_list;
+    fp.ntab = ntab;
+    fp.join = join;
+    fp.key2 = key2;
+    size_t pf;
+    {
+        ProfScope ps("msd_final", 0, s);
+        HIP_TRY(launch_msd_final(fp, s));
+    }
+    pf = prof_last();
+    auto compact = [&]() -> int {
+        {
+            ProfScope ps("msd_count_scan", 0, s);
+            HIP_TRY(launch_msd_count_scan(ms->counts, ms->offs, ms->plan, s));
+        }
+        ProfScope ps("msd_compact", 0, s);
+        HIP_TRY(launch_msd_compact((const int64_t *)ms->slots, ms->groups, ms->counts, ms->offs, ms->plan, tc, out_j,
+                                   s));
+        return SMJ_OK;
+    };
+    size_t pc = (size_t)-1;
+    if (join) {
+        SMJ_TRY(compact());
+        pc = prof_last();
+    }
+    HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    g_msd_stats[0] = ms->h_plan->nsingle;
+    g_msd_stats[1] = ms->h_plan->nbig;
+    g_msd_stats[2] = ms->h_plan->m[0];
+    g_msd_stats[3] = ms->h_plan->m[1];
+    bool redo = false;
+    SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
+    if (redo) {
+        SMJ_TRY(compact());
+        pc = prof_last();
+        HIP_TRY(hipMemcpyAsync(&ms->h_plan->joined, &ms->plan->joined, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    const MsdPlan &pl = *ms->h_plan;
+    for (int x = 0; x < ntab; x++) {
+        const double W = 8.0 * in[x].cols;
+        prof_set_bytes(pa[x], W * ((double)in[x].n + pl.m[x]));
+        prof_set_bytes(pb[x], W * 2.0 * pl.m[x]);
+        h_rows[x] = pl.m[x];
+    }
+    const double Jb = join ? 8.0 * tc * (double)pl.joined : 0.0;
+    double fb = Jb;
+    for (int x = 0; x < ntab; x++) fb += 2.0 * 8.0 * in[x].cols * pl.m[x];
+    prof_set_bytes(pf, fb);
+    prof_set_bytes(pc, 2.0 * Jb);
+    if (join) h_rows[2] = pl.joined;
+    return SMJ_OK;
+}
+
+int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int key, const T *out) {
+    SMJ_TRY(check_table(n, cols, use_sel ? sel_col : 0, key));
+    if (n > 0 && (!src || !out || src == out)) return SMJ_ERR_INVALID;
+    return SMJ_OK;
+}
+}  // namespace
+
+extern "C" void smj_debug_msd_stats(int64_t *out4) {
+    for (int i = 0; i < 4; i++) out4[i] = g_msd_stats[i];
+}
+
+extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                                   T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                                   void *stream) {
+    (void)key_base;  // the MSD pipeline derives its digits from the data
+    if (!out_rows) return SMJ_ERR_INVALID;
+    *out_rows = 0;
+    SMJ_TRY(msd_check(in, n_rows, col_num, use_select, select_col, key_col, out));
+    if (n_rows == 0) return SMJ_OK;
+    MsdIn t{in, n_rows, col_num, use_select, select_col, key_col, select_val, out};
+    int64_t rows[3] = {0, 0, 0};
+    SMJ_TRY(msd_run(&t, 1, 0, 0, nullptr, rows, (hipStream_t)stream));
+    *out_rows = rows[0];
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
+                                       int key1, const T *S, int64_t ns, int c2, int use_sel2, int sel_col2,
+                                       T sel_val2, int key2, T *R_sorted, T *S_sorted, T *out, int64_t *h_rows,
+                                       void *stream) {
+    if (!h_rows) return SMJ_ERR_INVALID;
+    h_rows[0] = h_rows[1] = h_rows[2] = 0;
+    SMJ_TRY(msd_check(R, nr, c1, use_sel1, sel_col1, key1, R_sorted));
+    SMJ_TRY(msd_check(S, ns, c2, use_sel2, sel_col2, key2, S_sorted));
+    if (nr + ns >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    if (nr > 0 && ns > 0 && !out) return SMJ_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (nr == 0 || ns == 0) {  // nothing to join: sort what there is
+        if (nr) SMJ_TRY(smj_dev_select_sort(R, nr, c1, use_sel1, sel_col1, sel_val1, key1, 0, R_sorted, &h_rows[0], s));
+        if (ns) SMJ_TRY(smj_dev_select_sort(S, ns, c2, use_sel2, sel_col2, sel_val2, key2, 0, S_sorted, &h_rows[1], s));
+        return SMJ_OK;
+    }
+    const MsdIn t[2] = {{R, nr, c1, use_sel1, sel_col1, key1, sel_val1, R_sorted},
+                        {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
+    return msd_run(t, 2, 1, key2, out, h_rows, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,6 +898,7 @@ extern "C" void smj_finalize(void) {
         hipHostFree(s.h_small);
     }
     g_scratch.clear();
+    msd_free_all();
     for (auto e : g_event_pool) hipEventDestroy(e);
     g_event_pool.clear();
     if (g_host_stream) {
@@ -628,7 +972,7 @@ extern "C" int smj_sort(const dpu_block_t *bl, T *rows, int key_col) {
     hipStream_t s = g_host_stream;
     HIP_TRY(hipMemcpyAsync(din.p, rows, bytes, hipMemcpyHostToDevice, s));
     int64_t m = 0;
-    SMJ_TRY(dev_select_sort((T *)din.p, bl->row_num, bl->col_num, 0, 0, 0, key_col, 0, (T *)dout.p, &m, s));
+    SMJ_TRY(smj_dev_select_sort((T *)din.p, bl->row_num, bl->col_num, 0, 0, 0, key_col, 0, (T *)dout.p, &m, s));
     HIP_TRY(hipMemcpyAsync(rows, dout.p, bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     DevScratch *sc;
@@ -713,12 +1057,11 @@ extern "C" int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_b
     if (nr) HIP_TRY(hipMemcpyAsync(dr.p, R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
     if (ns) HIP_TRY(hipMemcpyAsync(ds.p, S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipEventRecord(ev[1], st));
-    int64_t mr = 0, ms = 0, j = 0;
-    SMJ_TRY(dev_select_sort((T *)dr.p, nr, c1, 1, select_col1, select_val1, key1, 0, (T *)drs.p, &mr, st));
-    SMJ_TRY(dev_select_sort((T *)ds.p, ns, c2, 1, select_col2, select_val2, key2, 0, (T *)dss.p, &ms, st));
-    SMJ_TRY(dout.alloc((size_t)std::min(mr, ms) * tc * 8));
-    SMJ_TRY(smj_dev_join((T *)drs.p, mr, c1, (T *)dss.p, ms, c2, key1, key2, (T *)dout.p, (int64_t *)dcnt.p, &j,
-                         st));
+    SMJ_TRY(dout.alloc((size_t)std::max<int64_t>(1, std::min(nr, ns)) * tc * 8));
+    int64_t rows[3] = {0, 0, 0};
+    SMJ_TRY(smj_dev_sort_merge_join((T *)dr.p, nr, c1, 1, select_col1, select_val1, key1, (T *)ds.p, ns, c2, 1,
+                                    select_col2, select_val2, key2, (T *)drs.p, (T *)dss.p, (T *)dout.p, rows, st));
+    const int64_t j = rows[2];
     HIP_TRY(hipEventRecord(ev[2], st));
     T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
     if (!res) return SMJ_ERR_NOMEM;

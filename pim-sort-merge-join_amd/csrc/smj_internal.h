@@ -130,4 +130,145 @@ hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
                            double theta, double zeta_n, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// MSD sample-sort pipeline (smj_msd.hip): sample -> part_a -> runs -> part_b
+// -> group -> final (+ single / LSD fallback) -> compact.  DESIGN.md §3.
+// ---------------------------------------------------------------------------
+constexpr int kMsdThreads = 512;
+constexpr int kMsdWaves = kMsdThreads / 64;
+// rows per thread of a tile: a tile is <= 64 KiB of rows whatever the width
+__host__ __device__ constexpr int msd_items(int cols) {
+    return cols == 1 ? 16 : cols == 2 ? 8 : cols == 3 ? 5 : cols == 4 ? 4 : cols == 5 ? 3 : 2;
+}
+__host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_items(cols); }
+constexpr int kSplA = 127;                 // pass-A splitters
+constexpr int kBucketsA = 2 * kSplA + 1;   // 255 pass-A buckets (odd = one key value)
+constexpr int kOffsA = 256;                // offsA row: 255 bucket starts + the tile's row count
+constexpr int kBitsB = 10;
+constexpr int kRadB = 1 << kBitsB;         // 1024 pass-B sub-buckets per bucket
+constexpr int kOffsB = kRadB + 1;          // offsB row: 1024 starts + the tile's row count
+constexpr int kGroupCap = 2048;            // rows per table in one final group (LDS)
+constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots
+constexpr int kMsdFinalGrid = 512;         // persistent final kernel: 2 workgroups per CU
+constexpr int kSampleMax = 8192;           // sampled keys per table
+constexpr int kMsdSegs = 64;               // segments of the run scans
+constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
+
+struct MsdTable {        // an input table as the sampler and part_a see it
+    const int64_t *src;
+    int64_t n;
+    int cols, key_col, use_sel, sel_col;
+    int64_t sel_val;
+};
+struct MsdSampleParams {
+    MsdTable tab[2];
+    int ntab;
+    int64_t *spl;        // out: kSplA splitters
+};
+struct MsdPartAParams {
+    const int64_t *src;
+    int64_t n;
+    int use_sel, sel_col, key_col, pad;
+    int64_t sel_val;
+    const int64_t *spl;
+    int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
+    uint32_t *offs;      // [tiles][kOffsA]
+    int64_t *tmm;        // [tiles][2] min / max selected key
+};
+struct MsdBucket {       // per pass-A bucket and table
+    int64_t lo;          // pass-B digit (common to R and S): with r = key - lo,
+    uint64_t scale;      //   scale == 0: r (interval < kRadB keys: one key per sub-bucket)
+                         //   else min(kRadB - 1, mulhi(r, scale)), scale = 2^64 * kRadB / (hi - lo + 1)
+    uint32_t maxspan;    // sub-buckets a final group may span (its key range stays < 2^48)
+    uint32_t L;          // rows of this table in the bucket
+    uint32_t row_start;  // first sorted-output row of the bucket
+    uint32_t list_base;  // first run-list entry
+    uint32_t nruns;      // run-list entries
+    uint32_t tile_base;  // first pass-B tile
+};
+struct MsdPlan {         // device-side pipeline state (zeroed per call)
+    uint32_t m[2];       // selected rows per table
+    uint32_t ntilesB[2]; // pass-B tiles per table
+    uint32_t nsingle, nbig;
+    int64_t gmin, gmax;
+    int64_t joined;      // written by the count scan
+    uint32_t ngroups;    // dense groups (key order)
+    uint32_t pad;
+};
+struct MsdBasesParams {
+    const uint32_t *segL[2];
+    const uint32_t *segC[2];
+    const int64_t *tmm[2];
+    int64_t ntiles[2];
+    int tile[2];
+    int ntab;
+    const int64_t *spl;
+    MsdBucket *bk[2];
+    MsdPlan *plan;
+};
+struct MsdPartBParams {
+    const int64_t *srcA;
+    int64_t *out;        // tempB: pass-B tile g at rows [g*T, g*T + rows)
+    const uint2 *list;
+    const uint2 *tinfo;  // per pass-B tile: {bucket, first run-list entry}
+    const MsdBucket *bk;
+    const MsdPlan *plan;
+    uint32_t *offs;      // [tilesB][kOffsB]
+    int key_col, x;
+};
+struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
+    uint16_t a, flags, b0, b1;
+    uint32_t nR, nS, outR, outS;
+    uint32_t pad[2];
+};
+struct MsdGroupParams {
+    const uint32_t *offs[2];
+    const MsdBucket *bk[2];
+    int tile[2];
+    int ntab;
+    MsdGroup *slot_groups;  // [kBucketsA][kRadB]: bucket a's groups at slots a * kRadB + j
+    uint32_t *ngrp;         // [kBucketsA] groups per bucket
+    MsdGroup *groups;       // dense, key order (msd_group_pack)
+    uint32_t *counts;       // dense: join rows per group (single-key groups: known here)
+    MsdPlan *plan;
+    uint32_t *single_list, *big_list;  // dense group indices
+};
+struct MsdTab {          // a table as the final kernels see it
+    const int64_t *tempB;
+    const uint32_t *offs;
+    const MsdBucket *bk;
+    int64_t *out;        // sorted rows
+    int tile, cols, key, x;
+};
+struct MsdFinalParams {
+    MsdTab tab[2];
+    const MsdGroup *groups;
+    int64_t *slots;      // join rows of group s at slot row groups[s].outR
+    uint32_t *counts;
+    MsdPlan *plan;
+    uint32_t *big_list;
+    int ntab, join, key2, pad;
+};
+
+hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
+hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
+hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
+                               hipStream_t s);
+hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
+hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, const uint32_t *segL,
+                                 const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
+                                 hipStream_t s);
+hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
+hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
+hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
+hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
+hipError_t launch_msd_gather(const MsdTab &tb, const MsdGroup *groups, uint32_t slot, int64_t rows,
+                             int64_t *dst, hipStream_t s);
+hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
+                              const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, hipStream_t s);
+// exclusive scan of the plan->ngroups dense group counts -> offs, total -> plan->joined
+hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *offs, MsdPlan *plan, hipStream_t s);
+// exclusive scan of n u32 counts -> offs, total -> *total (one workgroup)
+hipError_t launch_count_scan(const uint32_t *counts, int64_t n, uint32_t *offs, int64_t *total, hipStream_t s);
+
 }  // namespace smj

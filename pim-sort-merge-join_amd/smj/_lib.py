@@ -42,6 +42,8 @@ SIGNATURES = {
     "smj_join": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(_P), _PL]),
     "smj_sort_merge_join": (_I, [_P, _P, _P, _P, _I, _L, _I, _L, _I, _I, ctypes.POINTER(_P), _PL, _P]),
     "smj_dev_select_sort": (_I, [_P, _L, _I, _I, _I, _L, _I, _U, _P, _PL, _P]),
+    "smj_dev_select_sort_lsd": (_I, [_P, _L, _I, _I, _I, _L, _I, _U, _P, _PL, _P]),
+    "smj_dev_sort_merge_join": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _L, _I, _I, _I, _L, _I, _P, _P, _P, _PL, _P]),
     "smj_dev_select": (_I, [_P, _L, _I, _I, _L, _P, _PL, _P]),
     "smj_dev_merge": (_I, [_P, _L, _P, _L, _I, _I, _P, _P]),
     "smj_dev_join": (_I, [_P, _L, _I, _P, _L, _I, _I, _I, _P, _P, _PL, _P]),
@@ -50,6 +52,7 @@ SIGNATURES = {
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),
+    "smj_debug_msd_stats": (None, [_PL]),
     "smj_prof_enable": (None, [_I]),
     "smj_prof_report": (_I, [ctypes.c_char_p, ctypes.c_size_t]),
 }

@@ -53,6 +53,54 @@ def select_sort(table, key_col=0, select_col=0, select_val=None, key_base=0, out
     return out[: m.value]
 
 
+def select_sort_lsd(table, key_col=0, select_col=0, select_val=None, key_base=0, out=None, stream=None):
+    """select_sort on the LSD radix path (the MSD pipeline's fallback)."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    if out is None:
+        out = torch.empty_like(table)
+    m = ctypes.c_int64(0)
+    use = select_val is not None
+    _lib.check(lib.smj_dev_select_sort_lsd(_ptr(table), n, cols, int(use), select_col,
+                                           int(select_val) if use else 0, key_col, biased_base(key_base),
+                                           _ptr(out), ctypes.byref(m), _stream(stream)), "smj_dev_select_sort_lsd")
+    return out[: m.value]
+
+
+def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=None, S_sorted=None, out=None,
+                    stream=None):
+    """The fused hot path (cpu_app.c main :303-364): select (select = (col, val)
+    keeps rows with row[col] > val; None keeps all), stable sort on the key,
+    1:1 zip join.  Returns (R_sorted[:mR], S_sorted[:mS], out[:J])."""
+    lib = _lib.load()
+    _table(R, "R")
+    _table(S, "S")
+    nr, c1 = R.shape
+    ns, c2 = S.shape
+    if R_sorted is None:
+        R_sorted = torch.empty_like(R)
+    if S_sorted is None:
+        S_sorted = torch.empty_like(S)
+    if out is None:
+        out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=torch.int64, device=R.device)
+    rows = (ctypes.c_int64 * 3)()
+    s1 = select1 or (0, 0)
+    s2 = select2 or (0, 0)
+    _lib.check(lib.smj_dev_sort_merge_join(_ptr(R), nr, c1, int(select1 is not None), s1[0], int(s1[1]), key1,
+                                           _ptr(S), ns, c2, int(select2 is not None), s2[0], int(s2[1]), key2,
+                                           _ptr(R_sorted), _ptr(S_sorted), _ptr(out), rows, _stream(stream)),
+               "smj_dev_sort_merge_join")
+    return R_sorted[: rows[0]], S_sorted[: rows[1]], out[: rows[2]]
+
+
+def msd_stats():
+    """(single-key groups, LSD-fallback groups, m_R, m_S) of the last MSD pipeline call."""
+    out = (ctypes.c_int64 * 4)()
+    _lib.load().smj_debug_msd_stats(out)
+    return tuple(int(v) for v in out)
+
+
 def biased_base(key_base):
     return int(key_base) & ((1 << 64) - 1)
 

@@ -1,0 +1,152 @@
+"""GPU parity of the fused MSD sample-sort pipeline (smj_dev_sort_merge_join:
+select -> stable sort -> 1:1 zip join, cpu_app.c main :303-364) against the
+CPU oracle, bit for bit: sorted R, sorted S and the joined rows.  The cases
+cover the pipeline's paths: normal LDS-sorted groups, single-key groups
+streamed without a sort (heavy / duplicate keys), and the LSD fallback for
+multi-key groups over the LDS capacity."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+I64 = np.iinfo(np.int64)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def table(rng, n, cols, kind, key_col, payload0):
+    if kind == "uniform":
+        t = rng.integers(1, 3 * max(n, 1), size=(n, cols), dtype=np.int64, endpoint=True)
+    elif kind == "dups":
+        t = rng.integers(-50, 50, size=(n, cols), dtype=np.int64)
+    elif kind == "dom3":
+        t = rng.integers(-3, 3, size=(n, cols), dtype=np.int64)
+    elif kind == "same":
+        t = np.full((n, cols), 7, dtype=np.int64)
+    elif kind == "wide":
+        t = rng.integers(I64.min, I64.max, size=(n, cols), dtype=np.int64, endpoint=True)
+    elif kind == "extremes":
+        vals = np.array([I64.min, -1, 0, 1, I64.max], dtype=np.int64)
+        t = vals[rng.integers(0, 5, size=(n, cols))]
+    elif kind == "zipf":
+        ranks = np.minimum(rng.zipf(1.3, size=(n, cols)), 10 ** 6)
+        t = (ranks * 2654435761) % 1000003
+    else:
+        raise ValueError(kind)
+    if cols > 1:
+        t[:, (key_col + 1) % cols] = payload0 + np.arange(n)  # payload = row id: stability is visible
+    return t
+
+
+FUSED_CASES = [
+    # nr, ns, c1, c2, key1, key2, kind, select1, select2
+    (0, 1000, 2, 2, 0, 0, "uniform", None, None),
+    (1000, 0, 2, 2, 0, 0, "uniform", None, None),
+    (1, 1, 2, 2, 0, 0, "same", None, None),
+    (5000, 5000, 2, 2, 0, 0, "uniform", (0, 100), (0, 100)),
+    (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 5000), (0, 5000)),
+    (70_000, 9_000, 3, 2, 1, 0, "dups", (2, -10), None),
+    (9_000, 70_000, 2, 4, 0, 3, "dups", None, (1, 0)),
+    (200_000, 150_000, 4, 5, 2, 4, "dom3", None, None),
+    (40_000, 40_000, 1, 1, 0, 0, "wide", None, None),
+    (50_000, 60_000, 8, 8, 7, 0, "dups", (0, 10), None),
+    (300_000, 300_000, 2, 2, 0, 0, "same", None, None),
+    (120_000, 80_000, 2, 2, 0, 0, "extremes", None, None),
+    (250_000, 250_000, 2, 2, 0, 0, "zipf", None, None),
+    (33_333, 44_444, 5, 3, 4, 2, "wide", (0, 0), (1, 0)),
+    (1_000_000, 1_000_000, 2, 2, 0, 0, "uniform", (0, 5000), (0, 5000)),
+]
+
+
+def ref_pipeline(R, S, k1, k2, s1, s2):
+    Rs = oracle.select_sort(R, k1, s1[0] if s1 else 0, s1[1] if s1 else None)
+    Ss = oracle.select_sort(S, k2, s2[0] if s2 else 0, s2[1] if s2 else None)
+    return Rs, Ss, oracle.join(Rs, Ss, k1, k2)
+
+
+@pytest.mark.parametrize("nr,ns,c1,c2,k1,k2,kind,s1,s2", FUSED_CASES)
+def test_fused_pipeline_matches_oracle(gpu, oracle_built, nr, ns, c1, c2, k1, k2, kind, s1, s2):
+    from smj import ops
+    rng = np.random.default_rng(nr * 13 + ns * 7 + c1)
+    R = table(rng, nr, c1, kind, k1, 0)
+    S = table(rng, ns, c2, kind, k2, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R).reshape(nr, c1), dev(S).reshape(ns, c2), k1, k2, s1, s2)
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, s2)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, c1))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, c2))
+    if nr and ns:
+        np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
+
+
+def test_single_key_groups_stream(gpu, oracle_built):
+    """Heavy keys (over the LDS group capacity) take the no-sort streaming path."""
+    from smj import ops
+    rng = np.random.default_rng(1)
+    n = 400_000
+    R = rng.integers(0, 8, size=(n, 2), dtype=np.int64)
+    S = rng.integers(4, 12, size=(n // 2, 2), dtype=np.int64)
+    R[:, 1] = np.arange(n)
+    S[:, 1] = -np.arange(n // 2)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S))
+    assert ops.msd_stats()[0] > 0
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
+def test_multi_key_oversized_group_falls_back(gpu, oracle_built):
+    """A far outlier stretches the first bucket's key interval, so thousands of
+    distinct keys share one sub-bucket: the LSD fallback sorts and joins it."""
+    from smj import ops
+    rng = np.random.default_rng(2)
+    n = 1_000_000
+    keys = rng.integers(10, 10 ** 6, size=n)
+    keys[rng.choice(n, 5000, replace=False)] = rng.integers(0, 2, size=5000)
+    keys[123] = -(1 << 62)
+    R = np.stack([keys, np.arange(n)], axis=1).astype(np.int64)
+    S = R[rng.permutation(n)[: n // 2]].copy()
+    S[:, 1] = 10 ** 9 + np.arange(len(S))
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S))
+    assert ops.msd_stats()[1] > 0
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
+@pytest.mark.parametrize("n,cols,kind", [(100_000, 2, "uniform"), (70_000, 3, "dups"), (4097, 2, "wide")])
+def test_lsd_select_sort_matches_oracle(gpu, oracle_built, n, cols, kind):
+    from smj import ops
+    rng = np.random.default_rng(n)
+    t = table(rng, n, cols, kind, 0, 0)
+    got = ops.select_sort_lsd(dev(t), 0, 0, 0)
+    np.testing.assert_array_equal(host(got), oracle.select_sort(t, 0, 0, 0).reshape(-1, cols))
+
+
+def test_fused_c3_baseline_size(gpu, oracle_built):
+    """C3 (1e8 x 1e8 uniform keys in [1, 3n], WHERE col0 > 5000), the bench
+    workload, through the fused pipeline: sorted outputs against numpy's
+    stable argsort of the selected inputs, joined rows against the C oracle's
+    O(n) zip join of those."""
+    from smj import ops
+    n = 100_000_000
+    R = ops.gen_uniform(n, seed=1, key_range=3 * n)
+    S = ops.gen_uniform(n, seed=2, key_range=3 * n)
+    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000))
+    sorted_np = []
+    for T, got in ((R, gR), (S, gS)):
+        t = host(T)
+        keep = t[t[:, 0] > 5000]
+        np.testing.assert_array_equal(host(got), keep[np.argsort(keep[:, 0], kind="stable")])
+        sorted_np.append(keep[np.argsort(keep[:, 0], kind="stable")])
+    np.testing.assert_array_equal(host(gJ), oracle.join(sorted_np[0], sorted_np[1]))

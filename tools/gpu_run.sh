@@ -23,11 +23,12 @@ for s in $STEPS; do
   case $s in
     build) run build 600 make -s -j16 -C pim-sort-merge-join_amd ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 1200 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider ;;
+    tests) run tests 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 ;;
+               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0
+           rm -f "$OUT/prof/run_kernel_trace.csv" ;;
     pmcf)  export TMPDIR=/tmp
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 ;;
