@@ -109,6 +109,13 @@ extern "C" int smj_debug_phase_cycles(unsigned long long *out16) {
     return read_phase_cycles(out16) == hipSuccess ? SMJ_OK : SMJ_ERR_HIP;
 }
 
+// Diagnostic only (not part of smj.h): msd_final phase cycles collected under
+// SMJ_DEBUG_MSD=1; out[k] cycles of phase k summed over workgroups, out[9] groups.
+extern "C" int smj_debug_msd_phases(unsigned long long *out16) {
+    hipDeviceSynchronize();
+    return read_msd_phases(out16) == hipSuccess ? SMJ_OK : SMJ_ERR_HIP;
+}
+
 static std::string prof_json() {
     struct Agg { long launches = 0; double ms = 0, bytes = 0; };
     std::map<std::string, Agg> agg;
@@ -425,7 +432,8 @@ struct MsdScratch {
     MsdTabScratch t[2];
     int64_t *spl = nullptr;
     MsdGroup *groups = nullptr, *slot_groups = nullptr;
-    uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr;
+    uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr,
+             *wide_list = nullptr, *radix_list = nullptr;
     MsdPlan *plan = nullptr, *h_plan = nullptr;
     void *slots = nullptr;
     size_t c_slots = 0;
@@ -450,6 +458,8 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.single_list, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.big_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.wide_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(hipMalloc(&m.radix_list, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
         HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
@@ -466,7 +476,7 @@ void msd_free_all() {
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.groups, (void *)m.slot_groups, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
-                        (void *)m.big_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
+                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
             hipFree(p);
         hipHostFree(m.h_plan);
     }
@@ -563,7 +573,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
         SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
         SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
-        SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * 4));
+        SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * sizeof(uint16_t)));
         SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4));
         SMJ_TRY(grow(&ts.bk, &ts.c_bk, 256 * sizeof(MsdBucket)));
     }
@@ -617,7 +627,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     for (int x = 0; x < ntab; x++) {
         MsdPartBParams p{(const int64_t *)ms->t[x].tempA, (int64_t *)ms->t[x].tempB, (const uint2 *)ms->t[x].list,
                          (const uint2 *)ms->t[x].tinfo, (const MsdBucket *)ms->t[x].bk, ms->plan,
-                         (uint32_t *)ms->t[x].offsB, in[x].key, x};
+                         (uint16_t *)ms->t[x].offsB, in[x].key, x};
         {
             ProfScope ps("msd_part_b", 0, s);
             HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s));
@@ -627,7 +637,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     {
         MsdGroupParams gp{};
         for (int x = 0; x < ntab; x++) {
-            gp.offs[x] = (const uint32_t *)ms->t[x].offsB;
+            gp.offs[x] = (const uint16_t *)ms->t[x].offsB;
             gp.bk[x] = (const MsdBucket *)ms->t[x].bk;
             gp.tile[x] = T_[x];
         }
@@ -644,13 +654,15 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     MsdFinalParams fp{};
     for (int x = 0; x < ntab; x++)
-        fp.tab[x] = MsdTab{(const int64_t *)ms->t[x].tempB, (const uint32_t *)ms->t[x].offsB,
+        fp.tab[x] = MsdTab{(const int64_t *)ms->t[x].tempB, (const uint16_t *)ms->t[x].offsB,
                            (const MsdBucket *)ms->t[x].bk, in[x].out, T_[x], in[x].cols, in[x].key, x};
     fp.groups = ms->groups;
     fp.slots = (int64_t *)ms->slots;
     fp.counts = ms->counts;
     fp.plan = ms->plan;
     fp.big_list = ms->big_list;
+    fp.wide_list = ms->wide_list;
+    fp.radix_list = ms->radix_list;
     fp.ntab = ntab;
     fp.join = join;
     fp.key2 = key2;

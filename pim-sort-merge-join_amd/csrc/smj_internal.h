@@ -144,12 +144,16 @@ __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_
 constexpr int kSplA = 127;                 // pass-A splitters
 constexpr int kBucketsA = 2 * kSplA + 1;   // 255 pass-A buckets (odd = one key value)
 constexpr int kOffsA = 256;                // offsA row: 255 bucket starts + the tile's row count
-constexpr int kBitsB = 10;
-constexpr int kRadB = 1 << kBitsB;         // 1024 pass-B sub-buckets per bucket
-constexpr int kOffsB = kRadB + 1;          // offsB row: 1024 starts + the tile's row count
-constexpr int kGroupCap = 2048;            // rows per table in one final group (LDS)
+constexpr int kBitsB = 11;
+constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
+constexpr int kOffsB = kRadB + 1;          // offsB row (u16): 2048 starts + the tile's row count
+constexpr int kGroupCap = 1024;            // rows per table in one final group (LDS)
+constexpr int kStageRange = 4096;          // key range of the staged final path's counting sort
 constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots
-constexpr int kMsdFinalGrid = 512;         // persistent final kernel: 2 workgroups per CU
+constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
+constexpr int kFinWaves = kFinThreads / 64;
+constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
+constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
 constexpr int kSampleMax = 8192;           // sampled keys per table
 constexpr int kMsdSegs = 64;               // segments of the run scans
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
@@ -193,7 +197,9 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     int64_t gmin, gmax;
     int64_t joined;      // written by the count scan
     uint32_t ngroups;    // dense groups (key order)
-    uint32_t pad;
+    uint32_t nwide;      // groups for the 64-bit final path
+    uint32_t nradix;     // groups for the radix-sort final path
+    uint32_t pad2;
 };
 struct MsdBasesParams {
     const uint32_t *segL[2];
@@ -213,16 +219,20 @@ struct MsdPartBParams {
     const uint2 *tinfo;  // per pass-B tile: {bucket, first run-list entry}
     const MsdBucket *bk;
     const MsdPlan *plan;
-    uint32_t *offs;      // [tilesB][kOffsB]
+    uint16_t *offs;      // [tilesB][kOffsB] tile-local sub-bucket starts
     int key_col, x;
 };
 struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
     uint16_t a, flags, b0, b1;
     uint32_t nR, nS, outR, outS;
-    uint32_t pad[2];
+    uint32_t tb[2];      // first pass-B tile of the bucket, per table
+    uint32_t kt[2];      // pass-B tiles of the bucket, per table
+    int64_t base;        // smallest key the group's sub-buckets can hold
+    uint32_t span;       // keys the group's sub-buckets can hold (saturated): key - base < span
+    uint32_t pad[3];
 };
 struct MsdGroupParams {
-    const uint32_t *offs[2];
+    const uint16_t *offs[2];
     const MsdBucket *bk[2];
     int tile[2];
     int ntab;
@@ -235,7 +245,7 @@ struct MsdGroupParams {
 };
 struct MsdTab {          // a table as the final kernels see it
     const int64_t *tempB;
-    const uint32_t *offs;
+    const uint16_t *offs;
     const MsdBucket *bk;
     int64_t *out;        // sorted rows
     int tile, cols, key, x;
@@ -247,7 +257,9 @@ struct MsdFinalParams {
     uint32_t *counts;
     MsdPlan *plan;
     uint32_t *big_list;
-    int ntab, join, key2, pad;
+    uint32_t *wide_list; // dense indices of groups for msd_final_wide_kernel
+    uint32_t *radix_list;// groups for the radix tier (msd_final_kernel in list mode; nullptr = contiguous mode)
+    int ntab, join, key2, dbg;
 };
 
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
@@ -266,6 +278,7 @@ hipError_t launch_msd_gather(const MsdTab &tb, const MsdGroup *groups, uint32_t 
                              int64_t *dst, hipStream_t s);
 hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
                               const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, hipStream_t s);
+hipError_t read_msd_phases(unsigned long long *out16);  // diagnostic (SMJ_DEBUG_MSD=1)
 // exclusive scan of the plan->ngroups dense group counts -> offs, total -> plan->joined
 hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *offs, MsdPlan *plan, hipStream_t s);
 // exclusive scan of n u32 counts -> offs, total -> *total (one workgroup)

@@ -389,9 +389,11 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
             const unsigned __int128 one73 = (unsigned __int128)1 << (64 + kBitsB);
             const unsigned __int128 q = one73 / ((unsigned __int128)range + 1u);
             scale = q >> 64 ? ~0ull : (uint64_t)q;
-            // keys per sub-bucket <= ceil((range + 1) / kRadB) + 1: spans keep group ranges < 2^48
+            // keys per sub-bucket <= ceil((range + 1) / kRadB) + 1 =: w.  Group spans stay
+            // within the final kernel's counting range when one sub-bucket fits it,
+            // else below 2^48 (the radix tiers' sort word)
             const uint64_t w = (range >> kBitsB) + 2u;
-            const uint64_t span = ((uint64_t)1 << 48) / w;
+            const uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
             maxspan = span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
         }
     }
@@ -547,7 +549,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    for (int d = tid; d <= RADIX; d += kMsdThreads) p.offs[g * kOffsB + d] = s_bin[d];  // s_bin[RADIX] = nrows
+    for (int d = tid; d <= RADIX; d += kMsdThreads) p.offs[g * kOffsB + d] = (uint16_t)s_bin[d];  // [RADIX] = nrows
     __syncthreads();
     int64_t *dst = p.out + g * T * COLS;
 #pragma unroll
@@ -562,37 +564,57 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
 // ---------------------------------------------------------------------------
 // group: pack the sub-buckets of every bucket into final groups
 // ---------------------------------------------------------------------------
-// one workgroup of kRadB threads per bucket a (thread = sub-bucket): per-table
-// sub-bucket totals, their prefixes, greedy packing into groups written to
-// slots a * kRadB + j.  msd_group_pack_kernel then lays them out densely.
-__global__ __launch_bounds__(kRadB) void msd_group_kernel(const MsdGroupParams p) {
-    constexpr int NW = kRadB / 64;
+// one workgroup of 1024 threads per bucket a; thread t owns sub-buckets
+// [t*SB, t*SB + SB): per-table sub-bucket totals and prefixes, then greedy
+// packing into groups written to slots a * kRadB + j.  msd_group_pack_kernel
+// then lays them out densely.
+constexpr int kGroupThreads = 1024;
+__global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroupParams p) {
+    constexpr int NW = kGroupThreads / 64, SB = kRadB / kGroupThreads;
     __shared__ uint32_t s_tot[2][kRadB];
     __shared__ uint32_t s_pre[2][kRadB];
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];  // groups: sub-buckets [b0, b1)
     __shared__ int s_ng;
-    const int a = blockIdx.x, b = threadIdx.x;
+    const int a = blockIdx.x, t = threadIdx.x;
     for (int x = 0; x < 2; x++) {
-        uint32_t tot = 0;
+        uint32_t tot[SB];
+#pragma unroll
+        for (int i = 0; i < SB; i++) tot[i] = 0;
         if (x < p.ntab) {
             const MsdBucket bk = p.bk[x][a];
             const uint32_t K = (bk.L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
-            const uint32_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + b;
-#pragma unroll 4
-            for (uint32_t k = 0; k < K; k++) tot += o[(int64_t)k * kOffsB + 1] - o[(int64_t)k * kOffsB];
+            const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
+#pragma unroll 2
+            for (uint32_t k = 0; k < K; k++) {
+                const uint16_t *r = o + (int64_t)k * kOffsB;
+                uint32_t prev = r[0];
+#pragma unroll
+                for (int i = 0; i < SB; i++) {
+                    const uint32_t nx = r[i + 1];
+                    tot[i] += nx - prev;
+                    prev = nx;
+                }
+            }
         }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int i = 0; i < SB; i++) sum += tot[i];
         uint32_t all;
-        const uint32_t ex = block_excl_scan<NW>(tot, s_wsum, &all);
-        s_tot[x][b] = tot;
-        s_pre[x][b] = ex;
+        uint32_t ex = block_excl_scan<NW>(sum, s_wsum, &all);
+#pragma unroll
+        for (int i = 0; i < SB; i++) {
+            s_tot[x][t * SB + i] = tot[i];
+            s_pre[x][t * SB + i] = ex;
+            ex += tot[i];
+        }
     }
     __syncthreads();
     const bool single_sub = (a & 1) || p.bk[0][a].scale == 0;  // every sub-bucket holds one key value
-    // a group spans < 2^48 key values, so that (residual << 16 | index) fits one
+    // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
-    if (b == 0) {  // greedy packing; a group that is over the cap holds exactly one sub-bucket
+    if (t == 0) {  // greedy packing; a group that is over the cap holds exactly one sub-bucket
         int ng = 0, b0 = -1, last = -1;
         uint32_t cr = 0, cs = 0;
         for (int j = 0; j < kRadB; j++) {
@@ -619,20 +641,38 @@ __global__ __launch_bounds__(kRadB) void msd_group_kernel(const MsdGroupParams p
         p.ngrp[a] = (uint32_t)ng;
     }
     __syncthreads();
-    const int j = b;
-    if (j >= s_ng) return;
-    const uint32_t b0 = s_g0[j], b1 = s_g1[j];
-    MsdGroup gr{};
-    gr.a = (uint16_t)a;
-    gr.b0 = (uint16_t)b0;
-    gr.b1 = (uint16_t)b1;
-    gr.nR = s_pre[0][b1 - 1] + s_tot[0][b1 - 1] - s_pre[0][b0];
-    gr.nS = s_pre[1][b1 - 1] + s_tot[1][b1 - 1] - s_pre[1][b0];
-    gr.outR = p.bk[0][a].row_start + s_pre[0][b0];
-    gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_pre[1][b0] : 0u;
-    gr.flags = 0;
-    if (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap) gr.flags = single_sub ? kGroupSingle : kGroupBig;
-    p.slot_groups[(int64_t)a * kRadB + j] = gr;
+    for (int j = t; j < s_ng; j += kGroupThreads) {
+        const uint32_t b0 = s_g0[j], b1 = s_g1[j];
+        MsdGroup gr{};
+        gr.a = (uint16_t)a;
+        gr.b0 = (uint16_t)b0;
+        gr.b1 = (uint16_t)b1;
+        gr.nR = s_pre[0][b1 - 1] + s_tot[0][b1 - 1] - s_pre[0][b0];
+        gr.nS = s_pre[1][b1 - 1] + s_tot[1][b1 - 1] - s_pre[1][b0];
+        gr.outR = p.bk[0][a].row_start + s_pre[0][b0];
+        gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_pre[1][b0] : 0u;
+        gr.flags = 0;
+        if (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap)
+            gr.flags = single_sub ? kGroupSingle : kGroupBig;
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            gr.tb[x] = x < p.ntab ? p.bk[x][a].tile_base : 0u;
+            gr.kt[x] = x < p.ntab ? (p.bk[x][a].L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x] : 0u;
+        }
+        // key interval of sub-buckets [b0, b1): residuals r = key - lo with
+        // digit(r) = floor(r * scale / 2^64) in [b0, b1) satisfy rmin(b0) <= r < rmin(b1),
+        // rmin(b) = ceil(b * 2^64 / scale); with scale == 0 the digit is r itself
+        const uint64_t sc = p.bk[0][a].scale;
+        unsigned __int128 r0 = b0, r1 = b1;
+        if (sc) {
+            r0 = (((unsigned __int128)b0 << 64) + sc - 1) / sc;
+            r1 = (((unsigned __int128)b1 << 64) + sc - 1) / sc;
+        }
+        gr.base = (int64_t)((uint64_t)p.bk[0][a].lo + (uint64_t)r0);
+        const unsigned __int128 sp = r1 - r0;
+        gr.span = sp > 0xffffffffu ? 0xffffffffu : (uint32_t)sp;
+        p.slot_groups[(int64_t)a * kRadB + j] = gr;
+    }
 }
 
 // grid kBucketsA x 256: bucket a's groups -> dense (key-ordered) indices
@@ -923,15 +963,903 @@ __device__ __forceinline__ void final_group(const MsdFinalParams &p, const int64
     }
 }
 
-// persistent: workgroup b takes dense groups b, b + grid, ... (key order)
-template <int C1, int C2>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_final_kernel(const MsdFinalParams p) {
-    __shared__ FinalSmem sm;
-    const int64_t ng = p.plan->ngroups;
-    for (int64_t gi = blockIdx.x; gi < ng; gi += gridDim.x) {
-        final_group<C1, C2>(p, gi, sm);
-        __syncthreads();  // LDS reused by the next group
+// ---- fast path ---------------------------------------------------------------
+// A group whose key range fits 21 bits (residual << 11 | row fits one 32-bit
+// sort word) and whose buckets have <= kFinThreads pass-B tiles per table is
+// sorted with 32-bit words, both tables ranked in the same LSD passes (four
+// barriers per pass), and software-pipelined one group deep: while group i
+// is written out and joined, the key gathers of group i + 1 are in flight.
+// Every other group goes to the wide list (msd_final_wide_kernel).
+constexpr int kFinIt = kGroupCap / kFinThreads;  // rows per table per thread
+constexpr int kFinIdxBits = 10;
+constexpr int kFinResBits = 32 - kFinIdxBits;     // 22-bit key residuals
+static_assert(kGroupCap == (1 << kFinIdxBits), "sort word = residual << 10 | group row");
+
+constexpr int kCountRange = 4096;  // counting-sort residual range (packed u16 bins)
+constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re-orders
+
+struct FinSmem {
+    uint32_t key[2][kGroupCap];   // sort words, sorted in place (via tmp)
+    uint32_t addr[2][kGroupCap];  // tempB row of group row v
+    union {
+        struct {
+            uint32_t tmp[2][kGroupCap];  // radix ping-pong; the next group's run lists (uint2[2][kFinThreads])
+            uint32_t cnt[2][kFinWaves][256];
+        };
+        uint32_t hist[2][kCountRange / 2];  // counting sort: two u16 bins per word
+    };
+    uint32_t bin[2][256];
+    uint32_t wsum[2][kFinWaves];  // double-buffered block-scan wave sums
+    uint32_t flag[2];
+    int64_t mm[2 * kFinWaves];
+};
+
+// exclusive block scan without the trailing barrier: callers alternate wsum
+// buffers so that the next scan cannot overwrite sums still being read
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan_nb(uint32_t v, uint32_t *s_wsum, uint32_t *total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const uint32_t x = s_wsum[w];
+        before += (w < wave) ? x : 0u;
+        all += x;
     }
+    *total = all;
+    return before + incl - v;
+}
+
+struct FinalPref {               // the group whose keys are in flight
+    uint32_t o0[2], o1[2];       // offsB[tile][b0], offsB[tile][b1] of this thread's tile
+    int64_t key[2][kFinIt];      // gathered keys (row v = tid + k * kFinThreads)
+    uint32_t src[2][kFinIt];     // their tempB rows
+};
+
+__device__ __forceinline__ uint32_t fin_tiles(const MsdTab &tb, uint16_t a) {
+    const uint32_t L = tb.bk[a].L;
+    return (L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
+}
+
+__device__ __forceinline__ bool fin_fast(const MsdFinalParams &p, const MsdGroup &g) {
+    return fin_tiles(p.tab[0], g.a) <= (uint32_t)kFinThreads &&
+           (p.ntab < 2 || fin_tiles(p.tab[1], g.a) <= (uint32_t)kFinThreads);
+}
+
+__device__ __forceinline__ void fin_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
+                                              uint32_t (&o1)[2]) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        o0[x] = o1[x] = 0;
+        if (x < p.ntab && tid < fin_tiles(p.tab[x], g.a)) {
+            const int64_t id = (int64_t)p.tab[x].bk[g.a].tile_base + tid;
+            o0[x] = p.tab[x].offs[id * kOffsB + g.b0];
+            o1[x] = p.tab[x].offs[id * kOffsB + g.b1];
+        }
+    }
+}
+
+// run lists of group g from its offsB values (into sm.tmp), then the key
+// gathers of its rows (fixed-step searches, interleaved over the rows)
+template <int C1, int C2>
+__device__ __forceinline__ void fin_issue_keys(const MsdFinalParams &p, const MsdGroup &g, FinalPref &f,
+                                               FinSmem &sm, int &wsb) {
+    const uint32_t tid = threadIdx.x;
+    uint2 *s_list = reinterpret_cast<uint2 *>(&sm.tmp[0][0]);  // [x * kFinThreads + tile]
+    const uint32_t lenR = f.o1[0] - f.o0[0], lenS = f.o1[1] - f.o0[1];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_nb<kFinWaves>(lenR | (lenS << 16), sm.wsum[wsb], &tot);  // halves <= kGroupCap
+    wsb ^= 1;
+    uint32_t K[2];
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        K[x] = x < p.ntab ? fin_tiles(p.tab[x], g.a) : 0u;
+        if (tid < K[x]) {
+            const uint32_t id = p.tab[x].bk[g.a].tile_base + tid;
+            s_list[x * kFinThreads + tid] =
+                make_uint2(id * (uint32_t)p.tab[x].tile + f.o0[x], x ? (ex >> 16) : (ex & 0xffffu));
+        }
+    }
+    __syncthreads();
+    const uint32_t n[2] = {g.nR, p.ntab > 1 ? g.nS : 0u};
+    uint32_t pos[2][kFinIt];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) pos[x][k] = 0;
+#pragma unroll
+    for (int step = kFinThreads / 2; step >= 1; step >>= 1) {  // last range starting at or before v
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < kFinIt; k++) {
+                const uint32_t v = tid + k * kFinThreads, q = pos[x][k] + step;
+                if (q < K[x] && s_list[x * kFinThreads + q].y <= v) pos[x][k] = q;
+            }
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        const MsdTab &tb = p.tab[x];
+        const int cols = C1 > 0 ? (x ? C2 : C1) : tb.cols;
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) {
+            const uint32_t v = tid + k * kFinThreads;
+            const uint2 e = s_list[x * kFinThreads + pos[x][k]];
+            const uint32_t src = e.x + (v - e.y);
+            f.src[x][k] = src;
+            f.key[x][k] = v < n[x] ? tb.tempB[(int64_t)src * cols + tb.key] : 0;
+        }
+    }
+}
+
+// one stable LSD pass over both tables' sort words by the 8-bit digit at shift
+__device__ __forceinline__ void fin_radix_pass(const uint32_t (*src)[kGroupCap], uint32_t (*dst)[kGroupCap],
+                                               const int (&n)[2], int shift, FinSmem &sm, int &wsb) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t val[2][kFinIt], dig[2][kFinIt], vm[2];
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t *wc = sm.cnt[x][wave];
+        zero_counters<256>(wc, lane);
+        vm[x] = 0;
+#pragma unroll
+        for (int it = 0; it < kFinIt; it++) {
+            const int e = (wave * kFinIt + it) * 64 + lane;
+            const bool v = e < n[x];
+            val[x][it] = v ? src[x][e] : 0u;
+            dig[x][it] = (val[x][it] >> shift) & 255u;
+            vm[x] |= v ? (1u << it) : 0u;
+        }
+        wave_rank<kFinIt, 8>(dig[x], vm[x], wc, lane);
+    }
+    __syncthreads();
+    uint32_t packed = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            uint32_t c[kFinWaves];
+#pragma unroll
+            for (int w = 0; w < kFinWaves; w++) c[w] = sm.cnt[x][w][tid];
+            uint32_t t = 0;
+#pragma unroll
+            for (int w = 0; w < kFinWaves; w++) {
+                sm.cnt[x][w][tid] = t;
+                t += c[w];
+            }
+            packed |= t << (16 * x);
+        }
+    }
+    uint32_t all;
+    const uint32_t ex = block_excl_scan_nb<kFinWaves>(packed, sm.wsum[wsb], &all);
+    wsb ^= 1;
+    if (tid < 256) {
+        sm.bin[0][tid] = ex & 0xffffu;
+        sm.bin[1][tid] = ex >> 16;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int it = 0; it < kFinIt; it++)
+            if ((vm[x] >> it) & 1u) {
+                const uint32_t d = dig[x][it] & 0xffffu;
+                dst[x][sm.bin[x][d] + sm.cnt[x][wave][d] + (dig[x][it] >> 16)] = val[x][it];
+            }
+    __syncthreads();
+}
+
+// Counting sort of both tables' sort words (residual < kCountRange): packed
+// u16 histograms (LDS atomics), one block scan for both tables, scatter, and
+// a re-ordering of equal-residual runs by group row (atomics place them in
+// arbitrary order).  False (nothing written) when a residual repeats more
+// than kMaxDupRun times: the radix path then sorts the group.
+__device__ __forceinline__ bool fin_count_sort(const uint32_t (&w)[2][kFinIt], const int (&n)[2], FinSmem &sm,
+                                               int &wsb) {
+    const int tid = threadIdx.x;
+    uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+    for (int i = tid; i < kCountRange / 4; i += kFinThreads) h4[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) sm.flag[wsb] = 0;
+    __syncthreads();
+    uint32_t rank[2][kFinIt];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) {
+            rank[x][k] = 0;
+            if (w[x][k] != ~0u) {
+                const uint32_t res = w[x][k] >> kFinIdxBits, sh = 16u * (res & 1u);
+                rank[x][k] = (atomicAdd(&sm.hist[x][res >> 1], 1u << sh) >> sh) & 0xffffu;
+            }
+        }
+    __syncthreads();
+    // exclusive starts: thread t owns words [t*W, t*W + W) of each table's histogram
+    constexpr int W = kCountRange / 2 / kFinThreads;
+    uint32_t tot = 0, heavy = 0;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i];
+            heavy |= ((h & 0xffffu) > (uint32_t)kMaxDupRun) | ((h >> 16) > (uint32_t)kMaxDupRun);
+            t += (h & 0xffffu) + (h >> 16);
+        }
+        tot |= t << (16 * x);
+    }
+    if (heavy) sm.flag[wsb] = 1;
+    uint32_t all;
+    const uint32_t ex = block_excl_scan_nb<kFinWaves>(tot, sm.wsum[wsb], &all);  // its barrier publishes flag[wsb]
+    const bool bail = sm.flag[wsb] != 0;
+    wsb ^= 1;
+    if (bail) {
+        __syncthreads();  // everyone read the flag before the radix path reuses the region
+        return false;
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i];
+            sm.hist[x][tid * W + i] = run | ((run + (h & 0xffffu)) << 16);
+            run += (h & 0xffffu) + (h >> 16);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++)
+            if (w[x][k] != ~0u) {
+                const uint32_t res = w[x][k] >> kFinIdxBits, sh = 16u * (res & 1u);
+                sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + rank[x][k]] = w[x][k];
+            }
+    __syncthreads();
+    // runs of one residual: insertion sort by word (= by group row), <= kMaxDupRun long
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) {
+            const int q = tid * kFinIt + k;
+            if (q + 1 < n[x]) {
+                const uint32_t rq = sm.key[x][q] >> kFinIdxBits;
+                if ((sm.key[x][q + 1] >> kFinIdxBits) == rq && (q == 0 || (sm.key[x][q - 1] >> kFinIdxBits) != rq)) {
+                    int e = q + 1;
+                    while (e < n[x] && (sm.key[x][e] >> kFinIdxBits) == rq) e++;
+                    for (int a = q + 1; a < e; a++) {
+                        const uint32_t v = sm.key[x][a];
+                        int b = a - 1;
+                        while (b >= q && sm.key[x][b] > v) {
+                            sm.key[x][b + 1] = sm.key[x][b];
+                            b--;
+                        }
+                        sm.key[x][b + 1] = v;
+                    }
+                }
+            }
+        }
+    __syncthreads();
+    return true;
+}
+
+// sort a group whose keys are in f; false when its key range is wider than
+// 21 bits (the group then goes to the wide list)
+__device__ __forceinline__ bool fin_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, const FinalPref &f,
+                                         FinSmem &sm, int &wsb) {
+    const int tid = threadIdx.x;
+    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) {
+            const int v = tid + k * kFinThreads;
+            if (v < n[x]) {
+                mn = min(mn, f.key[x][k]);
+                mx = max(mx, f.key[x][k]);
+                sm.addr[x][v] = f.src[x][k];
+            }
+        }
+    block_minmax<kFinWaves>(mn, mx, sm.mm);
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn;
+    const int bits = range ? 64 - __clzll((long long)range) : 0;
+    if (bits > kFinResBits) {
+        if (tid == 0) p.wide_list[atomicAdd(&p.plan->nwide, 1u)] = (uint32_t)gi;
+        return false;
+    }
+    uint32_t w[2][kFinIt];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++) {
+            const int v = tid + k * kFinThreads;
+            w[x][k] = v < n[x] ? ((uint32_t)((uint64_t)f.key[x][k] - (uint64_t)mn) << kFinIdxBits) | (uint32_t)v : ~0u;
+        }
+    if (range < (uint64_t)kCountRange && !(p.dbg & 32) && fin_count_sort(w, n, sm, wsb)) return true;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kFinIt; k++)
+            if (w[x][k] != ~0u) sm.key[x][tid + k * kFinThreads] = w[x][k];
+    __syncthreads();
+    const int npass = (p.dbg & 2) ? 0 : (bits + 7) >> 3;
+    for (int ps = 0; ps < npass; ps++) {
+        const bool fwd = (ps & 1) == 0;
+        fin_radix_pass(fwd ? sm.key : sm.tmp, fwd ? sm.tmp : sm.key, n, kFinIdxBits + 8 * ps, sm, wsb);
+    }
+    if (npass & 1) {
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+            for (int v = tid; v < n[x]; v += kFinThreads) sm.key[x][v] = sm.tmp[x][v];
+        __syncthreads();
+    }
+    return true;
+}
+
+// # of a[0, n) below t (a sorted), n <= kGroupCap: 12 fixed steps
+__device__ __forceinline__ int fin_lb(const uint32_t *a, int n, uint32_t t) {
+    int pos = 0;
+#pragma unroll
+    for (int step = kGroupCap; step >= 1; step >>= 1)
+        if (pos + step <= n && a[pos + step - 1] < t) pos += step;
+    return pos;
+}
+
+// sorted rows of both tables to their final places, then the zip join
+template <int C1, int C2>
+__device__ __forceinline__ void fin_out_join(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, FinSmem &sm,
+                                             int &wsb) {
+    const int tid = threadIdx.x;
+    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
+    constexpr uint32_t IDX = (1u << kFinIdxBits) - 1u;
+    if (p.dbg & 4) {
+    } else if constexpr (C1 == 2 && C2 == 2) {
+        i64x2 r[2][kFinIt];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < kFinIt; k++) {
+                const int v = tid + k * kFinThreads;
+                const uint32_t src = sm.addr[x][sm.key[x][v < n[x] ? v : 0] & IDX];
+                r[x][k] = n[x] ? reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[src] : i64x2{0, 0};
+            }
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            i64x2 *dst = reinterpret_cast<i64x2 *>(p.tab[x].out) + (x ? g.outS : g.outR);
+#pragma unroll
+            for (int k = 0; k < kFinIt; k++) {
+                const int v = tid + k * kFinThreads;
+                if (v < n[x]) dst[v] = r[x][k];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            if (n[x] == 0) continue;
+            const MsdTab &tb = p.tab[x];
+            const int cols = C1 > 0 ? (x ? C2 : C1) : tb.cols;
+            int64_t *dst = tb.out + (int64_t)(x ? g.outS : g.outR) * cols;
+            for (int v = tid; v < n[x]; v += kFinThreads) {
+                const uint32_t src = sm.addr[x][sm.key[x][v] & IDX];
+                copy_row<0>(tb.tempB + (int64_t)src * cols, dst + (int64_t)v * cols, cols);
+            }
+        }
+    }
+    if (!p.join) return;
+    // zip join: R position i pairs with S position lbS(k) + (i - lbR(k)).
+    // Thread t owns R positions [t*kFinIt, t*kFinIt + kFinIt).
+    const int nR = n[0], nS = n[1];
+    const uint32_t *kR = sm.key[0], *kS = sm.key[1];
+    uint32_t part[kFinIt], mmask = 0;
+    if (nS > 0 && nR > 0 && !(p.dbg & 16)) {
+        // merge-style lookups: one search for the thread's first key, then
+        // short forward walks (keys ascend along the thread's positions)
+        int lbR = 0, lbS = 0;
+        uint32_t prev = ~0u;
+#pragma unroll
+        for (int q = 0; q < kFinIt; q++) {
+            const int i = tid * kFinIt + q;
+            part[q] = 0;
+            if (i < nR) {
+                const uint32_t kk = kR[i] & ~IDX;
+                if (kk != prev) {
+                    if (q == 0) {
+                        lbR = (i > 0 && (kR[i - 1] & ~IDX) == kk) ? fin_lb(kR, i, kk) : i;
+                        lbS = fin_lb(kS, nS, kk);
+                    } else {
+                        lbR = i;
+                        int j = lbS, steps = 0;
+                        while (j < nS && (kS[j] & ~IDX) < kk && steps < 16) {
+                            j++;
+                            steps++;
+                        }
+                        lbS = (j < nS && (kS[j] & ~IDX) < kk) ? fin_lb(kS, nS, kk) : j;
+                    }
+                    prev = kk;
+                }
+                const int j = lbS + (i - lbR);
+                if (j < nS && (kS[j] & ~IDX) == kk) {
+                    part[q] = (uint32_t)j;
+                    mmask |= 1u << q;
+                }
+            }
+        }
+    }
+    uint32_t total;
+    uint32_t o = block_excl_scan_nb<kFinWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
+    wsb ^= 1;
+    if (tid == 0) p.counts[gi] = total;
+    if (total == 0 || (p.dbg & 8)) return;
+    const int c1 = C1 > 0 ? C1 : p.tab[0].cols, c2 = C2 > 0 ? C2 : p.tab[1].cols, tc = c1 + c2 - 1;
+    int64_t *dst = p.slots + (int64_t)g.outR * tc;
+#pragma unroll
+    for (int q = 0; q < kFinIt; q++) {
+        if ((mmask >> q) & 1u) {
+            const int i = tid * kFinIt + q;
+            const uint32_t ra = sm.addr[0][kR[i] & IDX];
+            const uint32_t sa = sm.addr[1][kS[part[q]] & IDX];
+            emit_join_row<C1, C2>(p.tab[0].tempB + (int64_t)ra * c1, p.tab[1].tempB + (int64_t)sa * c2,
+                                  dst + (int64_t)o * tc, c1, c2, p.key2);
+            o++;
+        }
+    }
+}
+
+// Diagnostic phase stamps of msd_final (SMJ_DEBUG_MSD=1; off in production):
+// s_memtime cycles of thread 0 per phase, summed over workgroups.
+__device__ unsigned long long g_fin_phase[16];
+#define FIN_STAMP(k)                                                \
+    if (p.dbg) {                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph[k] += t_ - ph_t;                                         \
+        ph_t = t_;                                                  \
+    }
+
+// persistent: workgroup b takes a contiguous range of dense groups (key
+// order), so consecutive groups share their bucket's tiles
+template <int C1, int C2>
+__global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p) {
+    __shared__ FinSmem sm;
+    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    // contiguous mode: workgroup b walks a range of dense groups (pipelined one
+    // group deep); list mode: the groups msd_final_stage_kernel handed over
+    const bool lm = p.radix_list != nullptr;
+    int64_t gb, ge, step;
+    if (lm) {
+        gb = blockIdx.x;
+        ge = p.plan->nradix;
+        step = gridDim.x;
+    } else {
+        const int64_t ng = p.plan->ngroups, per = (ng + gridDim.x - 1) / gridDim.x;
+        gb = (int64_t)blockIdx.x * per;
+        ge = min(ng, gb + per);
+        step = 1;
+    }
+    FinalPref f;
+    int wsb = 0;
+    bool have = false;  // f holds the keys of group gi
+    for (int64_t it = gb; it < ge; it += step) {
+        const int64_t gi = lm ? (int64_t)p.radix_list[it] : it;
+        const MsdGroup g = p.groups[gi];
+        if (g.flags) {
+            have = false;
+            continue;
+        }
+        if (!fin_fast(p, g)) {
+            if (threadIdx.x == 0) p.wide_list[atomicAdd(&p.plan->nwide, 1u)] = (uint32_t)gi;
+            have = false;
+            continue;
+        }
+        if (!have) {
+            fin_load_offs(p, g, f.o0, f.o1);
+            fin_issue_keys<C1, C2>(p, g, f, sm, wsb);
+        }
+        FIN_STAMP(0);
+        MsdGroup gn{};
+        bool nfast = false;
+        if (!lm && gi + 1 < ge) {
+            gn = p.groups[gi + 1];
+            nfast = !gn.flags && fin_fast(p, gn);
+        }
+        uint32_t o0[2], o1[2];  // the next group's offsB values, in flight during the sort
+        if (nfast) fin_load_offs(p, gn, o0, o1);
+        FIN_STAMP(1);
+        const bool ok = fin_sort(p, g, gi, f, sm, wsb);
+        FIN_STAMP(2);
+        if (nfast) {  // sm.tmp is free after the sort: the next run lists, its key gathers
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                f.o0[x] = o0[x];
+                f.o1[x] = o1[x];
+            }
+            fin_issue_keys<C1, C2>(p, gn, f, sm, wsb);
+        }
+        FIN_STAMP(3);
+        if (ok) fin_out_join<C1, C2>(p, g, gi, sm, wsb);
+        FIN_STAMP(4);
+        have = nfast;
+        __syncthreads();  // LDS reused by the next group
+        FIN_STAMP(5);
+        if (p.dbg) ph[9]++;
+    }
+    if (p.dbg && threadIdx.x == 0)
+        for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
+}
+
+// ---- 2-column staged path --------------------------------------------------------
+// The common case, (key, payload) tables: every row of a group is gathered
+// ONCE (16 B, lanes on consecutive rows of a pass-B tile range) into an LDS
+// stage; the 32-bit sort words (key - base) << 10 | row are counting-sorted
+// (base and key span come from the group record, no reduction); the zip
+// join reads its run starts straight from the histogram; sorted rows and
+// join rows leave through LDS as coalesced stores.  The next group's rows
+// are gathered into registers while this one is sorted and written.  Groups
+// outside its limits (key span > kStageRange, an equal-key run >
+// kMaxDupRun, > kStThreads pass-B tiles) go to the radix list.
+constexpr int kStThreads = 512, kStWaves = kStThreads / 64;
+constexpr int kStIt = kGroupCap / kStThreads;  // rows per table per thread
+constexpr int kStRange = kStageRange;
+constexpr int kStRecs = 64;                    // group records per LDS chunk (two chunks in flight)
+static_assert(kFinIdxBits == 10, "sort word = residual << 10 | group row");
+
+struct StSmem {
+    i64x2 stage[2][kGroupCap];        // rows in gather order
+    uint32_t key[2][kGroupCap];       // sort words, sorted
+    uint32_t hist[2][kStRange / 2];   // packed u16 bins (zeroed for the next group during the emit)
+    union {
+        struct {
+            uint2 list[2][kStThreads];             // run lists of the next group: {tempB row, group row}
+            uint16_t at[2][kGroupCap];             // list entry of the non-empty range starting at row v
+            uint32_t starts[2][kGroupCap / 32];    // bitmap: a non-empty range starts at row v
+            uint16_t btab[2][kGroupCap / 64];      // list entry holding row 64 * b
+        } L;
+        uint32_t match[kGroupCap];       // join rows: R position << 10 | S position
+    };
+    MsdGroup recs[2 * kStRecs];       // ring of this workgroup's group records
+    uint32_t wsum[2][kStWaves];
+    uint32_t flag[2];
+};
+
+__device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g) {
+    return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStThreads &&
+           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStThreads);
+}
+
+__device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
+                                             uint32_t (&o1)[2]) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        o0[x] = o1[x] = 0;
+        if (x < p.ntab && tid < g.kt[x]) {
+            const int64_t id = (int64_t)g.tb[x] + tid;
+            o0[x] = p.tab[x].offs[id * kOffsB + g.b0];
+            o1[x] = p.tab[x].offs[id * kOffsB + g.b1];
+        }
+    }
+}
+
+// run lists from the offsB values (union region), then the row gathers of
+// group g into registers (row v = tid + k * kStThreads).  Row v's range is
+// found in O(1): the range holding the wave's first row (btab) and the last
+// non-empty range starting in (64b, v] (bitmap word + at[]).
+__device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
+                                         const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
+    const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_nb<kStWaves>(len[0] | (len[1] << 16), sm.wsum[wsb], &tot);  // + barrier
+    wsb ^= 1;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        if (tid < g.kt[x] && x < p.ntab) {
+            const uint32_t vs = x ? (ex >> 16) : (ex & 0xffffu);
+            sm.L.list[x][tid] = make_uint2((g.tb[x] + tid) * (uint32_t)p.tab[x].tile + o0[x], vs);
+            if (len[x]) {
+                sm.L.at[x][vs] = (uint16_t)tid;
+                atomicOr(&sm.L.starts[x][vs >> 5], 1u << (vs & 31));
+                for (uint32_t b = (vs + 63) >> 6; b << 6 < vs + len[x]; b++) sm.L.btab[x][b] = (uint16_t)tid;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n[2] = {g.nR, p.ntab > 1 ? g.nS : 0u};
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t v = tid + k * kStThreads, b = v >> 6;
+            i64x2 r = {0, 0};
+            if (v < n[x]) {
+                const uint64_t m = ((uint64_t)sm.L.starts[x][2 * b + 1] << 32 | sm.L.starts[x][2 * b]) &
+                                   ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
+                const uint32_t j = m ? sm.L.at[x][(b << 6) + 63 - __clzll((long long)m)] : sm.L.btab[x][b];
+                const uint2 e = sm.L.list[x][j];
+                r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[e.x + (v - e.y)];
+            }
+            rows[x][k] = r;
+        }
+}
+
+__device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key ? r.y : r.x; }
+
+// stage + counting sort of group g whose rows are in `rows`, then the zip
+// join lookups (mmask / part); false: an equal-key run over kMaxDupRun (the
+// group is handed to the radix list)
+__device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
+                                        const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
+                                        uint32_t (&part)[kStIt]) {
+    const int tid = threadIdx.x;
+    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
+    uint32_t w[2][kStIt], rank[2][kStIt];
+    if (tid == 0) sm.flag[wsb] = 0;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const int v = tid + k * kStThreads;
+            w[x][k] = ~0u;
+            rank[x][k] = 0;
+            if (v < n[x]) {
+                sm.stage[x][v] = rows[x][k];
+                const uint32_t res = (uint32_t)((uint64_t)st_key(rows[x][k], p.tab[x].key) - (uint64_t)g.base);
+                w[x][k] = (res << kFinIdxBits) | (uint32_t)v;
+                const uint32_t sh = 16u * (res & 1u);
+                rank[x][k] = (atomicAdd(&sm.hist[x][res >> 1], 1u << sh) >> sh) & 0xffffu;
+            }
+        }
+    __syncthreads();
+    constexpr int W = kStRange / 2 / kStThreads;  // histogram words per thread
+    uint32_t tot = 0, heavy = 0, dup = 0;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i], lo = h & 0xffffu, hi = h >> 16;
+            heavy |= (lo > (uint32_t)kMaxDupRun) | (hi > (uint32_t)kMaxDupRun);
+            dup |= (lo > 1u) | (hi > 1u);
+            t += lo + hi;
+        }
+        tot |= t << (16 * x);
+    }
+    if (heavy | dup) atomicOr(&sm.flag[wsb], heavy ? 3u : 1u);
+    uint32_t all;
+    const uint32_t ex = block_excl_scan_nb<kStWaves>(tot, sm.wsum[wsb], &all);  // publishes flag[wsb]
+    const uint32_t fl = sm.flag[wsb];
+    wsb ^= 1;
+    if (fl & 2u) {
+        if (tid == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+        return false;
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i];
+            sm.hist[x][tid * W + i] = run | ((run + (h & 0xffffu)) << 16);
+            run += (h & 0xffffu) + (h >> 16);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int k = 0; k < kStIt; k++)
+            if (w[x][k] != ~0u) {
+                const uint32_t res = w[x][k] >> kFinIdxBits, sh = 16u * (res & 1u);
+                sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + rank[x][k]] = w[x][k];
+            }
+    __syncthreads();
+    if (fl & 1u) {  // equal residuals were placed in atomic order: re-order each run by row
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < kStIt; k++) {
+                const int q = tid * kStIt + k;
+                if (q + 1 < n[x]) {
+                    const uint32_t rq = sm.key[x][q] >> kFinIdxBits;
+                    if ((sm.key[x][q + 1] >> kFinIdxBits) == rq && (q == 0 || (sm.key[x][q - 1] >> kFinIdxBits) != rq)) {
+                        int e = q + 1;
+                        while (e < n[x] && (sm.key[x][e] >> kFinIdxBits) == rq) e++;
+                        for (int a = q + 1; a < e; a++) {
+                            const uint32_t v = sm.key[x][a];
+                            int b = a - 1;
+                            while (b >= q && sm.key[x][b] > v) {
+                                sm.key[x][b + 1] = sm.key[x][b];
+                                b--;
+                            }
+                            sm.key[x][b + 1] = v;
+                        }
+                    }
+                }
+            }
+        __syncthreads();
+    }
+    // zip join from the histogram starts: R position i with residual r pairs
+    // with S position startS(r) + (i - startR(r)) while i - startR(r) < countS(r)
+    mmask = 0;
+    if (p.join && n[0] > 0 && n[1] > 0) {
+#pragma unroll
+        for (int q = 0; q < kStIt; q++) {
+            const int i = tid * kStIt + q;
+            part[q] = 0;
+            if (i < n[0]) {
+                const uint32_t res = sm.key[0][i] >> kFinIdxBits, sh = 16u * (res & 1u);
+                const uint32_t sR = (sm.hist[0][res >> 1] >> sh) & 0xffffu;
+                const uint32_t hS = sm.hist[1][res >> 1];
+                const uint32_t sS = (hS >> sh) & 0xffffu;
+                const uint32_t eS = (res & 1u) ? ((res + 1u < (uint32_t)kStRange) ? (sm.hist[1][(res + 1) >> 1] & 0xffffu)
+                                                                                 : (uint32_t)n[1])
+                                               : (hS >> 16);
+                const uint32_t occ = (uint32_t)i - sR;
+                if (occ < eS - sS) {
+                    part[q] = sS + occ;
+                    mmask |= 1u << q;
+                }
+            }
+        }
+    }
+    return true;
+}
+
+// sorted rows out (coalesced), join rows out (word-coalesced); the histogram
+// is zeroed for the next group here (no one reads it after the lookups)
+__device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, StSmem &sm,
+                                        int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt]) {
+    constexpr uint32_t IDX = (1u << kFinIdxBits) - 1u;
+    const int tid = threadIdx.x;
+    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
+    {
+        uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+        for (int i = tid; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        i64x2 *dst = reinterpret_cast<i64x2 *>(p.tab[x].out) + (x ? g.outS : g.outR);
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const int q = tid + k * kStThreads;
+            if (q < n[x]) dst[q] = sm.stage[x][sm.key[x][q] & IDX];
+        }
+    }
+    if (!p.join) return;
+    const uint32_t *kR = sm.key[0], *kS = sm.key[1];
+    uint32_t total;
+    uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
+    wsb ^= 1;
+    if (tid == 0) p.counts[gi] = total;
+    if (total == 0) return;
+#pragma unroll
+    for (int q = 0; q < kStIt; q++)
+        if ((mmask >> q) & 1u) sm.match[o++] = ((uint32_t)(tid * kStIt + q) << kFinIdxBits) | part[q];
+    __syncthreads();
+    // output word wd = row * 3 + column: R key, R payload, S payload
+    int64_t *dst = p.slots + (int64_t)g.outR * 3;
+    const int key2 = p.key2;
+    for (uint32_t wd = tid; wd < total * 3u; wd += kStThreads) {
+        const uint32_t row = wd / 3u, c = wd - row * 3u;
+        const uint32_t m = sm.match[row];
+        int64_t val;
+        if (c < 2) {
+            const i64x2 r = sm.stage[0][kR[m >> kFinIdxBits] & IDX];
+            val = c ? r.y : r.x;
+        } else {
+            const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
+            val = key2 ? r.x : r.y;
+        }
+        dst[wd] = val;
+    }
+}
+
+// copy group records [r0, r0 + kStRecs) of the range into ring half h
+__device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t r0, int64_t ge, StSmem &sm, int h) {
+    constexpr int WORDS = sizeof(MsdGroup) / 8;
+    const int64_t *src = reinterpret_cast<const int64_t *>(p.groups + r0);
+    int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
+    const int64_t nw = min((int64_t)kStRecs, ge - r0) * WORDS;
+    for (int64_t i = threadIdx.x; i < nw; i += kStThreads) dst[i] = src[i];
+}
+
+// persistent staged kernel over contiguous ranges of dense groups
+__global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const MsdFinalParams p) {
+    __shared__ StSmem sm;
+    const int64_t ng = p.plan->ngroups;
+    const int64_t per = (ng + gridDim.x - 1) / gridDim.x;
+    const int64_t gb = (int64_t)blockIdx.x * per, ge = min(ng, gb + per);
+    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    {
+        uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+        for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+    }
+    if (gb < ge) st_load_recs(p, gb, ge, sm, 0);
+    if (gb + kStRecs < ge) st_load_recs(p, gb + kStRecs, ge, sm, 1);
+    __syncthreads();
+    i64x2 cur[2][kStIt];
+    int wsb = 0;
+    bool have = false;  // cur holds the rows of group gi
+    for (int64_t gi = gb; gi < ge; gi++) {
+        const int64_t li = gi - gb;
+        if (li >= kStRecs && li % kStRecs == 0) {  // entering chunk c: fetch chunk c + 1 into the other half
+            const int64_t c = li / kStRecs;
+            __syncthreads();
+            if (gi + kStRecs < ge) st_load_recs(p, gi + kStRecs, ge, sm, (int)((c + 1) & 1));
+            __syncthreads();
+        }
+        const MsdGroup g = sm.recs[li % (2 * kStRecs)];
+        if (g.flags) {
+            have = false;
+            continue;
+        }
+        if (!st_ok(p, g)) {
+            if (threadIdx.x == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            have = false;
+            continue;
+        }
+        if (!have) {
+            uint32_t o0[2], o1[2];
+            st_load_offs(p, g, o0, o1);
+            st_issue(p, g, o0, o1, cur, sm, wsb);
+            __syncthreads();  // the list region is reused by the join
+        }
+        FIN_STAMP(0);
+        bool nfit = false;
+        MsdGroup gn{};
+        uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
+        if (gi + 1 < ge) {
+            gn = sm.recs[(li + 1) % (2 * kStRecs)];
+            nfit = st_ok(p, gn);
+            if (nfit) st_load_offs(p, gn, o0, o1);
+        }
+        FIN_STAMP(1);
+        uint32_t mmask = 0, part[kStIt];
+        const bool ok = st_sort(p, g, gi, cur, sm, wsb, mmask, part);  // cur is staged in LDS here
+        __syncthreads();
+        FIN_STAMP(2);
+        if (nfit) {  // the next group's rows: in flight while this one is written out
+            st_issue(p, gn, o0, o1, cur, sm, wsb);
+            __syncthreads();  // list dead before the join reuses the region
+        }
+        FIN_STAMP(3);
+        if (ok) {
+            st_emit(p, g, gi, sm, wsb, mmask, part);
+        } else {  // hand-over: the histogram still needs zeroing
+            uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+            for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+        }
+        FIN_STAMP(4);
+        have = nfit;
+        __syncthreads();
+        FIN_STAMP(5);
+        if (p.dbg) ph[9]++;
+    }
+    if (p.dbg && threadIdx.x == 0)
+        for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
+}
+
+// groups of the wide list (key range over 22 bits, or a bucket with more than
+// kFinThreads pass-B tiles): the generic 64-bit path, persistent over the list
+template <int C1, int C2>
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const MsdFinalParams p) {
+    __shared__ FinalSmem sm;
+    const uint32_t nw = p.plan->nwide;
+    for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
+        final_group<C1, C2>(p, p.wide_list[i], sm);
+        __syncthreads();
+    }
+}
+
+hipError_t read_msd_phases(unsigned long long *out16) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 16);
+    if (e != hipSuccess) return e;
+    static const unsigned long long zero[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fin_phase), zero, sizeof(zero));
 }
 
 // ---------------------------------------------------------------------------
@@ -1104,16 +2032,28 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tile
 }
 
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(msd_group_kernel, dim3(kBucketsA), dim3(kRadB), 0, s, p);
+    hipLaunchKernelGGL(msd_group_kernel, dim3(kBucketsA), dim3(kGroupThreads), 0, s, p);
     hipLaunchKernelGGL(msd_group_pack_kernel, dim3(kBucketsA), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s) {
-    if (p.tab[0].cols == 2 && (p.ntab == 1 || p.tab[1].cols == 2))
-        hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL((msd_final_kernel<0, 0>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, p);
+hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
+    static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
+    MsdFinalParams p = p_in;
+    p.dbg = dbg;
+    const bool two = p.tab[0].cols == 2 && (p.ntab == 1 || p.tab[1].cols == 2);
+    if (two) {
+        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(kMsdStageGrid), dim3(kStThreads), 0, s, p);
+        MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
+        hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
+        q.radix_list = nullptr;
+        hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+    } else {
+        MsdFinalParams q = p;
+        q.radix_list = nullptr;  // contiguous mode
+        hipLaunchKernelGGL((msd_final_kernel<0, 0>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
+        hipLaunchKernelGGL((msd_final_wide_kernel<0, 0>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+    }
     return hipGetLastError();
 }
 
