@@ -432,6 +432,7 @@ struct MsdScratch {
     MsdTabScratch t[2];
     int64_t *spl = nullptr;
     MsdGroup *groups = nullptr, *slot_groups = nullptr;
+    uint32_t *gpart = nullptr;  // group_sum partials
     uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr,
              *wide_list = nullptr, *radix_list = nullptr;
     MsdPlan *plan = nullptr, *h_plan = nullptr;
@@ -453,6 +454,7 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
         HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
+        HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
         HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * 256));
         HIP_TRY(hipMalloc(&m.counts, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
@@ -475,7 +477,7 @@ void msd_free_all() {
         for (auto &t : m.t)
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
-        for (void *p : {(void *)m.spl, (void *)m.groups, (void *)m.slot_groups, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+        for (void *p : {(void *)m.spl, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
             hipFree(p);
         hipHostFree(m.h_plan);
@@ -574,7 +576,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
         SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
         SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * sizeof(uint16_t)));
-        SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4));
+        SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4 + kMsdSegs * 4 * 16));
         SMJ_TRY(grow(&ts.bk, &ts.c_bk, 256 * sizeof(MsdBucket)));
     }
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
@@ -582,6 +584,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     HIP_TRY(hipMemsetAsync(ms->plan, 0, sizeof(MsdPlan), s));
     auto segL = [&](int x) { return (uint32_t *)ms->t[x].seg; };
     auto segC = [&](int x) { return (uint32_t *)ms->t[x].seg + kMsdSegs * kOffsA; };
+    auto segMM = [&](int x) { return (int64_t *)((uint32_t *)ms->t[x].seg + 2 * kMsdSegs * kOffsA); };
     {
         MsdSampleParams sp{};
         for (int x = 0; x < ntab; x++)
@@ -604,12 +607,13 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     {
         ProfScope ps("msd_runs", 0, s);
         for (int x = 0; x < ntab; x++)
-            HIP_TRY(launch_msd_runs_seg((const uint32_t *)ms->t[x].offsA, tilesA[x], segL(x), segC(x), s));
+            HIP_TRY(launch_msd_runs_seg((const uint32_t *)ms->t[x].offsA, tilesA[x], segL(x), segC(x),
+                                        (const int64_t *)ms->t[x].tmm, segMM(x), s));
         MsdBasesParams bp{};
         for (int x = 0; x < ntab; x++) {
             bp.segL[x] = segL(x);
             bp.segC[x] = segC(x);
-            bp.tmm[x] = (const int64_t *)ms->t[x].tmm;
+            bp.segmm[x] = segMM(x);
             bp.ntiles[x] = tilesA[x];
             bp.tile[x] = T_[x];
             bp.bk[x] = (MsdBucket *)ms->t[x].bk;
@@ -642,6 +646,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             gp.tile[x] = T_[x];
         }
         gp.ntab = ntab;
+        gp.part = ms->gpart;
         gp.slot_groups = ms->slot_groups;
         gp.ngrp = ms->ngrp;
         gp.groups = ms->groups;

@@ -154,8 +154,9 @@ constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
 constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
-constexpr int kSampleMax = 8192;           // sampled keys per table
+constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = 64;               // segments of the run scans
+constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
 
 struct MsdTable {        // an input table as the sampler and part_a see it
@@ -204,7 +205,7 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
 struct MsdBasesParams {
     const uint32_t *segL[2];
     const uint32_t *segC[2];
-    const int64_t *tmm[2];
+    const int64_t *segmm[2];   // [kMsdSegs * 4][2] min / max partials
     int64_t ntiles[2];
     int tile[2];
     int ntab;
@@ -236,6 +237,7 @@ struct MsdGroupParams {
     const MsdBucket *bk[2];
     int tile[2];
     int ntab;
+    uint32_t *part;         // [2][kBucketsA][kGroupSlices][kRadB] partial sub-bucket totals
     MsdGroup *slot_groups;  // [kBucketsA][kRadB]: bucket a's groups at slots a * kRadB + j
     uint32_t *ngrp;         // [kBucketsA] groups per bucket
     MsdGroup *groups;       // dense, key order (msd_group_pack)
@@ -264,8 +266,10 @@ struct MsdFinalParams {
 
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
+// per-bucket run sums and counts per segment; also the selected-key min / max
+// per (segment, wave): segmm[kMsdSegs * 4][2] (256 entries, INT64_MAX / MIN when empty)
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
-                               hipStream_t s);
+                               const int64_t *tmm, int64_t *segmm, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
 hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, const uint32_t *segL,
                                  const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,

@@ -318,12 +318,29 @@ __device__ __forceinline__ void msd_seg_range(int64_t ntiles, int64_t &c0, int64
 // non-empty runs counted per segment
 __global__ __launch_bounds__(256) void msd_runs_seg_kernel(const uint32_t *__restrict__ offs, int64_t ntiles,
                                                            int width, int nb, uint32_t *__restrict__ segL,
-                                                           uint32_t *__restrict__ segC) {
+                                                           uint32_t *__restrict__ segC, const int64_t *__restrict__ tmm,
+                                                           int64_t *__restrict__ segmm) {
     __shared__ uint32_t partL[4][64], partC[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int a = blockIdx.x * 64 + lane;
     int64_t c0, c1;
     msd_seg_range(ntiles, c0, c1);
+    if (blockIdx.x == 0) {  // min / max of the selected keys over this wave's tiles
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        for (int64_t t = c0 + lane; t < c1; t += 64) {
+            mn = min(mn, tmm[2 * t]);
+            mx = max(mx, tmm[2 * t + 1]);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
+            mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
+        }
+        if (lane == 0) {
+            segmm[2 * (blockIdx.y * 4 + w)] = mn;
+            segmm[2 * (blockIdx.y * 4 + w) + 1] = mx;
+        }
+    }
     uint32_t L = 0, C = 0;
     if (a < nb) {
 #pragma unroll 8
@@ -350,11 +367,10 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
     const int a = threadIdx.x, lane = a & 63, wave = a >> 6;
     // global min / max of the selected keys over both tables
     int64_t mn = INT64_MAX, mx = INT64_MIN;
-    for (int x = 0; x < p.ntab; x++)
-        for (int64_t t = a; t < p.ntiles[x]; t += 256) {
-            mn = min(mn, p.tmm[x][2 * t]);
-            mx = max(mx, p.tmm[x][2 * t + 1]);
-        }
+    for (int x = 0; x < p.ntab; x++) {  // per (segment, wave) partials of msd_runs_seg_kernel
+        mn = min(mn, p.segmm[x][2 * a]);
+        mx = max(mx, p.segmm[x][2 * a + 1]);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
@@ -488,15 +504,21 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
 template <int COLS>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPartBParams p) {
     constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kRadB;
-    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4, LISTB = (T + 1) * 8;
+    // run lookup aids after the list: at[r] = entry of the run starting at tile
+    // row r, a bitmap of run starts, btab[b] = entry holding tile row 64 * b
+    constexpr int LISTB = (T + 1) * 8, ATB = T * 2, BMB = T / 8, BTB = T / 64 * 2;
+    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4, LKB = LISTB + ATB + BMB + BTB;
     constexpr int UB0 = ROWB > CNTB ? ROWB : CNTB;
-    constexpr int UB = UB0 > LISTB ? UB0 : LISTB;
+    constexpr int UB = UB0 > LKB ? UB0 : LKB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
     __shared__ uint32_t s_bin[RADIX + 1];
     __shared__ uint32_t s_wsum[kMsdWaves];
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
     uint2 *s_list = reinterpret_cast<uint2 *>(s_u);
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(s_u + LISTB);
+    uint32_t *s_bm = reinterpret_cast<uint32_t *>(s_u + LISTB + ATB);
+    uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + ATB + BMB);
 
     const int64_t g = blockIdx.x;
     if (g >= (int64_t)p.plan->ntilesB[p.x]) return;
@@ -508,20 +530,29 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
     const uint32_t q0 = ti.y;
     const int J = (int)min(b.list_base + b.nruns - q0, (uint32_t)nrows + 1u);
     for (int j = tid; j < J; j += kMsdThreads) s_list[j] = p.list[q0 + j];
+    for (int i = tid; i < T / 32; i += kMsdThreads) s_bm[i] = 0;
+    __syncthreads();
+    for (int j = tid; j < J; j += kMsdThreads) {  // runs are non-empty: starts strictly increase
+        const uint32_t y = s_list[j].y;
+        const uint32_t s0 = y > v0 ? y - v0 : 0u;
+        const uint32_t e = j + 1 < J ? s_list[j + 1].y - v0 : (uint32_t)nrows;
+        if (s0 < (uint32_t)nrows) {
+            s_at[s0] = (uint16_t)j;
+            atomicOr(&s_bm[s0 >> 5], 1u << (s0 & 31));
+            for (uint32_t bb = (s0 + 63) >> 6; (bb << 6) < e && (bb << 6) < (uint32_t)nrows; bb++) s_bt[bb] = (uint16_t)j;
+        }
+    }
     __syncthreads();
 
     const int lrow0 = wave * ITEMS * 64 + lane;
     int64_t rows[ITEMS][COLS];
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
-        const uint32_t v = v0 + (uint32_t)min(lrow0 + it * 64, nrows - 1);
-        int lo = 0, hi = J - 1;  // last run starting at or before v
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_list[mid].y <= v) lo = mid; else hi = mid - 1;
-        }
-        const uint2 e = s_list[lo];
-        load_row<COLS>(p.srcA + (int64_t)(e.x + (v - e.y)) * COLS, rows[it]);
+        const uint32_t r = (uint32_t)min(lrow0 + it * 64, nrows - 1), bb = r >> 6;
+        const uint64_t m = ((uint64_t)s_bm[2 * bb + 1] << 32 | s_bm[2 * bb]) & ((2ull << (r & 63)) - 1ull) & ~1ull;
+        const uint32_t j = m ? s_at[(bb << 6) + 63 - __clzll((long long)m)] : s_bt[bb];
+        const uint2 e = s_list[j];
+        load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
     }
     __syncthreads();  // list dead: the region becomes the counters
     uint32_t *wc = s_wcnt + wave * RADIX;
@@ -568,6 +599,37 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
 // [t*SB, t*SB + SB): per-table sub-bucket totals and prefixes, then greedy
 // packing into groups written to slots a * kRadB + j.  msd_group_pack_kernel
 // then lays them out densely.
+// grid (kBucketsA, kGroupSlices) x 256: partial sub-bucket totals of a slice
+// of the bucket's pass-B tiles (thread t owns sub-buckets [8t, 8t + 8))
+
+__global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams p) {
+    constexpr int SB = kRadB / 256;
+    const int a = blockIdx.x, sl = blockIdx.y, t = threadIdx.x;
+    for (int x = 0; x < p.ntab; x++) {
+        uint32_t tot[SB];
+#pragma unroll
+        for (int i = 0; i < SB; i++) tot[i] = 0;
+        const MsdBucket bk = p.bk[x][a];
+        const uint32_t K = (bk.L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
+        const uint32_t k0 = (uint32_t)(((uint64_t)K * sl) / kGroupSlices), k1 = (uint32_t)(((uint64_t)K * (sl + 1)) / kGroupSlices);
+        const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
+#pragma unroll 4
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint16_t *r = o + (int64_t)k * kOffsB;
+            uint32_t prev = r[0];
+#pragma unroll
+            for (int i = 0; i < SB; i++) {
+                const uint32_t nx = r[i + 1];
+                tot[i] += nx - prev;
+                prev = nx;
+            }
+        }
+        uint32_t *dst = p.part + (((int64_t)x * kBucketsA + a) * kGroupSlices + sl) * kRadB + t * SB;
+#pragma unroll
+        for (int i = 0; i < SB; i++) dst[i] = tot[i];
+    }
+}
+
 constexpr int kGroupThreads = 1024;
 __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroupParams p) {
     constexpr int NW = kGroupThreads / 64, SB = kRadB / kGroupThreads;
@@ -582,20 +644,11 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
 #pragma unroll
         for (int i = 0; i < SB; i++) tot[i] = 0;
         if (x < p.ntab) {
-            const MsdBucket bk = p.bk[x][a];
-            const uint32_t K = (bk.L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
-            const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
-#pragma unroll 2
-            for (uint32_t k = 0; k < K; k++) {
-                const uint16_t *r = o + (int64_t)k * kOffsB;
-                uint32_t prev = r[0];
+            const uint32_t *src = p.part + ((int64_t)x * kBucketsA + a) * kGroupSlices * kRadB + t * SB;
 #pragma unroll
-                for (int i = 0; i < SB; i++) {
-                    const uint32_t nx = r[i + 1];
-                    tot[i] += nx - prev;
-                    prev = nx;
-                }
-            }
+            for (int sl = 0; sl < kGroupSlices; sl++)
+#pragma unroll
+                for (int i = 0; i < SB; i++) tot[i] += src[(int64_t)sl * kRadB + i];
         }
         uint32_t sum = 0;
 #pragma unroll
@@ -614,31 +667,45 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
-    if (t == 0) {  // greedy packing; a group that is over the cap holds exactly one sub-bucket
+    if (t < 64) {  // greedy packing by wave 0 (counts in registers, one lane at a time);
+                   // a group that is over the cap holds exactly one sub-bucket
         int ng = 0, b0 = -1, last = -1;
         uint32_t cr = 0, cs = 0;
-        for (int j = 0; j < kRadB; j++) {
-            const uint32_t r = s_tot[0][j], s = s_tot[1][j];
-            if (r + s == 0) continue;
-            if (b0 >= 0 && (cr + r > (uint32_t)kGroupCap || cs + s > (uint32_t)kGroupCap || j - b0 >= maxspan)) {
-                s_g0[ng] = (uint16_t)b0;
-                s_g1[ng] = (uint16_t)(last + 1);
-                ng++;
-                b0 = -1;
-                cr = cs = 0;
+        for (int c = 0; c < kRadB; c += 64) {
+            const uint32_t rv = s_tot[0][c + t], sv = s_tot[1][c + t];
+            uint64_t nz = __ballot((rv | sv) != 0u);
+            while (nz) {
+                const int l = __ffsll((unsigned long long)nz) - 1;
+                nz &= nz - 1;
+                const int j = c + l;
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rv, l);
+                const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)sv, l);
+                if (b0 >= 0 && (cr + r > (uint32_t)kGroupCap || cs + s > (uint32_t)kGroupCap || j - b0 >= maxspan)) {
+                    if (t == 0) {
+                        s_g0[ng] = (uint16_t)b0;
+                        s_g1[ng] = (uint16_t)(last + 1);
+                    }
+                    ng++;
+                    b0 = -1;
+                    cr = cs = 0;
+                }
+                if (b0 < 0) b0 = j;
+                cr += r;
+                cs += s;
+                last = j;
             }
-            if (b0 < 0) b0 = j;
-            cr += r;
-            cs += s;
-            last = j;
         }
         if (b0 >= 0) {
-            s_g0[ng] = (uint16_t)b0;
-            s_g1[ng] = (uint16_t)(last + 1);
+            if (t == 0) {
+                s_g0[ng] = (uint16_t)b0;
+                s_g1[ng] = (uint16_t)(last + 1);
+            }
             ng++;
         }
-        s_ng = ng;
-        p.ngrp[a] = (uint32_t)ng;
+        if (t == 0) {
+            s_ng = ng;
+            p.ngrp[a] = (uint32_t)ng;
+        }
     }
     __syncthreads();
     for (int j = t; j < s_ng; j += kGroupThreads) {
@@ -2005,9 +2072,10 @@ hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
 }
 
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
-                               hipStream_t s) {
+                               const int64_t *tmm, int64_t *segmm, hipStream_t s) {
     const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
-    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsA, kBucketsA, segL, segC);
+    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsA, kBucketsA, segL, segC, tmm,
+                       segmm);
     return hipGetLastError();
 }
 
@@ -2032,6 +2100,7 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tile
 }
 
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(msd_group_sum_kernel, dim3(kBucketsA, kGroupSlices), dim3(256), 0, s, p);
     hipLaunchKernelGGL(msd_group_kernel, dim3(kBucketsA), dim3(kGroupThreads), 0, s, p);
     hipLaunchKernelGGL(msd_group_pack_kernel, dim3(kBucketsA), dim3(256), 0, s, p);
     return hipGetLastError();
