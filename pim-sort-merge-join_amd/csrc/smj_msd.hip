@@ -1658,13 +1658,21 @@ __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key 
 // stage + counting sort of group g whose rows are in `rows`, then the zip
 // join lookups (mmask / part); false: an equal-key run over kMaxDupRun (the
 // group is handed to the radix list)
+__device__ unsigned long long g_st_sub[8];
+#define ST_SUB(k)                                                   \
+    if (p.dbg && tid == 0) {                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        atomicAdd(&g_st_sub[k], t_ - st_t);                         \
+        st_t = t_;                                                  \
+    }
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt]) {
     const int tid = threadIdx.x;
+    unsigned long long st_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
     uint32_t w[2][kStIt], rank[2][kStIt];
-    if (tid == 0) sm.flag[wsb] = 0;
+    if (tid == 0) sm.flag[wsb] = 0;  // longest equal-key run (0: none)
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -1681,26 +1689,27 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             }
         }
     __syncthreads();
+    ST_SUB(0);
     constexpr int W = kStRange / 2 / kStThreads;  // histogram words per thread
-    uint32_t tot = 0, heavy = 0, dup = 0;
+    uint32_t tot = 0, mrun = 0;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         uint32_t t = 0;
 #pragma unroll
         for (int i = 0; i < W; i++) {
             const uint32_t h = sm.hist[x][tid * W + i], lo = h & 0xffffu, hi = h >> 16;
-            heavy |= (lo > (uint32_t)kMaxDupRun) | (hi > (uint32_t)kMaxDupRun);
-            dup |= (lo > 1u) | (hi > 1u);
+            mrun = max(mrun, max(lo, hi));
             t += lo + hi;
         }
         tot |= t << (16 * x);
     }
-    if (heavy | dup) atomicOr(&sm.flag[wsb], heavy ? 3u : 1u);
+    if (mrun > 1u) atomicMax(&sm.flag[wsb], mrun);  // longest equal-key run
     uint32_t all;
     const uint32_t ex = block_excl_scan_nb<kStWaves>(tot, sm.wsum[wsb], &all);  // publishes flag[wsb]
     const uint32_t fl = sm.flag[wsb];
     wsb ^= 1;
-    if (fl & 2u) {
+    ST_SUB(1);
+    if (fl > (uint32_t)kMaxDupRun) {
         if (tid == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
         return false;
     }
@@ -1724,31 +1733,25 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
                 sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + rank[x][k]] = w[x][k];
             }
     __syncthreads();
-    if (fl & 1u) {  // equal residuals were placed in atomic order: re-order each run by row
+    ST_SUB(2);
+    // equal residuals were placed in atomic order: odd-even transposition
+    // rounds (as many as the longest run) order every run by group row
+    static_assert(kGroupCap / 2 == kStThreads, "one compare-exchange per thread per table and round");
+    for (uint32_t rd = 0; rd < fl; rd++) {
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < kStIt; k++) {
-                const int q = tid * kStIt + k;
-                if (q + 1 < n[x]) {
-                    const uint32_t rq = sm.key[x][q] >> kFinIdxBits;
-                    if ((sm.key[x][q + 1] >> kFinIdxBits) == rq && (q == 0 || (sm.key[x][q - 1] >> kFinIdxBits) != rq)) {
-                        int e = q + 1;
-                        while (e < n[x] && (sm.key[x][e] >> kFinIdxBits) == rq) e++;
-                        for (int a = q + 1; a < e; a++) {
-                            const uint32_t v = sm.key[x][a];
-                            int b = a - 1;
-                            while (b >= q && sm.key[x][b] > v) {
-                                sm.key[x][b + 1] = sm.key[x][b];
-                                b--;
-                            }
-                            sm.key[x][b + 1] = v;
-                        }
-                    }
+        for (int x = 0; x < 2; x++) {
+            const int q = 2 * tid + (int)(rd & 1u);
+            if (q + 1 < n[x]) {
+                const uint32_t a = sm.key[x][q], b = sm.key[x][q + 1];
+                if ((a >> kFinIdxBits) == (b >> kFinIdxBits) && a > b) {
+                    sm.key[x][q] = b;
+                    sm.key[x][q + 1] = a;
                 }
             }
+        }
         __syncthreads();
     }
+    ST_SUB(3);
     // zip join from the histogram starts: R position i with residual r pairs
     // with S position startS(r) + (i - startR(r)) while i - startR(r) < countS(r)
     mmask = 0;
@@ -1923,8 +1926,12 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const Ms
 }
 
 hipError_t read_msd_phases(unsigned long long *out16) {
-    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 16);
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 10);
     if (e != hipSuccess) return e;
+    e = hipMemcpyFromSymbol(out16 + 10, HIP_SYMBOL(g_st_sub), sizeof(unsigned long long) * 4);
+    if (e != hipSuccess) return e;
+    static const unsigned long long zero8[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_st_sub), zero8, sizeof(zero8));
     static const unsigned long long zero[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_fin_phase), zero, sizeof(zero));
 }

@@ -38,3 +38,6 @@ for k in range(9):
     if names[k]:
         print(f"  {names[k]:18s} {buf[k] / max(groups, 1):10.0f}  {100 * buf[k] / max(tot, 1):5.1f}%")
 print(f"  total              {tot / max(groups, 1):10.0f}")
+sub = ["sort: stage+hist", "sort: scan", "sort: scatter", "sort: dup fix-up"]
+for k in range(4):
+    print(f"    {sub[k]:18s} {buf[10 + k] / max(groups, 1):10.0f}")
