@@ -110,10 +110,12 @@ extern "C" int smj_debug_phase_cycles(unsigned long long *out16) {
 }
 
 // Diagnostic only (not part of smj.h): msd_final phase cycles collected under
-// SMJ_DEBUG_MSD=1; out[k] cycles of phase k summed over workgroups, out[9] groups.
-extern "C" int smj_debug_msd_phases(unsigned long long *out16) {
+// SMJ_DEBUG_MSD=1 (24 words): out[k] cycles of staged-final phase k summed
+// over workgroups, out[9] groups, out[10..13] its sort sub-phases,
+// out[16..21] part_b phases, out[23] part_b tiles.
+extern "C" int smj_debug_msd_phases(unsigned long long *out24) {
     hipDeviceSynchronize();
-    return read_msd_phases(out16) == hipSuccess ? SMJ_OK : SMJ_ERR_HIP;
+    return read_msd_phases(out24) == hipSuccess ? SMJ_OK : SMJ_ERR_HIP;
 }
 
 static std::string prof_json() {

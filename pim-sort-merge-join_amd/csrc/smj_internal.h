@@ -222,6 +222,7 @@ struct MsdPartBParams {
     const MsdPlan *plan;
     uint16_t *offs;      // [tilesB][kOffsB] tile-local sub-bucket starts
     int key_col, x;
+    int dbg;             // SMJ_DEBUG_MSD: phase stamps (tools/msd_phases.py)
 };
 struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
     uint16_t a, flags, b0, b1;

@@ -501,6 +501,16 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
 // part_b: gather a pass-B tile through the run list, stable tile-local
 // partition by the 9-bit sub-bucket
 // ---------------------------------------------------------------------------
+// Diagnostic phase stamps of part_b (SMJ_DEBUG_MSD=1; off in production):
+// [k] cycles of phase k summed over tiles (thread 0's view), [7] tiles
+__device__ unsigned long long g_pb_phase[8];
+#define PB_STAMP(k)                                                 \
+    if (p.dbg && tid == 0) {                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        atomicAdd(&g_pb_phase[k], t_ - pb_t);                       \
+        pb_t = t_;                                                  \
+    }
+
 template <int COLS>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPartBParams p) {
     constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kRadB;
@@ -523,6 +533,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
     const int64_t g = blockIdx.x;
     if (g >= (int64_t)p.plan->ntilesB[p.x]) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long pb_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
     const uint2 ti = p.tinfo[g];
     const MsdBucket b = p.bk[ti.x];
     const uint32_t v0 = (uint32_t)(g - b.tile_base) * (uint32_t)T;
@@ -543,6 +554,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         }
     }
     __syncthreads();
+    PB_STAMP(0);
 
     const int lrow0 = wave * ITEMS * 64 + lane;
     int64_t rows[ITEMS][COLS];
@@ -555,6 +567,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
     }
     __syncthreads();  // list dead: the region becomes the counters
+    PB_STAMP(1);
     uint32_t *wc = s_wcnt + wave * RADIX;
     zero_counters<RADIX>(wc, lane);
 
@@ -570,6 +583,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
     }
     wave_rank<ITEMS, kBitsB>(dig, vmask, wc, lane);
     __syncthreads();
+    PB_STAMP(2);
     tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
@@ -577,11 +591,13 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         dig[it] = s_bin[d] + wc[d] + (dig[it] >> 16);
     }
     __syncthreads();  // counters dead: the region becomes the staging tile
+    PB_STAMP(3);
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
     for (int d = tid; d <= RADIX; d += kMsdThreads) p.offs[g * kOffsB + d] = (uint16_t)s_bin[d];  // [RADIX] = nrows
     __syncthreads();
+    PB_STAMP(4);
     int64_t *dst = p.out + g * T * COLS;
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
@@ -590,6 +606,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         load_row<COLS>(s_rows + (size_t)s * COLS, r);
         store_row<COLS>(dst + (size_t)s * COLS, r);
     }
+    PB_STAMP(5);
+    if (p.dbg && tid == 0) atomicAdd(&g_pb_phase[7], 1ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -1735,7 +1753,8 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     __syncthreads();
     ST_SUB(2);
     // equal residuals were placed in atomic order: odd-even transposition
-    // rounds (as many as the longest run) order every run by group row
+    // rounds (as many as the longest run) order every run by group row.
+    // (Measured: cheaper than ranking each run member by a scan of its run.)
     static_assert(kGroupCap / 2 == kStThreads, "one compare-exchange per thread per table and round");
     for (uint32_t rd = 0; rd < fl; rd++) {
 #pragma unroll
@@ -1828,38 +1847,52 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     }
 }
 
-// copy group records [r0, r0 + kStRecs) of the range into ring half h
-__device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t r0, int64_t ge, StSmem &sm, int h) {
+// copy the records of this workgroup's local groups [t0, t0 + kStRecs) into
+// ring half h (local group t is dense group g0 + t * gs)
+__device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0, int64_t gs, int64_t t0,
+                                             int64_t cnt, StSmem &sm, int h) {
     constexpr int WORDS = sizeof(MsdGroup) / 8;
-    const int64_t *src = reinterpret_cast<const int64_t *>(p.groups + r0);
     int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
-    const int64_t nw = min((int64_t)kStRecs, ge - r0) * WORDS;
-    for (int64_t i = threadIdx.x; i < nw; i += kStThreads) dst[i] = src[i];
+    const int64_t nw = min((int64_t)kStRecs, cnt - t0) * WORDS;
+    for (int64_t i = threadIdx.x; i < nw; i += kStThreads) {
+        const int64_t t = t0 + i / WORDS;
+        dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
+    }
 }
 
-// persistent staged kernel over contiguous ranges of dense groups
+// persistent staged kernel.  XCD-aware schedule: the dense (key-ordered)
+// groups are cut into kXcdSlots contiguous ranges, one per set of blocks
+// sharing an XCD (blocks b, b + 8, ... -- MI355X_MICROARCH.md, workgroup
+// dispatch), and the set's blocks interleave over their range (block j of the
+// set takes groups j, j + gs, ...).  Groups in flight on one XCD are then
+// neighbours in key order: the pass-B tile lines and offsB lines two
+// neighbouring groups share are fetched into that XCD's L2 once.
+constexpr int kXcdSlots = 8;
 __global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     const int64_t ng = p.plan->ngroups;
-    const int64_t per = (ng + gridDim.x - 1) / gridDim.x;
-    const int64_t gb = (int64_t)blockIdx.x * per, ge = min(ng, gb + per);
+    const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
+    const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
+    const int64_t x0 = (int64_t)(blockIdx.x % kXcdSlots) * xr, x1 = min(ng, x0 + xr);
+    const int64_t g0 = x0 + blockIdx.x / kXcdSlots;  // local group t = dense group g0 + t * gs
+    const int64_t cnt = x1 > g0 ? (x1 - g0 + gs - 1) / gs : 0;
     unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
         for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
     }
-    if (gb < ge) st_load_recs(p, gb, ge, sm, 0);
-    if (gb + kStRecs < ge) st_load_recs(p, gb + kStRecs, ge, sm, 1);
+    if (0 < cnt) st_load_recs(p, g0, gs, 0, cnt, sm, 0);
+    if (kStRecs < cnt) st_load_recs(p, g0, gs, kStRecs, cnt, sm, 1);
     __syncthreads();
     i64x2 cur[2][kStIt];
     int wsb = 0;
     bool have = false;  // cur holds the rows of group gi
-    for (int64_t gi = gb; gi < ge; gi++) {
-        const int64_t li = gi - gb;
+    for (int64_t li = 0; li < cnt; li++) {
+        const int64_t gi = g0 + li * gs;
         if (li >= kStRecs && li % kStRecs == 0) {  // entering chunk c: fetch chunk c + 1 into the other half
             const int64_t c = li / kStRecs;
             __syncthreads();
-            if (gi + kStRecs < ge) st_load_recs(p, gi + kStRecs, ge, sm, (int)((c + 1) & 1));
+            if (li + kStRecs < cnt) st_load_recs(p, g0, gs, li + kStRecs, cnt, sm, (int)((c + 1) & 1));
             __syncthreads();
         }
         const MsdGroup g = sm.recs[li % (2 * kStRecs)];
@@ -1882,7 +1915,7 @@ __global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const Ms
         bool nfit = false;
         MsdGroup gn{};
         uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
-        if (gi + 1 < ge) {
+        if (li + 1 < cnt) {
             gn = sm.recs[(li + 1) % (2 * kStRecs)];
             nfit = st_ok(p, gn);
             if (nfit) st_load_offs(p, gn, o0, o1);
@@ -1925,11 +1958,15 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const Ms
     }
 }
 
+static const unsigned long long zero8_pb[8] = {0};
 hipError_t read_msd_phases(unsigned long long *out16) {
     hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 10);
     if (e != hipSuccess) return e;
     e = hipMemcpyFromSymbol(out16 + 10, HIP_SYMBOL(g_st_sub), sizeof(unsigned long long) * 4);
     if (e != hipSuccess) return e;
+    e = hipMemcpyFromSymbol(out16 + 16, HIP_SYMBOL(g_pb_phase), sizeof(unsigned long long) * 8);
+    if (e != hipSuccess) return e;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_pb_phase), zero8_pb, sizeof(zero8_pb));
     static const unsigned long long zero8[8] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_st_sub), zero8, sizeof(zero8));
     static const unsigned long long zero[16] = {0};
@@ -2099,8 +2136,11 @@ hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, co
     return hipGetLastError();
 }
 
-hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s) {
+hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_tiles, hipStream_t s) {
     if (max_tiles <= 0) return hipSuccess;
+    static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
+    MsdPartBParams p = p_in;
+    p.dbg = dbg;
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3((unsigned)max_tiles), dim3(kMsdThreads),
                                              0, s, p));
     return hipGetLastError();
@@ -2119,6 +2159,7 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     p.dbg = dbg;
     const bool two = p.tab[0].cols == 2 && (p.ntab == 1 || p.tab[1].cols == 2);
     if (two) {
+        static_assert(kMsdStageGrid % kXcdSlots == 0, "whole XCD sets");
         hipLaunchKernelGGL(msd_final_stage_kernel, dim3(kMsdStageGrid), dim3(kStThreads), 0, s, p);
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);

@@ -13,8 +13,9 @@ contiguous slice of R and of S (rank order = input order) and:
      bucket as the digit), an all_to_all of the W bucket counts and one
      all_to_all_single of the rows -- received chunks land in SOURCE-RANK
      order, so equal keys keep their global input order;
-  3. local stable select+sort (radix keyed relative to the rank's lower key
-     bound, which usually saves a pass) and the local zip join.
+  3. the fused local pipeline (smj_dev_sort_merge_join: MSD sample sort of
+     the received R and S slices + zip join) with no select -- the partition
+     step already applied the WHERE clause.
 
 Concatenating the per-rank outputs in rank order is exactly cpu_app.c's
 result (stable sort + zip join are per-key operations on disjoint key ranges).
@@ -26,14 +27,12 @@ import torch.distributed as dist
 
 from . import ops as hip_ops
 
-INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
 
 
 class HipOps:
     """The product operators: HIP kernels behind libsmj_hip.so."""
-    select_sort = staticmethod(hip_ops.select_sort)
-    join = staticmethod(hip_ops.join)
+    sort_merge_join = staticmethod(hip_ops.sort_merge_join)
     partition_count = staticmethod(hip_ops.partition_count)
     partition_scatter = staticmethod(hip_ops.partition_scatter)
 
@@ -46,10 +45,21 @@ def _sample_keys(table, key_col, samples):
     return table[idx, key_col].contiguous()
 
 
+def _wire_device(t, group=None):
+    """Where collective buffers live: the tensor's own device under RCCL; the
+    host under gloo (which moves CPU tensors only) -- used by the CPU tests and
+    by the 2-rank-on-one-GPU test, never by the RCCL product path."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return t.device
+
+
 def choose_splitters(tables_and_keys, world, group=None, samples=4096):
     """W-1 sorted key splitters, identical on every rank (one all_gather)."""
     local = torch.cat([_sample_keys(t, k, samples) for t, k in tables_and_keys])
-    dev = local.device
+    home = local.device
+    dev = _wire_device(local, group)
+    local = local.to(dev)
     # fixed-size exchange: pad with INT64_MAX and a count
     cnt = torch.tensor([local.numel()], dtype=torch.int64, device=dev)
     cap = len(tables_and_keys) * samples
@@ -61,17 +71,19 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096):
     dist.all_gather(all_buf, buf, group=group)
     keys = torch.cat([b[: int(c.item())] for b, c in zip(all_buf, all_cnt)])
     if keys.numel() == 0:
-        return torch.zeros(world - 1, dtype=torch.int64, device=dev)
+        return torch.zeros(world - 1, dtype=torch.int64, device=home)
     keys = torch.sort(keys).values
     L = keys.numel()
     pos = torch.tensor([max((i + 1) * L // world - 1, 0) for i in range(world - 1)], device=dev)
-    return keys[pos].contiguous()
+    return keys[pos].contiguous().to(home)
 
 
 def exchange_rows(send, counts, group=None):
     """all_to_all_single of bucket-contiguous rows; returns rows received in
     source-rank order."""
-    dev = send.device
+    home = send.device
+    dev = _wire_device(send, group)
+    send = send.to(dev)
     world = len(counts)
     send_counts = torch.tensor(counts, dtype=torch.int64, device=dev)
     recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
@@ -80,7 +92,7 @@ def exchange_rows(send, counts, group=None):
     recv = torch.empty((sum(rc), send.shape[1]), dtype=send.dtype, device=dev)
     dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rc, input_split_sizes=list(counts),
                            group=group)
-    return recv
+    return recv.to(home)
 
 
 def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, ops=None, samples=4096,
@@ -93,26 +105,13 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if world == 1:
-        Rs = ops.select_sort(R, k1, sc1, sv1)
-        Ss = ops.select_sort(S, k2, sc2, sv2)
-        return ops.join(Rs, Ss, k1, k2)
+        return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
 
     spl = choose_splitters([(R, k1), (S, k2)], world, group, samples)
     local = []
     for T, key, sc, sv in ((R, k1, sc1, sv1), (S, k2, sc2, sv2)):
-        counts, (mn, _mx) = ops.partition_count(T, spl, key, sc, sv)
+        counts, _ = ops.partition_count(T, spl, key, sc, sv)
         send = ops.partition_scatter(T, spl, counts, key, sc, sv)
-        recv = exchange_rows(send, counts, group)
+        local.append(exchange_rows(send, counts, group))
         del send
-        local.append((recv, key, mn))
-    # lower key bound of this rank's range -> radix base (fewer passes):
-    # the global minimum on rank 0, splitter + 1 elsewhere
-    mins = torch.tensor([local[0][2], local[1][2]], dtype=torch.int64, device=R.device)
-    dist.all_reduce(mins, op=dist.ReduceOp.MIN, group=group)
-    base_keys = []
-    for t in range(2):
-        lo = int(mins[t].item()) if rank == 0 else int(spl[rank - 1].item()) + 1
-        base_keys.append(lo if lo <= INT64_MAX else INT64_MIN)
-    Rs = ops.select_sort(local[0][0], k1, 0, None, key_base=hip_ops.biased(base_keys[0]))
-    Ss = ops.select_sort(local[1][0], k2, 0, None, key_base=hip_ops.biased(base_keys[1]))
-    return ops.join(Rs, Ss, k1, k2)
+    return ops.sort_merge_join(local[0], local[1], k1, k2, None, None)[2]

@@ -35,6 +35,12 @@ class OracleOps:
         return torch.from_numpy(oracle.join(R.numpy(), S.numpy(), key1, key2).reshape(-1, R.shape[1] + S.shape[1] - 1))
 
     @staticmethod
+    def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None):
+        Rs = OracleOps.select_sort(R, key1, *(select1 or (0, None)))
+        Ss = OracleOps.select_sort(S, key2, *(select2 or (0, None)))
+        return Rs, Ss, OracleOps.join(Rs, Ss, key1, key2)
+
+    @staticmethod
     def _keep(T, key, sc, sv, spl):
         t = T.numpy()
         keep = t if sv is None else t[t[:, sc] > sv]
@@ -76,8 +82,12 @@ def _worker(rank, world, port, R, S, cfg, outdir):
     cuts_s = cuts_s.astype(int)
     r = torch.from_numpy(R[cuts_r[rank]:cuts_r[rank + 1]].copy())
     s = torch.from_numpy(S[cuts_s[rank]:cuts_s[rank + 1]].copy())
-    out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=Ops, samples=cfg["samples"])
-    np.save(os.path.join(outdir, f"rank{rank}.npy"), out.numpy())
+    ops = Ops
+    if cfg.get("gpu"):  # the product operators (HipOps) on cuda:0, exchange staged through gloo
+        torch.cuda.set_device(0)
+        r, s, ops = r.cuda(), s.cuda(), None
+    out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=ops, samples=cfg["samples"])
+    np.save(os.path.join(outdir, f"rank{rank}.npy"), out.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -108,7 +118,24 @@ def make_tables(kind, n):
     (3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8}),
 ])
 def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
-    R, S = make_tables(kind, 30_000)
+    _run_and_check(tmp_path, world, kind, cfg, 30_000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,cfg", [
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
+    ("dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 256, "gpu": True}),
+    ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True}),
+])
+def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
+    """The product path of smj/dist.py -- HIP partition_count/scatter and the
+    fused local smj_dev_sort_merge_join -- with 2 ranks sharing cuda:0 and the
+    all_to_all staged through gloo (RCCL needs one GPU per rank)."""
+    _run_and_check(tmp_path, 2, kind, cfg, 400_000)
+
+
+def _run_and_check(tmp_path, world, kind, cfg, n):
+    R, S = make_tables(kind, n)
     mp.spawn(_worker, args=(world, free_port(), R, S, cfg, str(tmp_path)), nprocs=world, join=True)
     got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
     sc1, sv1, sc2, sv2 = cfg["select"]

@@ -24,7 +24,11 @@ for s in $STEPS; do
     build) run build 600 make -s -j16 -C pim-sort-merge-join_amd ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    msd)   run msd 600 python -u -m pytest tests/test_gpu_msd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
+    dist)  run dist 600 python -u -m pytest tests/test_dist_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    quick) run quick 300 python bench.py --cpu-sample 0 ;;
+    phases) run phases 300 python tools/msd_phases.py ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0

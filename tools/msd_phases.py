@@ -20,7 +20,7 @@ S = ops.gen_uniform(n, seed=2, key_range=3 * n)
 bufs = [torch.empty_like(R), torch.empty_like(S), torch.empty((n, 3), dtype=torch.int64, device=R.device)]
 ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000), *bufs)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 24)()
 lib.smj_debug_msd_phases(buf)  # reset
 reps = 3
 t0 = time.perf_counter()
@@ -41,3 +41,10 @@ print(f"  total              {tot / max(groups, 1):10.0f}")
 sub = ["sort: stage+hist", "sort: scan", "sort: scatter", "sort: dup fix-up"]
 for k in range(4):
     print(f"    {sub[k]:18s} {buf[10 + k] / max(groups, 1):10.0f}")
+tiles = buf[23]
+pb = ["list + lookups", "row loads issued", "rank (loads land)", "digit starts", "stage + offs", "stores issued"]
+print(f"part_b tiles {tiles}; cycles/tile (thread0 view):")
+tot = sum(buf[16 + k] for k in range(6))
+for k in range(6):
+    print(f"  {pb[k]:18s} {buf[16 + k] / max(tiles, 1):10.0f}  {100 * buf[16 + k] / max(tot, 1):5.1f}%")
+print(f"  total              {tot / max(tiles, 1):10.0f}")
