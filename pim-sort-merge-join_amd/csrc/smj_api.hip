@@ -111,7 +111,7 @@ extern "C" int smj_debug_phase_cycles(unsigned long long *out16) {
 
 // Diagnostic only (not part of smj.h): msd_final phase cycles collected under
 // SMJ_DEBUG_MSD=1 (24 words): out[k] cycles of staged-final phase k summed
-// over workgroups, out[9] groups, out[10..13] its sort sub-phases,
+// over workgroups, out[9] groups, out[10..15] its sort / issue sub-phases,
 // out[16..21] part_b phases, out[23] part_b tiles.
 extern "C" int smj_debug_msd_phases(unsigned long long *out24) {
     hipDeviceSynchronize();
@@ -446,6 +446,13 @@ struct MsdScratch {
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
+struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
+    MsdPartBParams p;
+    int cols;
+    int64_t maxB;
+};
+PbLast g_pb_last[2];
+int g_pb_ntab = 0;
 
 int msd_scratch(MsdScratch **out) {
     int dev = 0;
@@ -638,6 +645,8 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             ProfScope ps("msd_part_b", 0, s);
             HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s));
         }
+        g_pb_last[x] = PbLast{p, in[x].cols, maxB[x]};
+        g_pb_ntab = ntab;
         pb[x] = prof_last();
     }
     {
@@ -730,6 +739,30 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
     return SMJ_OK;
 }
 }  // namespace
+
+// Diagnostic only (not part of smj.h): re-run the last pipeline call's part_b
+// launches `reps` times with ablation bits `dbg` (smj_msd.hip, part_b) and
+// return the average ms per round over both tables.  Overwrites tempB / offsB.
+extern "C" int smj_debug_part_b_time(int dbg, int reps, float *ms) {
+    if (g_pb_ntab == 0 || reps <= 0 || !ms) return SMJ_ERR_INVALID;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventRecord(a, 0));
+    for (int r = 0; r < reps; r++)
+        for (int x = 0; x < g_pb_ntab; x++) {
+            MsdPartBParams p = g_pb_last[x].p;
+            p.dbg = dbg;
+            HIP_TRY(launch_msd_part_b(p, g_pb_last[x].cols, g_pb_last[x].maxB, 0));
+        }
+    HIP_TRY(hipEventRecord(b, 0));
+    HIP_TRY(hipEventSynchronize(b));
+    HIP_TRY(hipEventElapsedTime(ms, a, b));
+    *ms /= (float)reps;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return SMJ_OK;
+}
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {
     for (int i = 0; i < 4; i++) out4[i] = g_msd_stats[i];

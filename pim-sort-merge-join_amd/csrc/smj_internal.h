@@ -154,6 +154,7 @@ constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
 constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
+constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = 64;               // segments of the run scans
 constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel

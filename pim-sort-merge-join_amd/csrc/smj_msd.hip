@@ -501,11 +501,38 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
 // part_b: gather a pass-B tile through the run list, stable tile-local
 // partition by the 9-bit sub-bucket
 // ---------------------------------------------------------------------------
+// wave-uniform copies (SGPRs) of per-tile metadata loaded through vector loads
+// (kernel arguments may alias the outputs, so hipcc cannot use scalar loads)
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
+}
+__device__ __forceinline__ uint2 uni_tinfo(const uint2 *t, int64_t g) {
+    const uint2 v = t[g];
+    return make_uint2(uni32(v.x), uni32(v.y));
+}
+__device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a) {
+    const MsdBucket v = bk[a];
+    MsdBucket r;
+    r.lo = (int64_t)uni64((uint64_t)v.lo);
+    r.scale = uni64(v.scale);
+    r.maxspan = uni32(v.maxspan);
+    r.L = uni32(v.L);
+    r.row_start = uni32(v.row_start);
+    r.list_base = uni32(v.list_base);
+    r.nruns = uni32(v.nruns);
+    r.tile_base = uni32(v.tile_base);
+    return r;
+}
+
 // Diagnostic phase stamps of part_b (SMJ_DEBUG_MSD=1; off in production):
-// [k] cycles of phase k summed over tiles (thread 0's view), [7] tiles
+// [k] cycles of phase k summed over tiles (thread 0's view), [7] tiles.
+// Ablation bits for smj_debug_part_b_time (timing only, output invalid):
+// 2 = no row stores, 4 = synthetic rows instead of the gathers, 8 = no offsB stores,
+// 16 = no ballot ranking (ranks wrong), 32 = no run-list lookups (with 4)
 __device__ unsigned long long g_pb_phase[8];
 #define PB_STAMP(k)                                                 \
-    if (p.dbg && tid == 0) {                                        \
+    if ((p.dbg & 1) && tid == 0) {                                        \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
         atomicAdd(&g_pb_phase[k], t_ - pb_t);                       \
         pb_t = t_;                                                  \
@@ -530,84 +557,126 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
     uint32_t *s_bm = reinterpret_cast<uint32_t *>(s_u + LISTB + ATB);
     uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + ATB + BMB);
 
-    const int64_t g = blockIdx.x;
-    if (g >= (int64_t)p.plan->ntilesB[p.x]) return;
+    // persistent over tiles g = blockIdx.x + k * gridDim.x.  The next tile's
+    // metadata chain (tinfo -> bucket -> first run-list entries) is issued
+    // while this tile is ranked, staged and stored, so a tile starts with
+    // its run list already in registers.
+    const int64_t ntl = (int64_t)p.plan->ntilesB[p.x];
+    int64_t g = blockIdx.x;
+    if (g >= ntl) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     unsigned long long pb_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
-    const uint2 ti = p.tinfo[g];
-    const MsdBucket b = p.bk[ti.x];
-    const uint32_t v0 = (uint32_t)(g - b.tile_base) * (uint32_t)T;
-    const int nrows = (int)min((uint32_t)T, b.L - v0);
-    const uint32_t q0 = ti.y;
-    const int J = (int)min(b.list_base + b.nruns - q0, (uint32_t)nrows + 1u);
-    for (int j = tid; j < J; j += kMsdThreads) s_list[j] = p.list[q0 + j];
-    for (int i = tid; i < T / 32; i += kMsdThreads) s_bm[i] = 0;
-    __syncthreads();
-    for (int j = tid; j < J; j += kMsdThreads) {  // runs are non-empty: starts strictly increase
-        const uint32_t y = s_list[j].y;
-        const uint32_t s0 = y > v0 ? y - v0 : 0u;
-        const uint32_t e = j + 1 < J ? s_list[j + 1].y - v0 : (uint32_t)nrows;
-        if (s0 < (uint32_t)nrows) {
-            s_at[s0] = (uint16_t)j;
-            atomicOr(&s_bm[s0 >> 5], 1u << (s0 & 31));
-            for (uint32_t bb = (s0 + 63) >> 6; (bb << 6) < e && (bb << 6) < (uint32_t)nrows; bb++) s_bt[bb] = (uint16_t)j;
+    uint2 ti = uni_tinfo(p.tinfo, g);
+    MsdBucket b = uni_bucket(p.bk, ti.x);
+    auto runs_of = [&](const uint2 &t, const MsdBucket &bb, int64_t gg) {  // run-list entries of tile gg
+        const uint32_t vv = (uint32_t)(gg - bb.tile_base) * (uint32_t)T;
+        const uint32_t nr = min((uint32_t)T, bb.L - vv);
+        return min(bb.list_base + bb.nruns - t.y, nr + 1u);
+    };
+    const uint64_t *list64 = reinterpret_cast<const uint64_t *>(p.list);
+    uint64_t le = 0;  // run-list entry tid of the current tile ({x, y} as one word)
+    if ((uint32_t)tid < runs_of(ti, b, g)) le = list64[ti.y + tid];
+    // wait for le HERE on the prologue path: otherwise the loop-top use merges
+    // this path (nothing issued after the load) with the back edge and hipcc
+    // waits vmcnt(0) every tile, draining the previous tile's 64 KiB of stores
+    asm volatile("" ::"v"(le));
+    for (; g < ntl; g += gridDim.x) {
+        const uint32_t v0 = (uint32_t)(g - b.tile_base) * (uint32_t)T;
+        const int nrows = (int)min((uint32_t)T, b.L - v0);
+        const uint32_t q0 = ti.y;
+        const int J = (int)runs_of(ti, b, g);
+        if (p.dbg & 32) goto lookups_done;
+        if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
+        for (int j = tid + kMsdThreads; j < J; j += kMsdThreads)  // > kMsdThreads runs: rare
+            reinterpret_cast<uint64_t *>(s_list)[j] = list64[q0 + j];
+        for (int i = tid; i < T / 32; i += kMsdThreads) s_bm[i] = 0;
+        __syncthreads();
+        for (int j = tid; j < J; j += kMsdThreads) {  // runs are non-empty: starts strictly increase
+            const uint32_t y = s_list[j].y;
+            const uint32_t s0 = y > v0 ? y - v0 : 0u;
+            const uint32_t e = j + 1 < J ? s_list[j + 1].y - v0 : (uint32_t)nrows;
+            if (s0 < (uint32_t)nrows) {
+                s_at[s0] = (uint16_t)j;
+                atomicOr(&s_bm[s0 >> 5], 1u << (s0 & 31));
+                for (uint32_t bb = (s0 + 63) >> 6; (bb << 6) < e && (bb << 6) < (uint32_t)nrows; bb++)
+                    s_bt[bb] = (uint16_t)j;
+            }
         }
-    }
-    __syncthreads();
-    PB_STAMP(0);
+        __syncthreads();
+    lookups_done:
+        PB_STAMP(0);
 
-    const int lrow0 = wave * ITEMS * 64 + lane;
-    int64_t rows[ITEMS][COLS];
+        const int lrow0 = wave * ITEMS * 64 + lane;
+        int64_t rows[ITEMS][COLS];
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const uint32_t r = (uint32_t)min(lrow0 + it * 64, nrows - 1), bb = r >> 6;
-        const uint64_t m = ((uint64_t)s_bm[2 * bb + 1] << 32 | s_bm[2 * bb]) & ((2ull << (r & 63)) - 1ull) & ~1ull;
-        const uint32_t j = m ? s_at[(bb << 6) + 63 - __clzll((long long)m)] : s_bt[bb];
-        const uint2 e = s_list[j];
-        load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
-    }
-    __syncthreads();  // list dead: the region becomes the counters
-    PB_STAMP(1);
-    uint32_t *wc = s_wcnt + wave * RADIX;
-    zero_counters<RADIX>(wc, lane);
+        for (int it = 0; it < ITEMS; it++) {
+            const uint32_t r = (uint32_t)min(lrow0 + it * 64, nrows - 1), bb = r >> 6;
+            const uint64_t m = ((uint64_t)s_bm[2 * bb + 1] << 32 | s_bm[2 * bb]) & ((2ull << (r & 63)) - 1ull) & ~1ull;
+            const uint32_t j = m ? s_at[(bb << 6) + 63 - __clzll((long long)m)] : s_bt[bb];
+            const uint2 e = s_list[j];
+            if (p.dbg & 4) {
+#pragma unroll
+                for (int c = 0; c < COLS; c++) rows[it][c] = b.lo + (int64_t)((v0 + r) * 7u % (b.L + 1u));
+            } else {
+                load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
+            }
+        }
+        const int64_t gn = g + gridDim.x;
+        const uint2 tin = uni_tinfo(p.tinfo, min(gn, ntl - 1));  // prefetch 1: next tile's info
+        __syncthreads();  // list dead: the region becomes the counters
+        PB_STAMP(1);
+        uint32_t *wc = s_wcnt + wave * RADIX;
+        zero_counters<RADIX>(wc, lane);
 
-    uint32_t dig[ITEMS];
-    uint32_t vmask = 0;
+        uint32_t dig[ITEMS];
+        uint32_t vmask = 0;
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const bool v = lrow0 + it * 64 < nrows;
-        const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
-        const uint32_t d = b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1)) : (uint32_t)r;
-        dig[it] = v ? d & (RADIX - 1) : 0u;
-        vmask |= v ? (1u << it) : 0u;
+        for (int it = 0; it < ITEMS; it++) {
+            const bool v = lrow0 + it * 64 < nrows;
+            const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
+            const uint32_t d = b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1)) : (uint32_t)r;
+            dig[it] = v ? d & (RADIX - 1) : 0u;
+            vmask |= v ? (1u << it) : 0u;
+        }
+        if (!(p.dbg & 16)) wave_rank<ITEMS, kBitsB>(dig, vmask, wc, lane);
+        const MsdBucket bn = uni_bucket(p.bk, tin.x);  // prefetch 2: its bucket
+        __syncthreads();
+        PB_STAMP(2);
+        tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const uint32_t d = dig[it] & 0xffffu;
+            dig[it] = s_bin[d] + wc[d] + (dig[it] >> 16);
+        }
+        __syncthreads();  // counters dead: the region becomes the staging tile
+        PB_STAMP(3);
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+        if (gn < ntl && (uint32_t)tid < runs_of(tin, bn, gn)) le = list64[tin.y + tid];  // prefetch 3: its runs
+#pragma unroll
+        for (int k = 0; k < (RADIX + kMsdThreads) / kMsdThreads; k++) {  // fixed count: see st_load_recs
+            const int d = tid + k * kMsdThreads;
+            if (d <= RADIX && !(p.dbg & 8)) p.offs[g * kOffsB + d] = (uint16_t)s_bin[d];  // [RADIX] = nrows
+        }
+        __syncthreads();
+        PB_STAMP(4);
+        int64_t *dst = p.out + g * T * COLS;
+        if (!(p.dbg & 2)) {
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const int s = min(tid + it * kMsdThreads, nrows - 1);
+                int64_t r[COLS];
+                load_row<COLS>(s_rows + (size_t)s * COLS, r);
+                store_row<COLS>(dst + (size_t)s * COLS, r);
+            }
+        }
+        PB_STAMP(5);
+        if ((p.dbg & 1) && tid == 0) atomicAdd(&g_pb_phase[7], 1ull);
+        __syncthreads();  // staging region read out before the next tile's list lands in it
+        ti = tin;
+        b = bn;
     }
-    wave_rank<ITEMS, kBitsB>(dig, vmask, wc, lane);
-    __syncthreads();
-    PB_STAMP(2);
-    tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const uint32_t d = dig[it] & 0xffffu;
-        dig[it] = s_bin[d] + wc[d] + (dig[it] >> 16);
-    }
-    __syncthreads();  // counters dead: the region becomes the staging tile
-    PB_STAMP(3);
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++)
-        if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    for (int d = tid; d <= RADIX; d += kMsdThreads) p.offs[g * kOffsB + d] = (uint16_t)s_bin[d];  // [RADIX] = nrows
-    __syncthreads();
-    PB_STAMP(4);
-    int64_t *dst = p.out + g * T * COLS;
-#pragma unroll
-    for (int it = 0; it < ITEMS; it++) {
-        const int s = min(tid + it * kMsdThreads, nrows - 1);
-        int64_t r[COLS];
-        load_row<COLS>(s_rows + (size_t)s * COLS, r);
-        store_row<COLS>(dst + (size_t)s * COLS, r);
-    }
-    PB_STAMP(5);
-    if (p.dbg && tid == 0) atomicAdd(&g_pb_phase[7], 1ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -1628,6 +1697,14 @@ __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdG
     }
 }
 
+__device__ unsigned long long g_st_sub[8];
+#define ST_SUB(k)                                                   \
+    if (p.dbg && tid == 0) {                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        atomicAdd(&g_st_sub[k], t_ - st_t);                         \
+        st_t = t_;                                                  \
+    }
+
 // run lists from the offsB values (union region), then the row gathers of
 // group g into registers (row v = tid + k * kStThreads).  Row v's range is
 // found in O(1): the range holding the wave's first row (btab) and the last
@@ -1635,6 +1712,7 @@ __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdG
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    unsigned long long st_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
@@ -1653,6 +1731,7 @@ __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup
         }
     }
     __syncthreads();
+    ST_SUB(4);
     const uint32_t n[2] = {g.nR, p.ntab > 1 ? g.nS : 0u};
 #pragma unroll
     for (int x = 0; x < 2; x++)
@@ -1669,6 +1748,7 @@ __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup
             }
             rows[x][k] = r;
         }
+    ST_SUB(5);
 }
 
 __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key ? r.y : r.x; }
@@ -1676,13 +1756,6 @@ __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key 
 // stage + counting sort of group g whose rows are in `rows`, then the zip
 // join lookups (mmask / part); false: an equal-key run over kMaxDupRun (the
 // group is handed to the radix list)
-__device__ unsigned long long g_st_sub[8];
-#define ST_SUB(k)                                                   \
-    if (p.dbg && tid == 0) {                                        \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        atomicAdd(&g_st_sub[k], t_ - st_t);                         \
-        st_t = t_;                                                  \
-    }
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt]) {
@@ -1832,32 +1905,40 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     // output word wd = row * 3 + column: R key, R payload, S payload
     int64_t *dst = p.slots + (int64_t)g.outR * 3;
     const int key2 = p.key2;
-    for (uint32_t wd = tid; wd < total * 3u; wd += kStThreads) {
-        const uint32_t row = wd / 3u, c = wd - row * 3u;
-        const uint32_t m = sm.match[row];
-        int64_t val;
-        if (c < 2) {
-            const i64x2 r = sm.stage[0][kR[m >> kFinIdxBits] & IDX];
-            val = c ? r.y : r.x;
-        } else {
-            const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
-            val = key2 ? r.x : r.y;
+    // fixed trip count (total <= kGroupCap), see st_load_recs
+    constexpr int EMIT_IT = (3 * kGroupCap + kStThreads - 1) / kStThreads;
+#pragma unroll
+    for (int it = 0; it < EMIT_IT; it++) {
+        const uint32_t wd = tid + it * kStThreads;
+        if (wd < total * 3u) {
+            const uint32_t row = wd / 3u, c = wd - row * 3u;
+            const uint32_t m = sm.match[row];
+            int64_t val;
+            if (c < 2) {
+                const i64x2 r = sm.stage[0][kR[m >> kFinIdxBits] & IDX];
+                val = c ? r.y : r.x;
+            } else {
+                const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
+                val = key2 ? r.x : r.y;
+            }
+            dst[wd] = val;
         }
-        dst[wd] = val;
     }
 }
 
 // copy the records of this workgroup's local groups [t0, t0 + kStRecs) into
-// ring half h (local group t is dense group g0 + t * gs)
+// ring half h (local group t is dense group g0 + t * gs): one word per thread,
+// no loop -- a dynamic-count load loop here would make hipcc's waitcnt pass
+// give up counting, and every group's prefetched rows would then be consumed
+// behind a vmcnt(0) that also drains the previous group's stores
 __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0, int64_t gs, int64_t t0,
                                              int64_t cnt, StSmem &sm, int h) {
     constexpr int WORDS = sizeof(MsdGroup) / 8;
+    static_assert(kStRecs * WORDS == kStThreads, "one record word per thread");
     int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
-    const int64_t nw = min((int64_t)kStRecs, cnt - t0) * WORDS;
-    for (int64_t i = threadIdx.x; i < nw; i += kStThreads) {
-        const int64_t t = t0 + i / WORDS;
-        dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
-    }
+    const int i = threadIdx.x;
+    const int64_t t = t0 + i / WORDS;
+    if (t < cnt) dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
 }
 
 // persistent staged kernel.  XCD-aware schedule: the dense (key-ordered)
@@ -1962,7 +2043,7 @@ static const unsigned long long zero8_pb[8] = {0};
 hipError_t read_msd_phases(unsigned long long *out16) {
     hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 10);
     if (e != hipSuccess) return e;
-    e = hipMemcpyFromSymbol(out16 + 10, HIP_SYMBOL(g_st_sub), sizeof(unsigned long long) * 4);
+    e = hipMemcpyFromSymbol(out16 + 10, HIP_SYMBOL(g_st_sub), sizeof(unsigned long long) * 6);
     if (e != hipSuccess) return e;
     e = hipMemcpyFromSymbol(out16 + 16, HIP_SYMBOL(g_pb_phase), sizeof(unsigned long long) * 8);
     if (e != hipSuccess) return e;
@@ -2140,8 +2221,9 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
     if (max_tiles <= 0) return hipSuccess;
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
     MsdPartBParams p = p_in;
-    p.dbg = dbg;
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3((unsigned)max_tiles), dim3(kMsdThreads),
+    p.dbg = p_in.dbg ? p_in.dbg : dbg;  // explicit ablation bits (smj_debug_part_b_time) or SMJ_DEBUG_MSD
+    const unsigned grid = (unsigned)std::min<int64_t>(max_tiles, kMsdPartBGrid);  // persistent
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(kMsdThreads),
                                              0, s, p));
     return hipGetLastError();
 }

@@ -29,6 +29,7 @@ for s in $STEPS; do
     dist)  run dist 600 python -u -m pytest tests/test_dist_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     quick) run quick 300 python bench.py --cpu-sample 0 ;;
     phases) run phases 300 python tools/msd_phases.py ;;
+    pbab)  run pbab 300 python tools/pb_ablate.py ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0

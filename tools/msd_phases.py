@@ -38,8 +38,8 @@ for k in range(9):
     if names[k]:
         print(f"  {names[k]:18s} {buf[k] / max(groups, 1):10.0f}  {100 * buf[k] / max(tot, 1):5.1f}%")
 print(f"  total              {tot / max(groups, 1):10.0f}")
-sub = ["sort: stage+hist", "sort: scan", "sort: scatter", "sort: dup fix-up"]
-for k in range(4):
+sub = ["sort: stage+hist", "sort: scan", "sort: scatter", "sort: dup fix-up", "issue: lists", "issue: row loads"]
+for k in range(6):
     print(f"    {sub[k]:18s} {buf[10 + k] / max(groups, 1):10.0f}")
 tiles = buf[23]
 pb = ["list + lookups", "row loads issued", "rank (loads land)", "digit starts", "stage + offs", "stores issued"]
