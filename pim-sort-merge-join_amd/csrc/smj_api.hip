@@ -569,17 +569,18 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
 int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
-    int T_[2] = {1, 1};
+    int T_[2] = {1, 1}, TB_[2] = {1, 1};  // pass-A / pass-B tile rows
     int64_t tilesA[2] = {0, 0}, maxB[2] = {0, 0};
     for (int x = 0; x < ntab; x++) {
         const MsdIn &t = in[x];
         MsdTabScratch &ts = ms->t[x];
         T_[x] = msd_tile(t.cols);
+        TB_[x] = msd_tile_b(t.cols);
         tilesA[x] = (t.n + T_[x] - 1) / T_[x];
-        maxB[x] = tilesA[x] + kBucketsA;
+        maxB[x] = (t.n + TB_[x] - 1) / TB_[x] + kBucketsA;  // every bucket adds <= 1 partial pass-B tile
         const size_t W = (size_t)t.cols * 8;
         SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, std::max<size_t>(1, t.n) * W));
-        SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * T_[x] * W));
+        SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * TB_[x] * W));
         SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsA * 4));
         SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
         SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
@@ -624,7 +625,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             bp.segC[x] = segC(x);
             bp.segmm[x] = segMM(x);
             bp.ntiles[x] = tilesA[x];
-            bp.tile[x] = T_[x];
+            bp.tile[x] = TB_[x];
             bp.bk[x] = (MsdBucket *)ms->t[x].bk;
         }
         bp.ntab = ntab;
@@ -632,7 +633,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         bp.plan = ms->plan;
         HIP_TRY(launch_msd_bases(bp, s));
         for (int x = 0; x < ntab; x++)
-            HIP_TRY(launch_msd_runs_apply((const uint32_t *)ms->t[x].offsA, tilesA[x], T_[x], segL(x), segC(x),
+            HIP_TRY(launch_msd_runs_apply((const uint32_t *)ms->t[x].offsA, tilesA[x], T_[x], TB_[x], segL(x), segC(x),
                                           (const MsdBucket *)ms->t[x].bk, (uint2 *)ms->t[x].list,
                                           (uint2 *)ms->t[x].tinfo, s));
     }
@@ -654,7 +655,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         for (int x = 0; x < ntab; x++) {
             gp.offs[x] = (const uint16_t *)ms->t[x].offsB;
             gp.bk[x] = (const MsdBucket *)ms->t[x].bk;
-            gp.tile[x] = T_[x];
+            gp.tile[x] = TB_[x];
         }
         gp.ntab = ntab;
         gp.part = ms->gpart;
@@ -671,7 +672,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     MsdFinalParams fp{};
     for (int x = 0; x < ntab; x++)
         fp.tab[x] = MsdTab{(const int64_t *)ms->t[x].tempB, (const uint16_t *)ms->t[x].offsB,
-                           (const MsdBucket *)ms->t[x].bk, in[x].out, T_[x], in[x].cols, in[x].key, x};
+                           (const MsdBucket *)ms->t[x].bk, in[x].out, TB_[x], in[x].cols, in[x].key, x};
     fp.groups = ms->groups;
     fp.slots = (int64_t *)ms->slots;
     fp.counts = ms->counts;

@@ -141,6 +141,10 @@ __host__ __device__ constexpr int msd_items(int cols) {
     return cols == 1 ? 16 : cols == 2 ? 8 : cols == 3 ? 5 : cols == 4 ? 4 : cols == 5 ? 3 : 2;
 }
 __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_items(cols); }
+// pass-B tiles (rows); part_b runs 1024 threads x 4 rows for 2-column tables
+// (64 VGPRs, 2 x 16 waves per CU: part_b is latency-bound)
+__host__ __device__ constexpr int msd_tile_b(int cols) { return msd_tile(cols); }
+__host__ __device__ constexpr int pb_threads(int cols) { return cols == 2 ? 1024 : kMsdThreads; }
 constexpr int kSplA = 127;                 // pass-A splitters
 constexpr int kBucketsA = 2 * kSplA + 1;   // 255 pass-A buckets (odd = one key value)
 constexpr int kOffsA = 256;                // offsA row: 255 bucket starts + the tile's row count
@@ -273,7 +277,7 @@ hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
                                const int64_t *tmm, int64_t *segmm, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
-hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, const uint32_t *segL,
+hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
                                  const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
                                  hipStream_t s);
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);

@@ -63,6 +63,25 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum
     return before + incl - v;
 }
 
+// block_excl_scan without the trailing barrier (s_wsum must not be rewritten
+// before every thread has read it: callers separate uses by a barrier)
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan_nb(uint32_t v, uint32_t *s_wsum, uint32_t *total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const uint32_t x = s_wsum[w];
+        before += (w < wave) ? x : 0u;
+        all += x;
+    }
+    *total = all;
+    return before + incl - v;
+}
+
 template <int NW>
 __device__ __forceinline__ void block_minmax(int64_t &mn, int64_t &mx, int64_t *s_mm) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -451,7 +470,7 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
 // grid (ceil(nb / 64), kMsdSegs) x 256: emit the run list entries of every
 // bucket (lane) for this segment, and the first run of every pass-B tile
 __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__restrict__ offs, int64_t ntiles,
-                                                             int T, const uint32_t *__restrict__ segL,
+                                                             int T, int TB, const uint32_t *__restrict__ segL,
                                                              const uint32_t *__restrict__ segC,
                                                              const MsdBucket *__restrict__ bk,
                                                              uint2 *__restrict__ list, uint2 *__restrict__ tinfo) {
@@ -483,14 +502,14 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
         Q += partC[v][lane];
     }
     const MsdBucket b = bk[a];
-    const uint32_t uT = (uint32_t)T;
+    const uint32_t uT = (uint32_t)TB;  // pass-B tile rows (T: pass-A tile rows)
     for (int64_t t = c0; t < c1; t++) {
         const uint32_t o = offs[t * kOffsA + a];
         const uint32_t len = offs[t * kOffsA + a + 1] - o;
         if (len) {
             list[b.list_base + Q] = make_uint2((uint32_t)(t * T) + o, P);
-            const uint32_t k = (P + uT - 1) / uT;  // the pass-B tile starting inside this run, if any
-            if (k * uT < P + len) tinfo[b.tile_base + k] = make_uint2((uint32_t)a, b.list_base + Q);
+            for (uint32_t k = (P + uT - 1) / uT; k * uT < P + len; k++)  // pass-B tiles starting inside this run
+                tinfo[b.tile_base + k] = make_uint2((uint32_t)a, b.list_base + Q);
             Q++;
             P += len;
         }
@@ -529,7 +548,8 @@ __device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a)
 // [k] cycles of phase k summed over tiles (thread 0's view), [7] tiles.
 // Ablation bits for smj_debug_part_b_time (timing only, output invalid):
 // 2 = no row stores, 4 = synthetic rows instead of the gathers, 8 = no offsB stores,
-// 16 = no ballot ranking (ranks wrong), 32 = no run-list lookups (with 4)
+// 16 = force the ballot ranking path, 32 = no run-list lookups (with 4),
+// 64 = 40 KiB of padding LDS (one workgroup per CU)
 __device__ unsigned long long g_pb_phase[8];
 #define PB_STAMP(k)                                                 \
     if ((p.dbg & 1) && tid == 0) {                                        \
@@ -538,20 +558,31 @@ __device__ unsigned long long g_pb_phase[8];
         pb_t = t_;                                                  \
     }
 
+constexpr int kPbFastMax = 16;  // longest sub-bucket run of a tile the atomic-rank path orders
+
 template <int COLS>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPartBParams p) {
-    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kRadB;
-    // run lookup aids after the list: at[r] = entry of the run starting at tile
-    // row r, a bitmap of run starts, btab[b] = entry holding tile row 64 * b
+__global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4) void msd_part_b_kernel(
+    const MsdPartBParams p) {
+    constexpr int NT = pb_threads(COLS), NW = NT / 64, T = msd_tile_b(COLS), ITEMS = T / NT, RADIX = kRadB;
+    constexpr int DPT = RADIX / NT;  // histogram digits per thread (even)
+    static_assert(T % NT == 0 && RADIX % (2 * NT) == 0, "tile / histogram split");
+    // One LDS region, reused per phase: (1) the run list + lookup aids
+    // (at[r] = entry of the run starting at tile row r, a bitmap of run
+    // starts, btab[b] = entry holding tile row 64 * b); (2) the atomic path's
+    // tile-row permutation + the ballot path's counters; (3) the staging tile.
+    // ~36 KiB for 2 columns: 3-4 workgroups per CU (part_b is latency-bound:
+    // one workgroup per CU instead of two costs +54 %, tools/pb_ablate.py).
     constexpr int LISTB = (T + 1) * 8, ATB = T * 2, BMB = T / 8, BTB = T / 64 * 2;
-    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4, LKB = LISTB + ATB + BMB + BTB;
-    constexpr int UB0 = ROWB > CNTB ? ROWB : CNTB;
+    constexpr int ROWB = T * COLS * 8, PERMB = T * 2, CNTB = RADIX * 4, LKB = LISTB + ATB + BMB + BTB;
+    constexpr int UB0 = ROWB > PERMB + CNTB ? ROWB : PERMB + CNTB;
     constexpr int UB = UB0 > LKB ? UB0 : LKB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
-    __shared__ uint32_t s_bin[RADIX + 1];
-    __shared__ uint32_t s_wsum[kMsdWaves];
+    __shared__ uint32_t s_hist[RADIX / 2];  // packed u16 sub-bucket counts, then starts
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint32_t s_slow;
+    uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_u);
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_u + PERMB);
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
-    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
     uint2 *s_list = reinterpret_cast<uint2 *>(s_u);
     uint16_t *s_at = reinterpret_cast<uint16_t *>(s_u + LISTB);
     uint32_t *s_bm = reinterpret_cast<uint32_t *>(s_u + LISTB + ATB);
@@ -580,6 +611,9 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
     // this path (nothing issued after the load) with the back edge and hipcc
     // waits vmcnt(0) every tile, draining the previous tile's 64 KiB of stores
     asm volatile("" ::"v"(le));
+#pragma unroll
+    for (int k = 0; k < DPT / 2; k++) s_hist[DPT / 2 * tid + k] = 0;
+    if (tid == 0) s_slow = 0;
     for (; g < ntl; g += gridDim.x) {
         const uint32_t v0 = (uint32_t)(g - b.tile_base) * (uint32_t)T;
         const int nrows = (int)min((uint32_t)T, b.L - v0);
@@ -587,11 +621,11 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         const int J = (int)runs_of(ti, b, g);
         if (p.dbg & 32) goto lookups_done;
         if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
-        for (int j = tid + kMsdThreads; j < J; j += kMsdThreads)  // > kMsdThreads runs: rare
+        for (int j = tid + NT; j < J; j += NT)  // > NT runs: rare
             reinterpret_cast<uint64_t *>(s_list)[j] = list64[q0 + j];
-        for (int i = tid; i < T / 32; i += kMsdThreads) s_bm[i] = 0;
+        for (int i = tid; i < T / 32; i += NT) s_bm[i] = 0;
         __syncthreads();
-        for (int j = tid; j < J; j += kMsdThreads) {  // runs are non-empty: starts strictly increase
+        for (int j = tid; j < J; j += NT) {  // runs are non-empty: starts strictly increase
             const uint32_t y = s_list[j].y;
             const uint32_t s0 = y > v0 ? y - v0 : 0u;
             const uint32_t e = j + 1 < J ? s_list[j + 1].y - v0 : (uint32_t)nrows;
@@ -623,12 +657,10 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
         }
         const int64_t gn = g + gridDim.x;
         const uint2 tin = uni_tinfo(p.tinfo, min(gn, ntl - 1));  // prefetch 1: next tile's info
-        __syncthreads();  // list dead: the region becomes the counters
+        __syncthreads();  // list dead: the region becomes the counters or the staging tile
         PB_STAMP(1);
-        uint32_t *wc = s_wcnt + wave * RADIX;
-        zero_counters<RADIX>(wc, lane);
 
-        uint32_t dig[ITEMS];
+        uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
         uint32_t vmask = 0;
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
@@ -638,34 +670,108 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_b_kernel(const MsdPar
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
-        if (!(p.dbg & 16)) wave_rank<ITEMS, kBitsB>(dig, vmask, wc, lane);
+        // Atomic path: one packed-u16 LDS histogram, ranks in atomic order.
+        // Stability is restored per row below (sub-bucket runs of a tile are
+        // short); a tile with a sub-bucket over kPbFastMax rows takes the
+        // ballot path instead (wave_rank + per-wave counters).
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if ((vmask >> it) & 1u) {
+                const uint32_t d = dig[it], sh = 16u * (d & 1u);
+                dig[it] = d | (((atomicAdd(&s_hist[d >> 1], 1u << sh) >> sh) & 0xffffu) << 16);
+            }
         const MsdBucket bn = uni_bucket(p.bk, tin.x);  // prefetch 2: its bucket
         __syncthreads();
         PB_STAMP(2);
-        tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
+        {  // thread t owns digits [DPT t, DPT t + DPT): counts -> starts, packed alike
+            uint32_t hw[DPT / 2], sum = 0, cmax = 0;
 #pragma unroll
-        for (int it = 0; it < ITEMS; it++) {
-            const uint32_t d = dig[it] & 0xffffu;
-            dig[it] = s_bin[d] + wc[d] + (dig[it] >> 16);
+            for (int k = 0; k < DPT / 2; k++) {
+                hw[k] = s_hist[DPT / 2 * tid + k];
+                const uint32_t lo = hw[k] & 0xffffu, hi = hw[k] >> 16;
+                sum += lo + hi;
+                cmax = max(cmax, max(lo, hi));
+            }
+            if (cmax > (uint32_t)kPbFastMax || (p.dbg & 16)) s_slow = 1;
+            uint32_t tot;
+            uint32_t st = block_excl_scan_nb<NW>(sum, s_wsum, &tot);  // + barrier
+#pragma unroll
+            for (int k = 0; k < DPT / 2; k++) {
+                const uint32_t lo = hw[k] & 0xffffu, hi = hw[k] >> 16;
+                s_hist[DPT / 2 * tid + k] = st | ((st + lo) << 16);
+                st += lo + hi;
+            }
         }
-        __syncthreads();  // counters dead: the region becomes the staging tile
+        __syncthreads();
+        const bool slow = s_slow != 0;
+        if (!slow) {
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u);
+                    s_perm[((s_hist[d >> 1] >> sh) & 0xffffu) + (dig[it] >> 16)] = (uint16_t)(lrow0 + it * 64);
+                }
+            __syncthreads();
+            // stable rank: the rows of the sub-bucket run that precede this one in the tile
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u), hw = s_hist[d >> 1];
+                    const uint32_t st = (hw >> sh) & 0xffffu;
+                    const uint32_t en = (d & 1u) ? (d + 1u < (uint32_t)RADIX ? (s_hist[(d + 1) >> 1] & 0xffffu) : (uint32_t)nrows)
+                                                 : (hw >> 16);
+                    const uint32_t r = (uint32_t)(lrow0 + it * 64);
+                    uint32_t rank = 0;
+                    if (en - st > 1u)
+                        for (uint32_t j = st; j < en; j++) rank += (uint32_t)s_perm[j] < r;
+                    dig[it] = st + rank;
+                }
+        } else {
+            // a sub-bucket run over kPbFastMax rows: ballot ranks (wave_rank),
+            // the waves taking turns on one counter array so that the ranks
+            // follow tile-row order across waves too
+#pragma unroll
+            for (int k = 0; k < RADIX / NT; k++) s_cnt[tid + k * NT] = 0;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) dig[it] &= 0xffffu;
+            __syncthreads();
+            for (int w = 0; w < NW; w++) {
+                if (wave == w) wave_rank<ITEMS, kBitsB>(dig, vmask, s_cnt, lane);
+                __syncthreads();
+            }
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u);
+                    dig[it] = ((s_hist[d >> 1] >> sh) & 0xffffu) + (dig[it] >> 16);
+                }
+        }
+        __syncthreads();  // permutation / counters dead: the region becomes the staging tile
         PB_STAMP(3);
 #pragma unroll
         for (int it = 0; it < ITEMS; it++)
             if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
         if (gn < ntl && (uint32_t)tid < runs_of(tin, bn, gn)) le = list64[tin.y + tid];  // prefetch 3: its runs
+        if (!(p.dbg & 8)) {
+            uint16_t *o = p.offs + g * kOffsB;
 #pragma unroll
-        for (int k = 0; k < (RADIX + kMsdThreads) / kMsdThreads; k++) {  // fixed count: see st_load_recs
-            const int d = tid + k * kMsdThreads;
-            if (d <= RADIX && !(p.dbg & 8)) p.offs[g * kOffsB + d] = (uint16_t)s_bin[d];  // [RADIX] = nrows
+            for (int k = 0; k < DPT / 2; k++) {  // thread t's starts
+                const uint32_t w = s_hist[DPT / 2 * tid + k];
+                o[DPT * tid + 2 * k] = (uint16_t)w;
+                o[DPT * tid + 2 * k + 1] = (uint16_t)(w >> 16);
+            }
+            if (tid == 0) o[RADIX] = (uint16_t)nrows;
         }
         __syncthreads();
+#pragma unroll
+        for (int k = 0; k < DPT / 2; k++) s_hist[DPT / 2 * tid + k] = 0;  // for the next tile
+        if (tid == 0) s_slow = 0;
         PB_STAMP(4);
         int64_t *dst = p.out + g * T * COLS;
         if (!(p.dbg & 2)) {
 #pragma unroll
             for (int it = 0; it < ITEMS; it++) {
-                const int s = min(tid + it * kMsdThreads, nrows - 1);
+                const int s = min(tid + it * NT, nrows - 1);
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)s * COLS, r);
                 store_row<COLS>(dst + (size_t)s * COLS, r);
@@ -1150,22 +1256,6 @@ struct FinSmem {
 
 // exclusive block scan without the trailing barrier: callers alternate wsum
 // buffers so that the next scan cannot overwrite sums still being read
-template <int NW>
-__device__ __forceinline__ uint32_t block_excl_scan_nb(uint32_t v, uint32_t *s_wsum, uint32_t *total) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t incl = wave_incl_scan(v, lane);
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-        const uint32_t x = s_wsum[w];
-        before += (w < wave) ? x : 0u;
-        all += x;
-    }
-    *total = all;
-    return before + incl - v;
-}
 
 struct FinalPref {               // the group whose keys are in flight
     uint32_t o0[2], o1[2];       // offsB[tile][b0], offsB[tile][b1] of this thread's tile
@@ -2209,12 +2299,29 @@ hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, const uint32_t *segL,
+hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
                                  const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
                                  hipStream_t s) {
     const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
-    hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, offs, ntiles, T, segL, segC, bk, list, tinfo);
+    hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, offs, ntiles, T, TB, segL, segC, bk, list, tinfo);
     return hipGetLastError();
+}
+
+// resident workgroups of a `threads`-thread kernel on the current device
+// (occupancy x CUs), cached per kernel and LDS pad
+template <class K>
+static int64_t resident_blocks(K kernel, int threads, size_t dyn_lds) {
+    static int cached[2] = {0, 0};
+    int &c = cached[dyn_lds ? 1 : 0];
+    if (!c) {
+        int dev = 0, per = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, dyn_lds) != hipSuccess || per < 1)
+            return kMsdPartBGrid;
+        c = per * cus;
+    }
+    return c;
 }
 
 hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_tiles, hipStream_t s) {
@@ -2222,9 +2329,13 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
     MsdPartBParams p = p_in;
     p.dbg = p_in.dbg ? p_in.dbg : dbg;  // explicit ablation bits (smj_debug_part_b_time) or SMJ_DEBUG_MSD
-    const unsigned grid = (unsigned)std::min<int64_t>(max_tiles, kMsdPartBGrid);  // persistent
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(kMsdThreads),
-                                             0, s, p));
+    const size_t pad = (p.dbg & 64) ? 40960 : 0;  // ablation: dynamic LDS pad -> 1 workgroup per CU
+    // persistent: exactly the resident workgroups (tiles are dealt statically)
+    SMJ_COLS_SWITCH(cols, {
+        const unsigned grid =
+            (unsigned)std::min<int64_t>(max_tiles, resident_blocks(msd_part_b_kernel<C>, pb_threads(C), pad));
+        hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(pb_threads(C)), pad, s, p);
+    });
     return hipGetLastError();
 }
 

@@ -20,9 +20,9 @@ S = ops.gen_uniform(n, seed=2, key_range=3 * n)
 ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000))
 torch.cuda.synchronize()
 ms = ctypes.c_float()
-variants = [(0, "baseline"), (2, "no row stores"), (8, "no offs stores"), (10, "no stores at all"),
+variants = [(0, "baseline"), (64, "1 workgroup per CU"), (66, "1 WG/CU, no row stores"), (2, "no row stores"), (8, "no offs stores"), (10, "no stores at all"),
             (4, "synthetic rows (no gathers)"), (6, "no gathers, no row stores"), (14, "no global traffic"),
-            (30, "no traffic, no ranking"), (46, "no traffic, no lookups"), (62, "no traffic/ranking/lookups")]
+            (16, "ballot ranking path (forced)"), (30, "no traffic, ballot path"), (46, "no traffic, no lookups")]
 for dbg, name in variants:
     assert lib.smj_debug_part_b_time(dbg, 10, ctypes.byref(ms)) == 0
     print(f"dbg {dbg:2d} {name:30s} {ms.value:.3f} ms (R + S)", flush=True)
