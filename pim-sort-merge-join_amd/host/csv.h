@@ -33,6 +33,12 @@ int smj_csv_load(const char *path, int *col_num, int *row_num, T **out);
 /* Writes the result table.  Returns 0 or -1. */
 int smj_csv_save(const char *path, int col_num, int64_t row_num, const T *arr);
 
+/* Threads for smj_csv_load / smj_csv_save: n >= 1 fixes
+ * the count (1 = the serial code), 0 = SMJ_CSV_THREADS, else OMP_NUM_THREADS,
+ * else min(online CPUs, 16).  Small files use fewer threads.  The result is
+ * byte-identical whatever the count. */
+void smj_csv_set_threads(int n);
+
 #ifdef __cplusplus
 }
 #endif

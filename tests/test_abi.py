@@ -67,13 +67,32 @@ def csv_lib():
     lib.smj_csv_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                  ctypes.POINTER(ctypes.c_void_p)]
     lib.smj_csv_save.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]
+    lib.smj_csv_set_threads.argtypes = [ctypes.c_int]
     return lib
+
+
+@pytest.fixture(params=[1, 7], ids=["serial", "7threads"])
+def csv_threads(request):
+    """Both CSV code paths: the serial reference loop and the chunked parallel one."""
+    lib = csv_lib()
+    lib.smj_csv_set_threads(request.param)
+    yield request.param
+    lib.smj_csv_set_threads(0)
+
+
+def load_with(lib, path):
+    c, r, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_void_p()
+    assert lib.smj_csv_load(str(path).encode(), ctypes.byref(c), ctypes.byref(r), ctypes.byref(p)) == 0
+    n = c.value * r.value
+    got = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_int64)), shape=(max(n, 1),))[:n].copy()
+    ctypes.CDLL(None).free(p)
+    return got.reshape(r.value, c.value)
 
 
 @pytest.mark.parametrize("name", ["data1.csv.gz", "data_1.csv.gz", "kat_r.csv", "kat_s.csv", "dup_r.csv",
                                   "atoi_r.csv", "atoi_s.csv", "wide_s.csv", "neg_r.csv", "empty_t.csv",
                                   "one_r.csv"])
-def test_csv_load_matches_reference_semantics(pkg_built, oracle_built, golden_dir, name):
+def test_csv_load_matches_reference_semantics(pkg_built, oracle_built, golden_dir, name, csv_threads):
     lib = csv_lib()
     path = fixture_path(golden_dir, name)
     c, r, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_void_p()
@@ -86,7 +105,7 @@ def test_csv_load_matches_reference_semantics(pkg_built, oracle_built, golden_di
     np.testing.assert_array_equal(got.reshape(ref.shape), ref)
 
 
-def test_csv_long_lines_and_nul(pkg_built, oracle_built, tmp_path):
+def test_csv_long_lines_and_nul(pkg_built, oracle_built, tmp_path, csv_threads):
     """fgets(1024) line splitting and C-string truncation at NUL, as the reference."""
     p = tmp_path / "odd.csv"
     long_tok = "7" * 1500
@@ -101,7 +120,7 @@ def test_csv_long_lines_and_nul(pkg_built, oracle_built, tmp_path):
     np.testing.assert_array_equal(got.reshape(ref.shape), ref)
 
 
-def test_csv_save_bytes(pkg_built, oracle_built, tmp_path):
+def test_csv_save_bytes(pkg_built, oracle_built, tmp_path, csv_threads):
     rng = np.random.default_rng(1)
     t = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, size=(5000, 7), dtype=np.int64,
                      endpoint=True)
@@ -110,3 +129,52 @@ def test_csv_save_bytes(pkg_built, oracle_built, tmp_path):
     assert csv_lib().smj_csv_save(a.encode(), 7, len(t), t.ctypes.data) == 0
     oracle.save_csv(b, t)
     assert filecmp.cmp(a, b, shallow=False)
+
+
+def test_csv_parallel_load_spills_and_odd_lines(pkg_built, oracle_built, tmp_path):
+    """A messy file cut into many chunks: rows with extra tokens spill into
+    the next rows' cells (the reference's unbounded token index), short rows,
+    empty fields, CRLF, NUL, > 1023-byte lines, atoi overflow -- the parallel
+    loader must equal the oracle (reference semantics) cell for cell."""
+    rng = np.random.default_rng(5)
+    lines = [b"k,v,w"]
+    for i in range(60_000):
+        kind = rng.integers(0, 12)
+        if kind == 0:  # spill: 3..9 extra tokens
+            lines.append(b",".join(str(int(x)).encode() for x in rng.integers(-99, 99, size=3 + rng.integers(1, 10))))
+        elif kind == 1:  # short row
+            lines.append(str(int(rng.integers(-5, 5))).encode())
+        elif kind == 2:
+            lines.append(b",,%d,,%d\r" % (i, -i))
+        elif kind == 3:
+            lines.append(b"%d,9\x00%d,1" % (i, i))
+        elif kind == 4 and i % 50 == 0:  # a long line: fgets pieces
+            lines.append(b"5," * 700 + b"1")
+        elif kind == 5:
+            lines.append(b" +%d, -%d,99999999999999999999" % (i, i))
+        else:
+            lines.append(b"%d,%d,%d" % (int(rng.integers(0, 10**6)), i, -i))
+    p = tmp_path / "messy.csv"
+    p.write_bytes(b"\n".join(lines) + b"\n")
+    lib = csv_lib()
+    ref = oracle.load_csv(str(p))
+    for nt in (1, 3, 16, 61):
+        lib.smj_csv_set_threads(nt)
+        got = load_with(lib, p)
+        assert got.shape == ref.shape, nt
+        np.testing.assert_array_equal(got, ref, err_msg=f"{nt} threads")
+    lib.smj_csv_set_threads(0)
+
+
+def test_csv_parallel_save_equals_serial(pkg_built, tmp_path):
+    rng = np.random.default_rng(9)
+    t = rng.integers(-(10**12), 10**12, size=(700_001, 3), dtype=np.int64)
+    lib = csv_lib()
+    outs = []
+    for nt in (1, 5):
+        lib.smj_csv_set_threads(nt)
+        path = str(tmp_path / f"o{nt}.csv")
+        assert lib.smj_csv_save(path.encode(), 3, len(t), t.ctypes.data) == 0
+        outs.append(path)
+    lib.smj_csv_set_threads(0)
+    assert filecmp.cmp(outs[0], outs[1], shallow=False)
