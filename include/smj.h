@@ -14,7 +14,11 @@
  *     exit(EXIT_FAILURE) on error;
  *   - host-pointer calls are blocking (like dpu_launch(set, DPU_SYNCHRONOUS),
  *     app.c:247) and not re-entrant; one host thread drives the library;
- *   - tables are row-major T[row_num * col_num] (common.h), T = int64_t;
+ *   - tables are row-major T[row_num * col_num] (common.h).  The library's
+ *     cells are 64-bit; the entry points below take int64 tables (the
+ *     reference default, INT64).  Builds with T = uint64_t / double (common.h
+ *     UINT64 / DOUBLE) reach the fused pipeline through the *_typed entry
+ *     points; smj_sort_merge_join / smj_dev_sort_merge_join map to them;
  *   - all row counts must be < 2^30 per call and col_num in [1, 8].
  *
  * Two layers:
@@ -30,11 +34,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-#include "common.h"
+#include <string.h>
 
-#ifndef INT64
-#error "libsmj_hip is built for T = int64_t (common.h INT64, the reference default)"
-#endif
+#include "common.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -91,21 +93,21 @@ const char *smj_version(void);
  *   out <- rows of `in` with row[select_col] > select_val (signed 64-bit),
  *   input order kept.  bl->col_num / bl->row_num describe `in`; `out` must
  *   hold bl->row_num rows; *out_rows gets the kept count. */
-int smj_select(const dpu_block_t *bl, const T *in, T *out, int select_col, T select_val,
+int smj_select(const dpu_block_t *bl, const int64_t *in, int64_t *out, int select_col, int64_t select_val,
                int *out_rows);
 
 /* sort_dpu.c (main :189-328; host side app.c:309-406) + the merge tree:
  *   stable ascending sort of bl->row_num rows on row[key_col] (signed),
  *   in place from the caller's view.  Stability matches cpu_app.c
  *   insertion_sort_in_cpu (:172-202), the parity target. */
-int smj_sort(const dpu_block_t *bl, T *rows, int key_col);
+int smj_sort(const dpu_block_t *bl, int64_t *rows, int key_col);
 
 /* merge_dpu.c (main :55-223; host tournament app.c:412-547):
  *   out <- stable merge of two sorted runs a (bl1) and b (bl2) on key_col;
  *   equal keys take run a first.  bl1->col_num must equal bl2->col_num;
  *   out holds bl1->row_num + bl2->row_num rows. */
-int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const T *b,
-              int key_col, T *out);
+int smj_merge(const dpu_block_t *bl1, const int64_t *a, const dpu_block_t *bl2, const int64_t *b,
+              int key_col, int64_t *out);
 
 /* join.c (main :58-266; host splitters app.c:585-692):
  *   1:1 zip merge join of two tables sorted on key1 / key2 (cpu_app.c
@@ -113,15 +115,15 @@ int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const 
  *   except key2 (c1 + c2 - 1 columns), rows in key order.  *out is
  *   malloc'd by the library and free()'d by the caller (app.c:679,759);
  *   *out_rows gets the joined row count. */
-int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, const T *S, int key1,
-             int key2, T **out, int64_t *out_rows);
+int smj_join(const dpu_block_t *r, const int64_t *R, const dpu_block_t *s, const int64_t *S, int key1,
+             int key2, int64_t **out, int64_t *out_rows);
 
 /* The whole app.c pipeline (select -> sort -> merge -> join, :172-692) in one
  * call with one H2D copy per table and one D2H copy of the result.
  * *out is malloc'd (caller frees).  timing may be NULL. */
-int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, const T *S,
-                        int select_col1, T select_val1, int select_col2, T select_val2,
-                        int key1, int key2, T **out, int64_t *out_rows, smj_timing_t *timing);
+int smj_sort_merge_join(const dpu_block_t *r, const int64_t *R, const dpu_block_t *s, const int64_t *S,
+                        int select_col1, int64_t select_val1, int select_col2, int64_t select_val2,
+                        int key1, int key2, int64_t **out, int64_t *out_rows, smj_timing_t *timing);
 
 /* ---- device-pointer API ------------------------------------------------ */
 /* All smj_dev_* calls enqueue on `stream` (a hipStream_t, NULL = the legacy
@@ -134,15 +136,15 @@ int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, 
  * (sample splitters -> two tile-local partition passes -> LDS sort of final
  * groups); key_base is accepted for ABI stability and only used by the LSD
  * variant below.  Blocks until the row count is known; *out_rows gets it. */
-int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
-                        T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+int smj_dev_select_sort(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                        int64_t select_val, int key_col, uint64_t key_base, int64_t *out, int64_t *out_rows,
                         void *stream);
 
 /* The same select + sort on the LSD radix path (hist -> 10-bit chunk passes);
  * kept as the fallback of the MSD pipeline for groups it cannot sort in LDS
  * and for comparison.  Same contract as smj_dev_select_sort. */
-int smj_dev_select_sort_lsd(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
-                            T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+int smj_dev_select_sort_lsd(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                            int64_t select_val, int key_col, uint64_t key_base, int64_t *out, int64_t *out_rows,
                             void *stream);
 
 /* The whole hot path on device-resident tables in one pipeline (app.c
@@ -152,46 +154,46 @@ int smj_dev_select_sort_lsd(const T *in, int64_t n_rows, int col_num, int use_se
  * rows (min(nr, ns) x (c1 + c2 - 1) capacity).  Synchronises once at the end
  * (twice when oversized single-key or multi-key groups need the fallback);
  * h_rows[0..2] = selected rows of R, of S, joined rows. */
-int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1, int key1,
-                            const T *S, int64_t ns, int c2, int use_sel2, int sel_col2, T sel_val2, int key2,
-                            T *R_sorted, T *S_sorted, T *out, int64_t *h_rows, void *stream);
+int smj_dev_sort_merge_join(const int64_t *R, int64_t nr, int c1, int use_sel1, int sel_col1, int64_t sel_val1, int key1,
+                            const int64_t *S, int64_t ns, int c2, int use_sel2, int sel_col2, int64_t sel_val2, int key2,
+                            int64_t *R_sorted, int64_t *S_sorted, int64_t *out, int64_t *h_rows, void *stream);
 
 /* Stable select alone (a stable compaction). *out_rows is written after a
  * stream synchronisation. */
-int smj_dev_select(const T *in, int64_t n_rows, int col_num, int select_col, T select_val, T *out,
+int smj_dev_select(const int64_t *in, int64_t n_rows, int col_num, int select_col, int64_t select_val, int64_t *out,
                    int64_t *out_rows, void *stream);
 
 /* Stable merge of sorted runs a (na rows) and b (nb rows) -> out. Async. */
-int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int col_num, int key_col,
-                  T *out, void *stream);
+int smj_dev_merge(const int64_t *a, int64_t na, const int64_t *b, int64_t nb, int col_num, int key_col,
+                  int64_t *out, void *stream);
 
 /* 1:1 zip join of sorted R (nr x c1) and S (ns x c2) into out, which must
  * hold min(nr, ns) rows of (c1 + c2 - 1) columns.  The joined row count is
  * written to *d_out_rows (DEVICE int64) asynchronously; if h_out_rows is not
  * NULL the call synchronises and also stores it there. */
-int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t ns, int c2, int key1,
-                 int key2, T *out, int64_t *d_out_rows, int64_t *h_out_rows, void *stream);
+int smj_dev_join(const int64_t *R, int64_t nr, int c1, const int64_t *S, int64_t ns, int c2, int key1,
+                 int key2, int64_t *out, int64_t *d_out_rows, int64_t *h_out_rows, void *stream);
 
 /* Multi-GPU range partition, step 1: counts of selected rows
  * per destination bucket, bucket(k) = #{splitters < k} over n_split sorted
  * splitters (n_split + 1 <= 16 buckets), plus the min / max selected key.
  * Synchronises; h_counts gets n_split + 1 entries, h_minmax 2 (INT64_MAX /
  * INT64_MIN when nothing is selected). */
-int smj_dev_partition_count(const T *in, int64_t n_rows, int col_num, int use_select,
-                            int select_col, T select_val, int key_col, const T *d_splitters,
-                            int n_split, int64_t *h_counts, T *h_minmax, void *stream);
+int smj_dev_partition_count(const int64_t *in, int64_t n_rows, int col_num, int use_select,
+                            int select_col, int64_t select_val, int key_col, const int64_t *d_splitters,
+                            int n_split, int64_t *h_counts, int64_t *h_minmax, void *stream);
 
 /* Step 2: stable scatter of the selected rows into bucket-contiguous `out`
  * (bucket b starts at the exclusive prefix of h_counts).  Async. */
-int smj_dev_partition_scatter(const T *in, int64_t n_rows, int col_num, int use_select,
-                              int select_col, T select_val, int key_col, const T *d_splitters,
-                              int n_split, const int64_t *h_counts, T *out, void *stream);
+int smj_dev_partition_scatter(const int64_t *in, int64_t n_rows, int col_num, int use_select,
+                              int select_col, int64_t select_val, int key_col, const int64_t *d_splitters,
+                              int n_split, const int64_t *h_counts, int64_t *out, void *stream);
 
 /* Synthetic 2-column table (key, payload) for rows [row0, row0 + rows):
  * key = 1 + floor(splitmix64(g + seed * 0xD1B54A32D192ED03) * key_range / 2^64),
  * payload = g (the global row index).  Identical to the oracle's
  * smj_ref_gen_uniform.  Async. */
-int smj_dev_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
+int smj_dev_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
                         void *stream);
 
 /* Zipf(theta) keys over [1, domain]: rank r is drawn with
@@ -201,10 +203,64 @@ int smj_dev_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint6
  * rank scattered over [1, domain] by a bijective affine hash so hot keys are
  * spread over the key space.  zeta_n = smj_zipf_zeta(domain, theta).
  * payload = g.  Async. */
-int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
+int smj_dev_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
                      double theta, double zeta_n, void *stream);
 /* sum_{i=1..n} i^-theta (host). */
 double smj_zipf_zeta(int64_t n, double theta);
+
+/* ---- T = UINT64 / DOUBLE (common.h:3-9) ------------- */
+/* The fused pipeline with keys and select values compared as key_type
+ * (uint64 or IEEE double, as cpu_app.c compiled with that T): tables are
+ * 8-byte cells; select values are passed as their bit patterns.  The key and
+ * select columns are mapped order-preservingly onto int64 for the pipeline
+ * and back for the outputs.  DOUBLE: -0.0 equals +0.0 (and comes back as
+ * +0.0 in those columns); NaN keys are not supported. */
+#define SMJ_KEY_INT64 0
+#define SMJ_KEY_UINT64 1
+#define SMJ_KEY_DOUBLE 2
+int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, const void *R, const dpu_block_t *s,
+                              const void *S, int select_col1, uint64_t sel_bits1, int select_col2,
+                              uint64_t sel_bits2, int key1, int key2, void **out, int64_t *out_rows,
+                              smj_timing_t *timing);
+int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_t nr, int c1, int use_sel1, int sel_col1,
+                                  uint64_t sel_bits1, int key1, const void *S, int64_t ns, int c2, int use_sel2,
+                                  int sel_col2, uint64_t sel_bits2, int key2, void *R_sorted, void *S_sorted,
+                                  void *out, int64_t *h_rows, void *stream);
+
+#if defined(UINT64) || defined(DOUBLE)
+#ifdef UINT64
+#define SMJ_KEY_TYPE SMJ_KEY_UINT64
+#else
+#define SMJ_KEY_TYPE SMJ_KEY_DOUBLE
+#endif
+static inline uint64_t smj_T_bits(T v)
+{
+    uint64_t u;
+    memcpy(&u, &v, sizeof u);
+    return u;
+}
+static inline int smj_T_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s, const T *S,
+                                        int select_col1, T select_val1, int select_col2, T select_val2, int key1,
+                                        int key2, T **out, int64_t *out_rows, smj_timing_t *timing)
+{
+    return smj_sort_merge_join_typed(SMJ_KEY_TYPE, r, R, s, S, select_col1, smj_T_bits(select_val1), select_col2,
+                                     smj_T_bits(select_val2), key1, key2, (void **)out, out_rows, timing);
+}
+static inline int smj_T_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
+                                            int key1, const T *S, int64_t ns, int c2, int use_sel2, int sel_col2,
+                                            T sel_val2, int key2, T *R_sorted, T *S_sorted, T *out, int64_t *h_rows,
+                                            void *stream)
+{
+    return smj_dev_sort_merge_join_typed(SMJ_KEY_TYPE, R, nr, c1, use_sel1, sel_col1, smj_T_bits(sel_val1), key1, S,
+                                         ns, c2, use_sel2, sel_col2, smj_T_bits(sel_val2), key2, R_sorted, S_sorted,
+                                         out, h_rows, stream);
+}
+/* the app.c drop-in calls stay as written */
+#define smj_sort_merge_join smj_T_sort_merge_join
+#define smj_dev_sort_merge_join smj_T_dev_sort_merge_join
+#else
+#define SMJ_KEY_TYPE SMJ_KEY_INT64
+#endif
 
 /* ---- diagnostics ------------------------------------------------------- */
 /* Counters of the last MSD pipeline call: out4[0] = single-key groups

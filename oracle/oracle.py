@@ -14,50 +14,67 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libsmj_oracle.so")
+# the restatement compiled with common.h T = uint64_t / double (key types 1, 2)
+TYPED_LIBS = {1: os.path.join(HERE, "build", "libsmj_oracle_u64.so"),
+              2: os.path.join(HERE, "build", "libsmj_oracle_f64.so")}
+REF_LIB_U64 = os.path.join(HERE, "_ref", "libcpu_app_ref_u64.so")  # the real cpu_app.c, T = uint64_t
 CLI = os.path.join(HERE, "build", "cpu_ref")
 REF_LIB = os.path.join(HERE, "_ref", "libcpu_app_ref.so")   # the real cpu_app.c (when built)
 REF_DRIVER = os.path.join(HERE, "_ref", "ref_driver")
 
 _lib = None
+_typed = {}
 _P = ctypes.c_void_p
 _L = ctypes.c_int64
+_TV = {0: ctypes.c_int64, 1: ctypes.c_uint64, 2: ctypes.c_double}  # C type of a T value
 
 
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib():
+def lib(ktype=0):
+    """The restatement for T = int64 (0), uint64 (1) or double (2)."""
     global _lib
+    if ktype:
+        if ktype not in _typed:
+            if not os.path.exists(TYPED_LIBS[ktype]):
+                build()
+            _typed[ktype] = _bind(ctypes.CDLL(TYPED_LIBS[ktype]), ktype)
+        return _typed[ktype]
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        l = ctypes.CDLL(LIB)
-        l.smj_ref_select_into.restype = _L
-        l.smj_ref_select_into.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P]
-        l.smj_ref_insertion_sort.restype = None
-        l.smj_ref_insertion_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
-        l.smj_ref_stable_sort.restype = ctypes.c_int
-        l.smj_ref_stable_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
-        l.smj_ref_join_count.restype = _L
-        l.smj_ref_join_count.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int]
-        l.smj_ref_join.restype = _L
-        l.smj_ref_join.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int,
-                                   ctypes.POINTER(_P)]
-        l.smj_ref_gen_uniform.restype = None
-        l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
-        l.smj_ref_csv_size.restype = ctypes.c_int
-        l.smj_ref_csv_size.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
-        l.smj_ref_load_csv.restype = ctypes.c_int
-        l.smj_ref_load_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]
-        l.smj_ref_save_csv.restype = ctypes.c_int
-        l.smj_ref_save_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, _L, _P]
-        l.smj_ref_pipeline_csv.restype = _L
-        l.smj_ref_pipeline_csv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _L,
-                                           ctypes.c_int, _L, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                           ctypes.POINTER(ctypes.c_double)]
-        _lib = l
+        _lib = _bind(ctypes.CDLL(LIB), 0)
     return _lib
+
+
+def _bind(l, ktype):
+    V = _TV[ktype]
+    l.smj_ref_select_into.restype = _L
+    l.smj_ref_select_into.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, V, _P]
+    l.smj_ref_insertion_sort.restype = None
+    l.smj_ref_insertion_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
+    l.smj_ref_stable_sort.restype = ctypes.c_int
+    l.smj_ref_stable_sort.argtypes = [ctypes.c_int, _L, ctypes.c_int, _P]
+    l.smj_ref_join_count.restype = _L
+    l.smj_ref_join_count.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int]
+    l.smj_ref_join.restype = _L
+    l.smj_ref_join.argtypes = [ctypes.c_int, _L, _P, ctypes.c_int, _L, _P, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(_P)]
+    l.smj_ref_gen_uniform.restype = None
+    l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
+    l.smj_ref_csv_size.restype = ctypes.c_int
+    l.smj_ref_csv_size.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    l.smj_ref_load_csv.restype = ctypes.c_int
+    l.smj_ref_load_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]
+    l.smj_ref_save_csv.restype = ctypes.c_int
+    l.smj_ref_save_csv.argtypes = [ctypes.c_char_p, ctypes.c_int, _L, _P]
+    l.smj_ref_pipeline_csv.restype = _L
+    l.smj_ref_pipeline_csv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, V,
+                                       ctypes.c_int, V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_double)]
+    return l
 
 
 _libc = ctypes.CDLL(None)
@@ -198,12 +215,48 @@ def time_cpu_pipeline(R, S, sel=(0, 5000, 0, 5000), keys=(0, 0)):
     return dt, rows, "port"
 
 
-def pipeline_csv(path1, path2, out_path, sel=(0, 5000, 0, 5000), keys=(0, 0), insertion=False):
-    """cpu_app.c main (:303-361) with save_to_csv enabled; returns (rows, ms)."""
+def pipeline_csv(path1, path2, out_path, sel=(0, 5000, 0, 5000), keys=(0, 0), insertion=False, ktype=0):
+    """cpu_app.c main (:303-361) with save_to_csv enabled; returns (rows, ms).
+    ktype 1 / 2: the restatement compiled with T = uint64_t / double."""
     ms = ctypes.c_double(0)
-    j = lib().smj_ref_pipeline_csv(path1.encode(), path2.encode(), out_path.encode() if out_path else None,
-                                   sel[0], int(sel[1]), sel[2], int(sel[3]), keys[0], keys[1], int(insertion),
-                                   ctypes.byref(ms))
+    j = lib(ktype).smj_ref_pipeline_csv(path1.encode(), path2.encode(), out_path.encode() if out_path else None,
+                                        sel[0], sel[1], sel[2], sel[3], keys[0], keys[1], int(insertion),
+                                        ctypes.byref(ms))
     if j < 0:
         raise OSError("oracle pipeline failed")
     return j, ms.value
+
+
+# ---- T = UINT64 / DOUBLE (common.h:3-9) --------------------------------------
+def select_sort_t(table, ktype, key_col=0, select_col=0, select_val=None):
+    """select + stable sort with T = uint64 (ktype 1) / double (2): table is an
+    8-byte array of that dtype (or its int64 bits); returns the same dtype."""
+    dt = {1: np.uint64, 2: np.float64}[ktype]
+    t = np.ascontiguousarray(table).view(dt)
+    if select_val is not None:
+        out = np.empty_like(t)
+        m = lib(ktype).smj_ref_select_into(t.shape[1], t.shape[0], t.ctypes.data_as(_P), select_col,
+                                           _TV[ktype](select_val), out.ctypes.data_as(_P))
+        t = out[:m].copy()
+    else:
+        t = t.copy()
+    if lib(ktype).smj_ref_stable_sort(t.shape[1], t.shape[0], key_col, t.ctypes.data_as(_P)) != 0:
+        raise MemoryError("oracle sort")
+    return t
+
+
+def join_t(R, S, ktype, key1=0, key2=0):
+    """cpu_app.c join_in_cpu (:204-266) with T = uint64 / double."""
+    dt = {1: np.uint64, 2: np.float64}[ktype]
+    r = np.ascontiguousarray(R).view(dt)
+    s = np.ascontiguousarray(S).view(dt)
+    out = _P()
+    j = lib(ktype).smj_ref_join(r.shape[1], r.shape[0], r.ctypes.data_as(_P), s.shape[1], s.shape[0],
+                                s.ctypes.data_as(_P), key1, key2, ctypes.byref(out))
+    if j < 0:
+        raise MemoryError("oracle join")
+    tc = r.shape[1] + s.shape[1] - 1
+    res = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_int64)), shape=(max(j, 1) * tc,))
+    res = res[: j * tc].reshape(j, tc).copy().view(dt)
+    _libc.free(out)
+    return res

@@ -806,6 +806,66 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
 }
 
 // ---------------------------------------------------------------------------
+// T = UINT64 / DOUBLE (common.h:3-9): the int64 pipeline
+// on an order-preserving image of the key and select columns
+// (launch_key_map), the select value mapped alike, and the same columns of
+// the outputs mapped back.  NaN keys are outside the contract (the
+// reference's comparisons give no order for them); -0.0 compares equal to
+// +0.0 as in the reference and comes back as +0.0 in key / select columns.
+// ---------------------------------------------------------------------------
+namespace {
+struct TypedScratch {
+    void *r = nullptr, *s = nullptr;
+    size_t cr = 0, cs = 0;
+};
+std::map<int, TypedScratch> g_typed;
+
+int64_t key_fwd_host(uint64_t u, int ktype) {
+    if (ktype == SMJ_KEY_UINT64) return (int64_t)(u ^ 0x8000000000000000ull);
+    if (u == 0x8000000000000000ull) u = 0;  // -0.0
+    return (int64_t)((u >> 63) ? (u ^ 0x7fffffffffffffffull) : u);
+}
+uint32_t cols_mask(int key, int use_sel, int sel_col) { return (1u << key) | (use_sel ? 1u << sel_col : 0u); }
+}  // namespace
+
+extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_t nr, int c1, int use_sel1,
+                                             int sel_col1, uint64_t sel_bits1, int key1, const void *S, int64_t ns,
+                                             int c2, int use_sel2, int sel_col2, uint64_t sel_bits2, int key2,
+                                             void *R_sorted, void *S_sorted, void *out, int64_t *h_rows,
+                                             void *stream) {
+    if (key_type == SMJ_KEY_INT64)
+        return smj_dev_sort_merge_join((const T *)R, nr, c1, use_sel1, sel_col1, (T)sel_bits1, key1, (const T *)S, ns,
+                                       c2, use_sel2, sel_col2, (T)sel_bits2, key2, (T *)R_sorted, (T *)S_sorted,
+                                       (T *)out, h_rows, stream);
+    if (key_type != SMJ_KEY_UINT64 && key_type != SMJ_KEY_DOUBLE) return SMJ_ERR_INVALID;
+    if (!h_rows) return SMJ_ERR_INVALID;
+    SMJ_TRY(msd_check((const T *)R, nr, c1, use_sel1, sel_col1, key1, (const T *)R_sorted));
+    SMJ_TRY(msd_check((const T *)S, ns, c2, use_sel2, sel_col2, key2, (const T *)S_sorted));
+    hipStream_t st = (hipStream_t)stream;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    TypedScratch &ts = g_typed[dev];
+    SMJ_TRY(grow(&ts.r, &ts.cr, std::max<size_t>(1, (size_t)nr * c1 * 8)));
+    SMJ_TRY(grow(&ts.s, &ts.cs, std::max<size_t>(1, (size_t)ns * c2 * 8)));
+    const uint32_t mR = cols_mask(key1, use_sel1, sel_col1), mS = cols_mask(key2, use_sel2, sel_col2);
+    HIP_TRY(launch_key_map((const int64_t *)R, (int64_t *)ts.r, nr, c1, mR, key_type, 0, st));
+    HIP_TRY(launch_key_map((const int64_t *)S, (int64_t *)ts.s, ns, c2, mS, key_type, 0, st));
+    SMJ_TRY(smj_dev_sort_merge_join((const T *)ts.r, nr, c1, use_sel1, sel_col1, key_fwd_host(sel_bits1, key_type),
+                                    key1, (const T *)ts.s, ns, c2, use_sel2, sel_col2,
+                                    key_fwd_host(sel_bits2, key_type), key2, (T *)R_sorted, (T *)S_sorted, (T *)out,
+                                    h_rows, stream));
+    HIP_TRY(launch_key_map((const int64_t *)R_sorted, (int64_t *)R_sorted, h_rows[0], c1, mR, key_type, 1, st));
+    HIP_TRY(launch_key_map((const int64_t *)S_sorted, (int64_t *)S_sorted, h_rows[1], c2, mS, key_type, 1, st));
+    if (h_rows[2] > 0) {  // join rows: R's columns, then S's without key2
+        uint32_t mO = mR;
+        if (use_sel2 && sel_col2 != key2) mO |= 1u << (c1 + (sel_col2 < key2 ? sel_col2 : sel_col2 - 1));
+        HIP_TRY(launch_key_map((const int64_t *)out, (int64_t *)out, h_rows[2], c1 + c2 - 1, mO, key_type, 1, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return SMJ_OK;
+}
+
+// ---------------------------------------------------------------------------
 // multi-GPU range partition
 // ---------------------------------------------------------------------------
 extern "C" int smj_dev_partition_count(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
@@ -1087,9 +1147,17 @@ extern "C" int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_,
 extern "C" int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_, const T *S,
                                    int select_col1, T select_val1, int select_col2, T select_val2, int key1,
                                    int key2, T **out, int64_t *out_rows, smj_timing_t *timing) {
+    return smj_sort_merge_join_typed(SMJ_KEY_INT64, r, R, s_, S, select_col1, (uint64_t)select_val1, select_col2,
+                                     (uint64_t)select_val2, key1, key2, (void **)out, out_rows, timing);
+}
+
+extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, const void *R, const dpu_block_t *s_,
+                                         const void *S, int select_col1, uint64_t sel_bits1, int select_col2,
+                                         uint64_t sel_bits2, int key1, int key2, void **out, int64_t *out_rows,
+                                         smj_timing_t *timing) {
     SMJ_TRY(need_init());
-    SMJ_TRY(check_block(r, R));
-    SMJ_TRY(check_block(s_, S));
+    SMJ_TRY(check_block(r, (const T *)R));
+    SMJ_TRY(check_block(s_, (const T *)S));
     if (!out || !out_rows) return SMJ_ERR_INVALID;
     const int c1 = r->col_num, c2 = s_->col_num, tc = c1 + c2 - 1;
     if (key1 < 0 || key1 >= c1 || key2 < 0 || key2 >= c2 || select_col1 < 0 || select_col1 >= c1 ||
@@ -1112,8 +1180,8 @@ extern "C" int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_b
     HIP_TRY(hipEventRecord(ev[1], st));
     SMJ_TRY(dout.alloc((size_t)std::max<int64_t>(1, std::min(nr, ns)) * tc * 8));
     int64_t rows[3] = {0, 0, 0};
-    SMJ_TRY(smj_dev_sort_merge_join((T *)dr.p, nr, c1, 1, select_col1, select_val1, key1, (T *)ds.p, ns, c2, 1,
-                                    select_col2, select_val2, key2, (T *)drs.p, (T *)dss.p, (T *)dout.p, rows, st));
+    SMJ_TRY(smj_dev_sort_merge_join_typed(key_type, dr.p, nr, c1, 1, select_col1, sel_bits1, key1, ds.p, ns, c2, 1,
+                                          select_col2, sel_bits2, key2, drs.p, dss.p, dout.p, rows, st));
     const int64_t j = rows[2];
     HIP_TRY(hipEventRecord(ev[2], st));
     T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));

@@ -125,6 +125,10 @@ hipError_t launch_merge_tiles(const int64_t *a, int64_t na, const int64_t *b, in
                               int key_col, const int64_t *apart, int64_t ntiles, int64_t *out,
                               hipStream_t s);
 hipError_t read_phase_cycles(unsigned long long *out16);
+// T = UINT64 (ktype 1) / DOUBLE (2): order-preserving map of the colmask
+// columns onto int64 (inverse = 0) or back (inverse = 1); src may equal dst
+hipError_t launch_key_map(const int64_t *src, int64_t *dst, int64_t rows, int cols, uint32_t colmask, int ktype,
+                          int inverse, hipStream_t s);
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed,
                               uint64_t key_range, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,

@@ -1139,6 +1139,43 @@ hipError_t read_phase_cycles(unsigned long long *out16) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero));
 }
 
+// ---------------------------------------------------------------------------
+// T = UINT64 / DOUBLE (common.h): order-preserving maps onto int64, so the
+// int64 pipeline sorts, selects and joins in T's order.  uint64: x ^ 2^63
+// (an involution).  double: bits u (-0.0 folded onto +0.0, which compare
+// equal), negative values with their 63 low bits flipped.  key_map_kernel
+// applies the map (or its inverse) to the columns in colmask of every row.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t key_fwd(int64_t v, int ktype) {
+    uint64_t u = (uint64_t)v;
+    if (ktype == 1) return (int64_t)(u ^ 0x8000000000000000ull);
+    if (u == 0x8000000000000000ull) u = 0;  // -0.0
+    return (int64_t)((u >> 63) ? (u ^ 0x7fffffffffffffffull) : u);
+}
+__device__ __forceinline__ int64_t key_inv(int64_t k, int ktype) {
+    if (ktype == 1) return (int64_t)((uint64_t)k ^ 0x8000000000000000ull);
+    return k < 0 ? (int64_t)((uint64_t)k ^ 0x7fffffffffffffffull) : k;
+}
+
+__global__ __launch_bounds__(256) void key_map_kernel(const int64_t *src, int64_t *dst, int64_t cells,
+                                                      int cols, uint32_t colmask, int ktype, int inverse) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
+        int64_t v = src[i];
+        if ((colmask >> (int)(i % cols)) & 1u) v = inverse ? key_inv(v, ktype) : key_fwd(v, ktype);
+        dst[i] = v;
+    }
+}
+
+hipError_t launch_key_map(const int64_t *src, int64_t *dst, int64_t rows, int cols, uint32_t colmask, int ktype,
+                          int inverse, hipStream_t s) {
+    const int64_t cells = rows * cols;
+    if (cells <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(cells, 256), 16384));
+    hipLaunchKernelGGL(key_map_kernel, dim3(grid), dim3(256), 0, s, src, dst, cells, cols, colmask, ktype, inverse);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range,
                               hipStream_t s) {
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(rows, 256), 8192));

@@ -68,12 +68,29 @@ def select_sort_lsd(table, key_col=0, select_col=0, select_val=None, key_base=0,
     return out[: m.value]
 
 
+KEY_INT64, KEY_UINT64, KEY_DOUBLE = 0, 1, 2  # smj.h SMJ_KEY_* (common.h T)
+
+
+def _bits(v, key_type):
+    """64-bit pattern of a select value of type T."""
+    import struct
+    if key_type == KEY_DOUBLE:
+        return struct.unpack("<Q", struct.pack("<d", float(v)))[0]
+    return int(v) & ((1 << 64) - 1)
+
+
 def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=None, S_sorted=None, out=None,
-                    stream=None):
+                    stream=None, key_type=KEY_INT64):
     """The fused hot path (cpu_app.c main :303-364): select (select = (col, val)
     keeps rows with row[col] > val; None keeps all), stable sort on the key,
-    1:1 zip join.  Returns (R_sorted[:mR], S_sorted[:mS], out[:J])."""
+    1:1 zip join.  Returns (R_sorted[:mR], S_sorted[:mS], out[:J]).
+    key_type KEY_UINT64 / KEY_DOUBLE compares keys and select values as
+    common.h's T = uint64_t / double (tables: int64 tensors holding the bits,
+    or float64 tensors for double)."""
     lib = _lib.load()
+    if key_type != KEY_INT64:
+        return _sort_merge_join_typed(lib, R, S, key1, key2, select1, select2, R_sorted, S_sorted, out, stream,
+                                      key_type)
     _table(R, "R")
     _table(S, "S")
     nr, c1 = R.shape
@@ -91,6 +108,27 @@ def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=N
                                            _ptr(S), ns, c2, int(select2 is not None), s2[0], int(s2[1]), key2,
                                            _ptr(R_sorted), _ptr(S_sorted), _ptr(out), rows, _stream(stream)),
                "smj_dev_sort_merge_join")
+    return R_sorted[: rows[0]], S_sorted[: rows[1]], out[: rows[2]]
+
+
+def _sort_merge_join_typed(lib, R, S, key1, key2, select1, select2, R_sorted, S_sorted, out, stream, key_type):
+    for name, t in (("R", R), ("S", S)):
+        if not (t.is_cuda and t.dim() == 2 and t.is_contiguous() and t.element_size() == 8):
+            raise ValueError(f"{name}: contiguous 2-D 8-byte CUDA tensor required")
+    nr, c1 = R.shape
+    ns, c2 = S.shape
+    R_sorted = torch.empty_like(R) if R_sorted is None else R_sorted
+    S_sorted = torch.empty_like(S) if S_sorted is None else S_sorted
+    if out is None:
+        out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=R.dtype, device=R.device)
+    rows = (ctypes.c_int64 * 3)()
+    s1 = select1 or (0, 0)
+    s2 = select2 or (0, 0)
+    _lib.check(lib.smj_dev_sort_merge_join_typed(key_type, _ptr(R), nr, c1, int(select1 is not None), s1[0],
+                                                 _bits(s1[1], key_type), key1, _ptr(S), ns, c2,
+                                                 int(select2 is not None), s2[0], _bits(s2[1], key_type), key2,
+                                                 _ptr(R_sorted), _ptr(S_sorted), _ptr(out), rows, _stream(stream)),
+               "smj_dev_sort_merge_join_typed")
     return R_sorted[: rows[0]], S_sorted[: rows[1]], out[: rows[2]]
 
 

@@ -150,3 +150,69 @@ def test_fused_c3_baseline_size(gpu, oracle_built):
         np.testing.assert_array_equal(host(got), keep[np.argsort(keep[:, 0], kind="stable")])
         sorted_np.append(keep[np.argsort(keep[:, 0], kind="stable")])
     np.testing.assert_array_equal(host(gJ), oracle.join(sorted_np[0], sorted_np[1]))
+
+
+# ---- T = UINT64 / DOUBLE (common.h:3-9) ------------------
+def typed_table(rng, n, cols, kind, key_col):
+    if kind == "wide":      # full 64-bit patterns: half of them are >= 2^63 as uint64
+        t = rng.integers(I64.min, I64.max, size=(n, cols), dtype=np.int64, endpoint=True)
+    elif kind == "atoi":    # atoi-range values, negatives wrap to huge unsigned keys
+        t = rng.integers(-1000, 1000, size=(n, cols)).astype(np.int64)
+    elif kind == "double":
+        t = np.round(rng.normal(0, 1e7, size=(n, cols)), 1)
+        t[rng.random(n) < 0.05, key_col] = -0.0
+        t[rng.random(n) < 0.05, key_col] = 0.0
+    elif kind == "double_dups":
+        vals = np.array([-2.5, -0.0, 0.0, 1.0, 3.25, -1e300, 1e300, 5e-324])
+        t = vals[rng.integers(0, len(vals), size=(n, cols))]
+    else:
+        raise ValueError(kind)
+    if cols > 1:
+        t[:, (key_col + 1) % cols] = np.arange(n)  # payload = row id: stability is visible
+    return t
+
+
+TYPED_CASES = [
+    # key_type, nr, ns, c1, c2, key1, key2, kind, select1, select2
+    (1, 200_000, 150_000, 2, 2, 0, 0, "wide", (0, (1 << 63) + 5), None),
+    (1, 50_000, 60_000, 3, 2, 1, 0, "atoi", (2, 100), (1, 5)),
+    (1, 40_000, 40_000, 2, 3, 0, 2, "atoi", None, (1, (1 << 64) - 500)),
+    (2, 200_000, 200_000, 2, 2, 0, 0, "double", (0, -1e6), (0, 0.0)),
+    (2, 30_000, 40_000, 4, 3, 2, 1, "double_dups", (0, 0.5), None),
+    (2, 25_000, 25_000, 3, 3, 1, 2, "double_dups", (1, -0.0), (0, -3.0)),
+]
+
+
+def _pos_zero(a, cols):
+    """-0.0 -> +0.0 in the given columns (the pipeline's documented folding)."""
+    a = a.copy()
+    for c in cols:
+        a[:, c] = np.where(a[:, c] == 0.0, 0.0, a[:, c])
+    return a
+
+
+@pytest.mark.parametrize("kt,nr,ns,c1,c2,k1,k2,kind,s1,s2", TYPED_CASES)
+def test_typed_pipeline_matches_oracle(gpu, oracle_built, kt, nr, ns, c1, c2, k1, k2, kind, s1, s2):
+    """T = uint64 / double: keys and select values compare as T (the
+    restatement compiled with that T is the oracle; its UINT64 build is pinned
+    to the reference in tests/test_oracle.py), bit-exact outputs."""
+    from smj import ops
+    rng = np.random.default_rng(nr + kt)
+    R = typed_table(rng, nr, c1, kind, k1)
+    S = typed_table(rng, ns, c2, kind, k2)
+    S[: ns // 2, k2] = R[rng.integers(0, nr, size=ns // 2), k1]  # shared keys: the join is not empty
+    tdev = (lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda())
+    gR, gS, gJ = ops.sort_merge_join(tdev(R), tdev(S), k1, k2, s1, s2, key_type=kt)
+    Rs = oracle.select_sort_t(R, kt, k1, *(s1 or (0, None)))
+    Ss = oracle.select_sort_t(S, kt, k2, *(s2 or (0, None)))
+    J = oracle.join_t(Rs, Ss, kt, k1, k2)
+    if kt == 2:  # folded columns: keys and select columns
+        cR = {k1} | ({s1[0]} if s1 else set())
+        cS = {k2} | ({s2[0]} if s2 else set())
+        cJ = cR | {c1 + (c if c < k2 else c - 1) for c in cS if c != k2}
+        Rs, Ss, J = _pos_zero(Rs, cR), _pos_zero(Ss, cS), _pos_zero(J, cJ)
+    bits = (lambda a: np.ascontiguousarray(a).view(np.int64))
+    np.testing.assert_array_equal(bits(host(gR)), bits(Rs))
+    np.testing.assert_array_equal(bits(host(gS)), bits(Ss))
+    assert len(J) > 0
+    np.testing.assert_array_equal(bits(host(gJ)), bits(J))

@@ -261,3 +261,21 @@ def test_baseline_size_parity(gpu, oracle_built, n, kind):
     Rs, Ss = (dev(a) for a in sorted_np)
     J = host(ops.join(Rs, Ss))
     np.testing.assert_array_equal(J, oracle.join(sorted_np[0], sorted_np[1]))
+
+
+@pytest.mark.parametrize("binary,ktype", [("smj_app_u64", 1), ("smj_app_f64", 2)])
+@pytest.mark.parametrize("case", ["test_10k", "atoi_edge", "neg_wide", "dup_heavy_sel"])
+def test_smj_app_typed_result_csv(gpu, oracle_built, manifest, golden_dir, tmp_path, binary, ktype, case):
+    """The app.c drop-in built with common.h T = uint64_t / double: result.csv
+    byte-identical to cpu_app.c's pipeline restated with the same T (atoi
+    values converted to T, '%ld' of (long) T on output; the reference's own
+    '%ld' of a double is undefined behaviour, the restatement's cast is the
+    contract)."""
+    e = manifest["cases"][case]
+    sel, keys = case_config(e, manifest["user_h_defaults"])
+    out, ref = str(tmp_path / "result.csv"), str(tmp_path / "ref.csv")
+    ins = [fixture_path(golden_dir, f) for f in e["inputs"]]
+    cmd = [os.path.join(PKG, "bin", binary), *ins, "-o", out, "--select", *map(str, sel), "--keys", *map(str, keys)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+    oracle.pipeline_csv(ins[0], ins[1], ref, sel, keys, ktype=ktype)
+    assert sha(out) == sha(ref), case
