@@ -84,10 +84,12 @@ def main():
                 "J": torch.empty((n, 3), dtype=torch.int64, device=dev)}
     torch.cuda.synchronize()
 
+    lb = {}
+
     def step():
         if world == 1:
             return step_single(R, S, bufs)
-        return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS)
+        return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS, stats=lb)
 
     for _ in range(a.warmup):
         step()
@@ -169,7 +171,8 @@ def main():
             "config": {"workload": "C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, "
                                    "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
                        "rows_per_table_per_gpu": n, "rows_per_table_total": total, "key_range": key_range,
-                       "joined_rows": joined, "parallelism": f"range-partition x{world}"},
+                       "joined_rows": joined, "parallelism": f"range-partition x{world}",
+                       "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4)},
             "roofline": roof,
             "pipeline_roofline": {"alg_bytes_per_step": b_alg, "achieved": round(pipe_gbs, 1),
                                   "peak": HBM_PEAK_GBS * world, "unit": "GB/s",

@@ -7,12 +7,18 @@ with host binary searches (app.c:585-633).  Here every rank starts with a
 contiguous slice of R and of S (rank order = input order) and:
 
   1. splitters: every rank samples keys of its slices, one all_gather, and
-     the same W-1 key splitters are chosen everywhere (key-only splitters:
-     one key never spans two ranks);
-  2. per table: a stable select + bucket scatter (one onesweep pass with the
-     bucket as the digit), an all_to_all of the W bucket counts and one
-     all_to_all_single of the rows -- received chunks land in SOURCE-RANK
-     order, so equal keys keep their global input order;
+     the same W-1 sample quantiles are chosen everywhere; each distinct
+     splitter key u gets a single-key bucket (u-1, u] between the open
+     ranges (SURVEY 8(f) rank 4: a heavy key is a bucket of its own);
+  2. per table: a stable select + bucket scatter (one pass with the bucket as
+     the digit); one all_gather of every rank's bucket counts; the same W-1
+     cuts are computed everywhere over the bucket-ordered sequence (R + S
+     rows balanced per rank): at a bucket edge, or inside a single-key
+     bucket at an OCCURRENCE index -- the same index for R and S, so the
+     zip join's pairs (occurrence i of R with occurrence i of S) stay on one
+     rank; each rank then sends contiguous slices of its bucket-ordered rows
+     in one all_to_all_single -- received chunks land in SOURCE-RANK order,
+     so equal keys keep their global input order;
   3. the fused local pipeline (smj_dev_sort_merge_join: MSD sample sort of
      the received R and S slices + zip join) with no select -- the partition
      step already applied the WHERE clause.
@@ -27,7 +33,9 @@ import torch.distributed as dist
 
 from . import ops as hip_ops
 
+INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
+MAX_BOUNDS = 15  # smj_dev_partition_*: <= 16 buckets
 
 
 class HipOps:
@@ -78,6 +86,83 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096):
     return keys[pos].contiguous().to(home)
 
 
+def bucket_bounds(spl):
+    """Boundaries s for the partition kernels' bucket(k) = #{s < k}: every
+    distinct splitter key u gets the single-key bucket (u-1, u].  Returns (s,
+    single) with single[b] true when bucket b holds exactly one key value."""
+    s = []
+    for u in sorted(set(int(x) for x in spl.tolist())):
+        if u > INT64_MIN and (not s or s[-1] < u - 1):
+            s.append(u - 1)
+        s.append(u)
+    if len(s) > MAX_BOUNDS:  # too many ranks for single-key buckets: key-only splitters
+        s = sorted(set(int(x) for x in spl.tolist()))
+    single = [(b == 0 and bool(s) and s[0] == INT64_MIN) or (0 < b < len(s) and s[b] - s[b - 1] == 1)
+              for b in range(len(s) + 1)]
+    return s, single
+
+
+def choose_cuts(GR, GS, single, world):
+    """W-1 cuts (bucket, occurrence) over the global bucket-ordered sequence,
+    balancing R + S rows per rank: rows of buckets < b go left, and of bucket
+    b the occurrences < o (o = 0 unless b is a single-key bucket).  The same
+    o applies to R and S.  Identical on every rank (pure function of the
+    gathered counts)."""
+    nb = len(GR)
+    tot = [GR[b] + GS[b] for b in range(nb)]
+    total = sum(tot)
+    cuts, acc, b, prev = [], 0, 0, (0, 0)
+    for d in range(1, world):
+        target = total * d / world
+        while b < nb and acc + tot[b] <= target:
+            acc += tot[b]
+            b += 1
+        if b == nb:
+            cut = (nb, 0)
+        elif single[b]:
+            need = target - acc  # smallest o with min(o, GR) + min(o, GS) >= need, or o - 1 if closer
+            lo, hi = 0, max(GR[b], GS[b])
+            while lo < hi:
+                mid = (lo + hi) // 2
+                if min(mid, GR[b]) + min(mid, GS[b]) >= need:
+                    hi = mid
+                else:
+                    lo = mid + 1
+            left = min(lo, GR[b]) + min(lo, GS[b])
+            if lo > 0 and need - (min(lo - 1, GR[b]) + min(lo - 1, GS[b])) < left - need:
+                lo -= 1
+            cut = (b, lo)
+        else:  # a multi-key bucket moves whole: the nearer edge
+            cut = (b, 0) if target - acc <= acc + tot[b] - target else (b + 1, 0)
+        cut = max(cut, prev)
+        cuts.append(cut)
+        prev = cut
+    return cuts
+
+
+def slice_counts(local, prefix, cuts, nb):
+    """Rows of this rank's bucket-ordered buffer per destination rank: cut
+    (b, o) sits after the local buckets < b and, of bucket b, the local rows
+    whose global occurrence (prefix[b] = rows of bucket b on earlier ranks +
+    local offset) is below o."""
+    def pos(cut):
+        b, o = cut
+        p = sum(local[:b])
+        if b < nb:
+            p += min(max(o - prefix[b], 0), local[b])
+        return p
+    edges = [0] + [pos(c) for c in cuts] + [sum(local)]
+    return [edges[d + 1] - edges[d] for d in range(len(edges) - 1)]
+
+
+def gather_counts(counts, world, group=None, device=None):
+    """all_gather of this rank's integer vector; returns a world x len list."""
+    t = torch.tensor(counts, dtype=torch.int64, device=device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    return [[int(v) for v in o.tolist()] for o in out]
+
+
 def exchange_rows(send, counts, group=None):
     """all_to_all_single of bucket-contiguous rows; returns rows received in
     source-rank order."""
@@ -90,15 +175,18 @@ def exchange_rows(send, counts, group=None):
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     rc = [int(x) for x in recv_counts.tolist()]
     recv = torch.empty((sum(rc), send.shape[1]), dtype=send.dtype, device=dev)
-    dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rc, input_split_sizes=list(counts),
+    dist.all_to_all_single(recv, send[: sum(counts)].contiguous(), output_split_sizes=rc,
+                           input_split_sizes=list(counts),
                            group=group)
     return recv.to(home)
 
 
 def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, ops=None, samples=4096,
-                    timings=None):
+                    stats=None):
     """The distributed pipeline; returns this rank's slice of the result (the
-    global result is the concatenation over ranks in rank order)."""
+    global result is the concatenation over ranks in rank order).  stats
+    (optional dict) gets the rows this rank received per table and the
+    max / mean load over ranks (load-balance report)."""
     ops = ops or HipOps
     sc1, sv1, sc2, sv2 = select
     k1, k2 = keys
@@ -108,10 +196,26 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
         return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
 
     spl = choose_splitters([(R, k1), (S, k2)], world, group, samples)
-    local = []
+    bounds, single = bucket_bounds(spl)
+    bt = torch.tensor(bounds, dtype=torch.int64, device=R.device)
+    nb = len(bounds) + 1
+    counts, sends = [], []
     for T, key, sc, sv in ((R, k1, sc1, sv1), (S, k2, sc2, sv2)):
-        counts, _ = ops.partition_count(T, spl, key, sc, sv)
-        send = ops.partition_scatter(T, spl, counts, key, sc, sv)
-        local.append(exchange_rows(send, counts, group))
-        del send
+        c, _ = ops.partition_count(T, bt, key, sc, sv)
+        counts.append(c)
+        sends.append(ops.partition_scatter(T, bt, c, key, sc, sv))
+    allc = gather_counts(counts[0] + counts[1], world, group, _wire_device(R, group))
+    G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
+    cuts = choose_cuts(G[0], G[1], single, world)
+    local = []
+    for t in range(2):
+        prefix = [sum(allc[r][t * nb + b] for r in range(rank)) for b in range(nb)]
+        local.append(exchange_rows(sends[t], slice_counts(counts[t], prefix, cuts, nb), group))
+    del sends
+    if stats is not None:
+        rows = [int(local[0].shape[0]), int(local[1].shape[0])]
+        loads = gather_counts([rows[0] + rows[1]], world, group, _wire_device(R, group))
+        mean = sum(l[0] for l in loads) / world
+        stats.update(rows_in=rows, load_max_over_mean=(max(l[0] for l in loads) / mean) if mean else 1.0,
+                     cuts=cuts, buckets=nb)
     return ops.sort_merge_join(local[0], local[1], k1, k2, None, None)[2]

@@ -86,8 +86,12 @@ def _worker(rank, world, port, R, S, cfg, outdir):
     if cfg.get("gpu"):  # the product operators (HipOps) on cuda:0, exchange staged through gloo
         torch.cuda.set_device(0)
         r, s, ops = r.cuda(), s.cuda(), None
-    out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=ops, samples=cfg["samples"])
+    stats = {}
+    out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=ops, samples=cfg["samples"],
+                                stats=stats)
     np.save(os.path.join(outdir, f"rank{rank}.npy"), out.cpu().numpy())
+    if rank == 0:
+        np.save(os.path.join(outdir, "load.npy"), np.array([stats["load_max_over_mean"]]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -134,6 +138,32 @@ def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, ki
     _run_and_check(tmp_path, 2, kind, cfg, 400_000)
 
 
+def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):
+    """with 60 % of R and 50 % of S on one key, key-only
+    splitters would put that key on one rank; (key, occurrence) cuts spread
+    its occurrences (the same cut for R and S keeps the zip pairs together)
+    and the rank loads stay within 10 % of the mean."""
+    load = _run_and_check(tmp_path, 4, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 64},
+                          40_000)
+    assert load < 1.10, load
+
+
+def test_choose_cuts_pure():
+    from smj import dist as sdist
+    s, single = sdist.bucket_bounds(torch.tensor([5, 17, 17, 17, 40]))
+    assert s == [4, 5, 16, 17, 39, 40] and single == [False, True, False, True, False, True, False]
+    # bucket 3 (key 17) holds 60 of 100 R rows and 30 of 60 S rows
+    GR, GS = [10, 0, 10, 60, 10, 0, 10], [5, 0, 5, 30, 10, 0, 10]
+    cuts = sdist.choose_cuts(GR, GS, single, 4)
+    assert cuts[0][0] == 3 and cuts[1][0] == 3 and cuts == sorted(cuts)
+    # every rank's share of R + S = 160 rows is within one occurrence pair of 40
+    edges = [0]
+    for b, o in cuts:
+        edges.append(sum(GR[:b]) + sum(GS[:b]) + (min(o, GR[b]) + min(o, GS[b]) if b < len(GR) else 0))
+    edges.append(160)
+    assert all(abs((edges[i + 1] - edges[i]) - 40) <= 2 for i in range(4)), edges
+
+
 def _run_and_check(tmp_path, world, kind, cfg, n):
     R, S = make_tables(kind, n)
     mp.spawn(_worker, args=(world, free_port(), R, S, cfg, str(tmp_path)), nprocs=world, join=True)
@@ -143,3 +173,4 @@ def _run_and_check(tmp_path, world, kind, cfg, n):
     ref = oracle.join(oracle.select_sort(R, k1, sc1, sv1), oracle.select_sort(S, k2, sc2, sv2), k1, k2)
     assert len(ref) > 0
     np.testing.assert_array_equal(got, ref)
+    return float(np.load(tmp_path / "load.npy")[0])
