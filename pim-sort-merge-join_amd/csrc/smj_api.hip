@@ -453,6 +453,7 @@ struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
 };
 PbLast g_pb_last[2];
 int g_pb_ntab = 0;
+MsdFinalParams g_fin_last{};  // last pipeline call's final launch (smj_debug_final_time)
 
 int msd_scratch(MsdScratch **out) {
     int dev = 0;
@@ -683,6 +684,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.ntab = ntab;
     fp.join = join;
     fp.key2 = key2;
+    g_fin_last = fp;
     size_t pf;
     {
         ProfScope ps("msd_final", 0, s);
@@ -756,6 +758,29 @@ extern "C" int smj_debug_part_b_time(int dbg, int reps, float *ms) {
             p.dbg = dbg;
             HIP_TRY(launch_msd_part_b(p, g_pb_last[x].cols, g_pb_last[x].maxB, 0));
         }
+    HIP_TRY(hipEventRecord(b, 0));
+    HIP_TRY(hipEventSynchronize(b));
+    HIP_TRY(hipEventElapsedTime(ms, a, b));
+    *ms /= (float)reps;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return SMJ_OK;
+}
+
+// Diagnostic only (not part of smj.h): re-run the last pipeline call's final
+// launches `reps` times with ablation bits `dbg` (smj_msd.hip launch_msd_final)
+// and return the average ms.  Rewrites the same outputs.
+extern "C" int smj_debug_final_time(int dbg, int reps, float *ms) {
+    if (!g_fin_last.groups || reps <= 0 || !ms) return SMJ_ERR_INVALID;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventRecord(a, 0));
+    for (int r = 0; r < reps; r++) {
+        MsdFinalParams p = g_fin_last;
+        p.dbg = dbg;
+        HIP_TRY(launch_msd_final(p, 0));
+    }
     HIP_TRY(hipEventRecord(b, 0));
     HIP_TRY(hipEventSynchronize(b));
     HIP_TRY(hipEventElapsedTime(ms, a, b));

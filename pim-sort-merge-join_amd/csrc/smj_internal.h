@@ -164,7 +164,7 @@ constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgro
 constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
 constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
-constexpr int kMsdSegs = 64;               // segments of the run scans
+constexpr int kMsdSegs = 256;              // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
 constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
 

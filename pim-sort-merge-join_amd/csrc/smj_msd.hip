@@ -36,6 +36,12 @@
 #include "smj_internal.h"
 #include "smj_device.h"
 
+// Phase stamps (tools/msd_phases.py) are compiled in only with -DSMJ_STAMPS=1
+// (they hold registers); at run time they also need SMJ_DEBUG_MSD=1.
+#ifndef SMJ_STAMPS
+#define SMJ_STAMPS 0
+#endif
+
 #include <stdlib.h>
 
 #include <algorithm>
@@ -184,13 +190,37 @@ __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
 // ---------------------------------------------------------------------------
 // sample -> splitters
 // ---------------------------------------------------------------------------
+// bitonic compare-exchange step of distance J (< E: both elements in this
+// thread's registers) for sequence size k; element e of thread t is t*E + e
+template <int E, int J>
+__device__ __forceinline__ void bitonic_regs(int64_t (&v)[E], int tid, int k) {
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if ((e & J) == 0) {
+            const bool up = (((tid * E + e) & k) == 0);
+            const int64_t a = v[e], b = v[e | J];
+            if ((a > b) == up) {
+                v[e] = b;
+                v[e | J] = a;
+            }
+        }
+}
+
 __global__ __launch_bounds__(1024) void msd_sample_kernel(const MsdSampleParams p) {
-    constexpr int N = 2 * kSampleMax;  // 16 Ki keys = 128 KiB of LDS
+    // bitonic sort of 2 x kSampleMax keys, E per thread in registers: steps
+    // with the partner in the same thread use registers, in the same wave
+    // __shfl_xor, and only those across waves (distance >= 64 E) go through
+    // LDS with barriers (10 of the 91 steps)
+    constexpr int N = 2 * kSampleMax, E = N / 1024;
+    static_assert(E == 8, "8 keys per thread");
     __shared__ int64_t s_key[N];
     __shared__ uint32_t s_wsum[16];
     const int tid = threadIdx.x;
     uint32_t valid = 0;
-    for (int j = tid; j < N; j += 1024) {
+    int64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int j = tid * E + e;
         int64_t k = INT64_MAX;
         const int x = j >= kSampleMax ? 1 : 0;
         const int jj = j - x * kSampleMax;
@@ -206,14 +236,14 @@ __global__ __launch_bounds__(1024) void msd_sample_kernel(const MsdSampleParams 
                 }
             }
         }
-        s_key[j] = k;
+        v[e] = k;
     }
     // valid sample count
     {
-        uint32_t v = valid;
+        uint32_t c = valid;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((tid & 63) == 0) s_wsum[tid >> 6] = v;
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((tid & 63) == 0) s_wsum[tid >> 6] = c;
     }
     __syncthreads();
     uint32_t M = 0;
@@ -221,20 +251,36 @@ __global__ __launch_bounds__(1024) void msd_sample_kernel(const MsdSampleParams 
     for (int w = 0; w < 16; w++) M += s_wsum[w];
     // bitonic sort ascending (invalid samples are INT64_MAX: they sort behind every valid key)
     for (int k = 2; k <= N; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = tid; q < N / 2; q += 1024) {
-                const int i = (q / j) * 2 * j + (q % j);
-                const int l = i + j;
-                const int64_t a = s_key[i], b = s_key[l];
-                const bool up = (i & k) == 0;
-                if ((a > b) == up) {
-                    s_key[i] = b;
-                    s_key[l] = a;
+        for (int j = k >> 1; j >= E; j >>= 1) {
+            const int m = j / E;  // partner thread tid ^ m
+            const bool lower = (tid & m) == 0;
+            if (m >= 64) {
+#pragma unroll
+                for (int e = 0; e < E; e++) s_key[tid * E + e] = v[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int64_t o = s_key[(tid ^ m) * E + e];
+                    const bool up = (((tid * E + e) & k) == 0);
+                    v[e] = (lower == up) ? min(v[e], o) : max(v[e], o);
+                }
+                __syncthreads();
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int64_t o = (int64_t)__shfl_xor((long long)v[e], m, 64);
+                    const bool up = (((tid * E + e) & k) == 0);
+                    v[e] = (lower == up) ? min(v[e], o) : max(v[e], o);
                 }
             }
-            __syncthreads();
         }
+        if (k >= 8) bitonic_regs<E, 4>(v, tid, k);
+        if (k >= 4) bitonic_regs<E, 2>(v, tid, k);
+        bitonic_regs<E, 1>(v, tid, k);
     }
+#pragma unroll
+    for (int e = 0; e < E; e++) s_key[tid * E + e] = v[e];
+    __syncthreads();
     if (tid < kSplA) {
         int64_t s = INT64_MAX;
         if (M > 0) {
@@ -386,10 +432,11 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
     const int a = threadIdx.x, lane = a & 63, wave = a >> 6;
     // global min / max of the selected keys over both tables
     int64_t mn = INT64_MAX, mx = INT64_MIN;
-    for (int x = 0; x < p.ntab; x++) {  // per (segment, wave) partials of msd_runs_seg_kernel
-        mn = min(mn, p.segmm[x][2 * a]);
-        mx = max(mx, p.segmm[x][2 * a + 1]);
-    }
+    for (int x = 0; x < p.ntab; x++)  // per (segment, wave) partials of msd_runs_seg_kernel
+        for (int i = a; i < kMsdSegs * 4; i += 256) {
+            mn = min(mn, p.segmm[x][2 * i]);
+            mx = max(mx, p.segmm[x][2 * i + 1]);
+        }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
@@ -552,7 +599,7 @@ __device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a)
 // 64 = 40 KiB of padding LDS (one workgroup per CU)
 __device__ unsigned long long g_pb_phase[8];
 #define PB_STAMP(k)                                                 \
-    if ((p.dbg & 1) && tid == 0) {                                        \
+    if (SMJ_STAMPS && (p.dbg & 1) && tid == 0) {                                        \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
         atomicAdd(&g_pb_phase[k], t_ - pb_t);                       \
         pb_t = t_;                                                  \
@@ -596,7 +643,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
     int64_t g = blockIdx.x;
     if (g >= ntl) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned long long pb_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long pb_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     uint2 ti = uni_tinfo(p.tinfo, g);
     MsdBucket b = uni_bucket(p.bk, ti.x);
     auto runs_of = [&](const uint2 &t, const MsdBucket &bb, int64_t gg) {  // run-list entries of tile gg
@@ -778,7 +825,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
             }
         }
         PB_STAMP(5);
-        if ((p.dbg & 1) && tid == 0) atomicAdd(&g_pb_phase[7], 1ull);
+        if (SMJ_STAMPS && (p.dbg & 1) && tid == 0) atomicAdd(&g_pb_phase[7], 1ull);
         __syncthreads();  // staging region read out before the next tile's list lands in it
         ti = tin;
         b = bn;
@@ -1657,7 +1704,7 @@ __device__ __forceinline__ void fin_out_join(const MsdFinalParams &p, const MsdG
 // s_memtime cycles of thread 0 per phase, summed over workgroups.
 __device__ unsigned long long g_fin_phase[16];
 #define FIN_STAMP(k)                                                \
-    if (p.dbg) {                                                    \
+    if (SMJ_STAMPS && (p.dbg & 1)) {                                                    \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
         ph[k] += t_ - ph_t;                                         \
         ph_t = t_;                                                  \
@@ -1668,7 +1715,7 @@ __device__ unsigned long long g_fin_phase[16];
 template <int C1, int C2>
 __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p) {
     __shared__ FinSmem sm;
-    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     // contiguous mode: workgroup b walks a range of dense groups (pipelined one
     // group deep); list mode: the groups msd_final_stage_kernel handed over
     const bool lm = p.radix_list != nullptr;
@@ -1728,9 +1775,9 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
         have = nfast;
         __syncthreads();  // LDS reused by the next group
         FIN_STAMP(5);
-        if (p.dbg) ph[9]++;
+        if (SMJ_STAMPS && (p.dbg & 1)) ph[9]++;
     }
-    if (p.dbg && threadIdx.x == 0)
+    if (SMJ_STAMPS && (p.dbg & 1) && threadIdx.x == 0)
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
 
@@ -1743,8 +1790,9 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
 // join rows leave through LDS as coalesced stores.  The next group's rows
 // are gathered into registers while this one is sorted and written.  Groups
 // outside its limits (key span > kStageRange, an equal-key run >
-// kMaxDupRun, > kStThreads pass-B tiles) go to the radix list.
-constexpr int kStThreads = 512, kStWaves = kStThreads / 64;
+// kMaxDupRun, > kStList pass-B tiles) go to the radix list.
+constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 2 per CU (1024-thread workgroups: slower, r01z)
+constexpr int kStList = 512;                   // pass-B tiles per bucket and table a staged group may span
 constexpr int kStIt = kGroupCap / kStThreads;  // rows per table per thread
 constexpr int kStRange = kStageRange;
 constexpr int kStRecs = 64;                    // group records per LDS chunk (two chunks in flight)
@@ -1756,7 +1804,7 @@ struct StSmem {
     uint32_t hist[2][kStRange / 2];   // packed u16 bins (zeroed for the next group during the emit)
     union {
         struct {
-            uint2 list[2][kStThreads];             // run lists of the next group: {tempB row, group row}
+            uint2 list[2][kStList];                // run lists of the next group: {tempB row, group row}
             uint16_t at[2][kGroupCap];             // list entry of the non-empty range starting at row v
             uint32_t starts[2][kGroupCap / 32];    // bitmap: a non-empty range starts at row v
             uint16_t btab[2][kGroupCap / 64];      // list entry holding row 64 * b
@@ -1769,8 +1817,8 @@ struct StSmem {
 };
 
 __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g) {
-    return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStThreads &&
-           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStThreads);
+    return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStList &&
+           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList);
 }
 
 __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
@@ -1789,7 +1837,7 @@ __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdG
 
 __device__ unsigned long long g_st_sub[8];
 #define ST_SUB(k)                                                   \
-    if (p.dbg && tid == 0) {                                        \
+    if (SMJ_STAMPS && (p.dbg & 1) && tid == 0) {                    \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
         atomicAdd(&g_st_sub[k], t_ - st_t);                         \
         st_t = t_;                                                  \
@@ -1802,7 +1850,7 @@ __device__ unsigned long long g_st_sub[8];
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    unsigned long long st_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
@@ -1850,7 +1898,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
                                         const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt]) {
     const int tid = threadIdx.x;
-    unsigned long long st_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
     uint32_t w[2][kStIt], rank[2][kStIt];
     if (tid == 0) sm.flag[wsb] = 0;  // longest equal-key run (0: none)
@@ -1918,7 +1966,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // equal residuals were placed in atomic order: odd-even transposition
     // rounds (as many as the longest run) order every run by group row.
     // (Measured: cheaper than ranking each run member by a scan of its run.)
-    static_assert(kGroupCap / 2 == kStThreads, "one compare-exchange per thread per table and round");
+    static_assert(kGroupCap / 2 <= kStThreads, "one compare-exchange per thread per table and round");
     for (uint32_t rd = 0; rd < fl; rd++) {
 #pragma unroll
         for (int x = 0; x < 2; x++) {
@@ -2024,11 +2072,11 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0, int64_t gs, int64_t t0,
                                              int64_t cnt, StSmem &sm, int h) {
     constexpr int WORDS = sizeof(MsdGroup) / 8;
-    static_assert(kStRecs * WORDS == kStThreads, "one record word per thread");
+    static_assert(kStRecs * WORDS <= kStThreads, "at most one record word per thread");
     int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
     const int i = threadIdx.x;
     const int64_t t = t0 + i / WORDS;
-    if (t < cnt) dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
+    if (i < kStRecs * WORDS && t < cnt) dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
 }
 
 // persistent staged kernel.  XCD-aware schedule: the dense (key-ordered)
@@ -2039,7 +2087,7 @@ __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0
 // neighbours in key order: the pass-B tile lines and offsB lines two
 // neighbouring groups share are fetched into that XCD's L2 once.
 constexpr int kXcdSlots = 8;
-__global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const MsdFinalParams p) {
+__global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
@@ -2047,7 +2095,7 @@ __global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const Ms
     const int64_t x0 = (int64_t)(blockIdx.x % kXcdSlots) * xr, x1 = min(ng, x0 + xr);
     const int64_t g0 = x0 + blockIdx.x / kXcdSlots;  // local group t = dense group g0 + t * gs
     const int64_t cnt = x1 > g0 ? (x1 - g0 + gs - 1) / gs : 0;
-    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = p.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
         for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
@@ -2111,9 +2159,9 @@ __global__ __launch_bounds__(kStThreads, 2) void msd_final_stage_kernel(const Ms
         have = nfit;
         __syncthreads();
         FIN_STAMP(5);
-        if (p.dbg) ph[9]++;
+        if (SMJ_STAMPS && (p.dbg & 1)) ph[9]++;
     }
-    if (p.dbg && threadIdx.x == 0)
+    if (SMJ_STAMPS && (p.dbg & 1) && threadIdx.x == 0)
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
 
@@ -2233,22 +2281,37 @@ __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restr
 // 16 Ki staged through LDS); plan->joined = total
 __global__ __launch_bounds__(1024) void msd_count_scan_kernel(const uint32_t *__restrict__ counts,
                                                               uint32_t *__restrict__ offs, MsdPlan *plan) {
+    // one workgroup; thread t owns 16 consecutive counts of a 16 Ki round,
+    // loaded / stored as 4 x 16 B, the next round's loads in flight during
+    // this round's scan
     constexpr int PER = 16, ROUND = 1024 * PER;
-    __shared__ uint32_t s_c[ROUND];
     __shared__ uint32_t s_w[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t ng = plan->ngroups;
-    uint32_t carry = 0;
-    for (int64_t base = 0; base < ng; base += ROUND) {
-        const int64_t n = min((int64_t)ROUND, ng - base);
-        for (int i = tid; i < ROUND; i += 1024) s_c[i] = i < n ? counts[base + i] : 0u;
-        __syncthreads();
-        uint32_t v[PER], sum = 0;
+    auto load = [&](int64_t base, uint32_t (&v)[PER]) {
+        const int64_t i0 = base + (int64_t)tid * PER;
+        if (i0 + PER <= ng) {
+            const uint4 *c4 = reinterpret_cast<const uint4 *>(counts + i0);
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            v[k] = s_c[tid * PER + k];
-            sum += v[k];
+            for (int q = 0; q < PER / 4; q++) {
+                const uint4 u = c4[q];
+                v[4 * q] = u.x;
+                v[4 * q + 1] = u.y;
+                v[4 * q + 2] = u.z;
+                v[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; k++) v[k] = i0 + k < ng ? counts[i0 + k] : 0u;
         }
+    };
+    uint32_t carry = 0, v[PER], nx[PER];
+    if (ng > 0) load(0, v);
+    for (int64_t base = 0; base < ng; base += ROUND) {
+        if (base + ROUND < ng) load(base + ROUND, nx);
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) sum += v[k];
         const uint32_t incl = wave_incl_scan(sum, lane);
         if (lane == 63) s_w[wave] = incl;
         __syncthreads();
@@ -2258,15 +2321,26 @@ __global__ __launch_bounds__(1024) void msd_count_scan_kernel(const uint32_t *__
             run += (w < wave) ? s_w[w] : 0u;
             all += s_w[w];
         }
+        __syncthreads();  // s_w reused next round
+        const int64_t i0 = base + (int64_t)tid * PER;
+        uint32_t o[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            s_c[tid * PER + k] = run;
+            o[k] = run;
             run += v[k];
         }
-        __syncthreads();
-        for (int i = tid; i < n; i += 1024) offs[base + i] = s_c[i];
+        if (i0 + PER <= ng) {
+            uint4 *o4 = reinterpret_cast<uint4 *>(offs + i0);
+#pragma unroll
+            for (int q = 0; q < PER / 4; q++) o4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; k++)
+                if (i0 + k < ng) offs[i0 + k] = o[k];
+        }
         carry += all;
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; k++) v[k] = nx[k];
     }
     if (tid == 0) plan->joined = (int64_t)carry;
 }
@@ -2349,11 +2423,13 @@ hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
 hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
     MsdFinalParams p = p_in;
-    p.dbg = dbg;
+    p.dbg = p_in.dbg ? p_in.dbg : dbg;  // explicit bits (smj_debug_final_time) or SMJ_DEBUG_MSD
+    const size_t pad = (p.dbg & 64) ? 40960 : 0;  // ablation: dynamic LDS pad -> 1 workgroup per CU
     const bool two = p.tab[0].cols == 2 && (p.ntab == 1 || p.tab[1].cols == 2);
     if (two) {
         static_assert(kMsdStageGrid % kXcdSlots == 0, "whole XCD sets");
-        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(kMsdStageGrid), dim3(kStThreads), 0, s, p);
+        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(pad ? kMsdStageGrid / 2 : kMsdStageGrid), dim3(kStThreads),
+                           pad, s, p);
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
         q.radix_list = nullptr;

@@ -30,6 +30,7 @@ for s in $STEPS; do
     quick) run quick 300 python bench.py --cpu-sample 0 ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
+    finab) run finab 300 python tools/final_ablate.py ;;
     h2d)   run h2d 300 python tools/h2d_probe.py ;;
     typed) run typed 600 python -u -m pytest tests -m gpu -x -q -k "typed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     prof)  export TMPDIR=/tmp
