@@ -871,14 +871,19 @@ __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams
 }
 
 constexpr int kGroupThreads = 1024;
+constexpr int kGroupLevels = 11;  // 2^11 = kRadB: binary-lifting levels over the group starts
+static_assert((1 << kGroupLevels) == kRadB, "one level per bit of a group index");
 __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroupParams p) {
     constexpr int NW = kGroupThreads / 64, SB = kRadB / kGroupThreads;
-    __shared__ uint32_t s_tot[2][kRadB];
-    __shared__ uint32_t s_pre[2][kRadB];
+    __shared__ uint32_t s_P[2][kRadB + 1];          // row prefix over sub-buckets, per table (P[kRadB] = total)
+    __shared__ uint16_t s_lift[kGroupLevels][kRadB + 1];  // f^(2^k): next group start after a start
+    __shared__ uint16_t s_nz[kRadB + 1];            // positions of the non-empty sub-buckets, in order
+    __shared__ uint16_t s_cnz[kRadB + 1];           // non-empty sub-buckets before position q
     __shared__ uint32_t s_wsum[NW];
-    __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];  // groups: sub-buckets [b0, b1)
+    __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];   // groups: sub-buckets [b0, b1)
     __shared__ int s_ng;
     const int a = blockIdx.x, t = threadIdx.x;
+    uint32_t nzmask = 0;  // thread t's sub-buckets [t*SB, t*SB + SB) that hold rows
     for (int x = 0; x < 2; x++) {
         uint32_t tot[SB];
 #pragma unroll
@@ -892,14 +897,31 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         }
         uint32_t sum = 0;
 #pragma unroll
-        for (int i = 0; i < SB; i++) sum += tot[i];
+        for (int i = 0; i < SB; i++) {
+            sum += tot[i];
+            nzmask |= tot[i] ? 1u << i : 0u;
+        }
         uint32_t all;
         uint32_t ex = block_excl_scan<NW>(sum, s_wsum, &all);
 #pragma unroll
         for (int i = 0; i < SB; i++) {
-            s_tot[x][t * SB + i] = tot[i];
-            s_pre[x][t * SB + i] = ex;
+            s_P[x][t * SB + i] = ex;
             ex += tot[i];
+        }
+        if (t == 0) s_P[x][kRadB] = all;
+    }
+    // compact list of the non-empty sub-buckets
+    {
+        uint32_t all;
+        uint32_t c = block_excl_scan<NW>((uint32_t)__popc(nzmask), s_wsum, &all);
+#pragma unroll
+        for (int i = 0; i < SB; i++) {
+            s_cnz[t * SB + i] = (uint16_t)c;
+            if ((nzmask >> i) & 1u) s_nz[c++] = (uint16_t)(t * SB + i);
+        }
+        if (t == 0) {
+            s_cnz[kRadB] = (uint16_t)all;
+            s_nz[all] = (uint16_t)kRadB;  // sentinel: "no further non-empty sub-bucket"
         }
     }
     __syncthreads();
@@ -907,45 +929,64 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
-    if (t < 64) {  // greedy packing by wave 0 (counts in registers, one lane at a time);
-                   // a group that is over the cap holds exactly one sub-bucket
-        int ng = 0, b0 = -1, last = -1;
-        uint32_t cr = 0, cs = 0;
-        for (int c = 0; c < kRadB; c += 64) {
-            const uint32_t rv = s_tot[0][c + t], sv = s_tot[1][c + t];
-            uint64_t nz = __ballot((rv | sv) != 0u);
-            while (nz) {
-                const int l = __ffsll((unsigned long long)nz) - 1;
-                nz &= nz - 1;
-                const int j = c + l;
-                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rv, l);
-                const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)sv, l);
-                if (b0 >= 0 && (cr + r > (uint32_t)kGroupCap || cs + s > (uint32_t)kGroupCap || j - b0 >= maxspan)) {
-                    if (t == 0) {
-                        s_g0[ng] = (uint16_t)b0;
-                        s_g1[ng] = (uint16_t)(last + 1);
-                    }
-                    ng++;
-                    b0 = -1;
-                    cr = cs = 0;
+    // The greedy packing (a group takes consecutive non-empty sub-buckets while
+    // both tables stay <= kGroupCap rows and the sub-bucket span < maxspan; a
+    // sub-bucket over the cap is a group of its own), computed in parallel:
+    // from a group start i the next start is f(i) = the first non-empty j > i
+    // at which the R or S rows of [i, j] exceed the cap or j - i >= maxspan.
+    // The starts are the orbit of the first non-empty sub-bucket under f;
+    // binary lifting (f^(2^k)) gives start number s to every thread at once.
+    auto next_nz = [&](int q) -> int { return q >= kRadB ? kRadB : (int)s_nz[s_cnz[q]]; };
+    for (int i = t; i <= kRadB; i += kGroupThreads) {
+        int f = kRadB;
+        if (i < kRadB) {
+            int lim = min(kRadB, i + maxspan);
+#pragma unroll
+            for (int x = 0; x < 2; x++) {  // first m in [i + 2, kRadB] with P[m] - P[i] > cap: j = m - 1
+                const uint32_t cap = s_P[x][i] + (uint32_t)kGroupCap;
+                int lo = i + 2, hi = kRadB + 1;  // answer in [lo, hi); hi = none
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_P[x][mid] > cap) hi = mid; else lo = mid + 1;
                 }
-                if (b0 < 0) b0 = j;
-                cr += r;
-                cs += s;
-                last = j;
+                if (lo <= kRadB) lim = min(lim, lo - 1);
+                else if (i + 1 <= kRadB && s_P[x][i + 1] > cap) lim = min(lim, i + 1);
             }
+            f = next_nz(max(lim, i + 1));
         }
-        if (b0 >= 0) {
-            if (t == 0) {
-                s_g0[ng] = (uint16_t)b0;
-                s_g1[ng] = (uint16_t)(last + 1);
-            }
-            ng++;
+        s_lift[0][i] = (uint16_t)f;
+    }
+    __syncthreads();
+    for (int k = 1; k < kGroupLevels; k++) {
+        for (int i = t; i <= kRadB; i += kGroupThreads) s_lift[k][i] = s_lift[k - 1][s_lift[k - 1][i]];
+        __syncthreads();
+    }
+    const int s0 = next_nz(0);
+    int ng_local = 0;
+    for (int sidx = t; sidx < kRadB; sidx += kGroupThreads) {
+        int pos = s0;
+#pragma unroll
+        for (int k = 0; k < kGroupLevels; k++)
+            if ((sidx >> k) & 1) pos = s_lift[k][pos];
+        if (pos < kRadB) {
+            const int nxt = s_lift[0][pos];
+            s_g0[sidx] = (uint16_t)pos;
+            s_g1[sidx] = (uint16_t)(s_nz[s_cnz[nxt] - 1] + 1);  // after the last non-empty sub-bucket before nxt
+            ng_local = max(ng_local, sidx + 1);
         }
-        if (t == 0) {
-            s_ng = ng;
-            p.ngrp[a] = (uint32_t)ng;
-        }
+    }
+    {
+        int m = ng_local;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if ((t & 63) == 0) s_wsum[t >> 6] = (uint32_t)m;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int ng = 0;
+        for (int w = 0; w < NW; w++) ng = max(ng, (int)s_wsum[w]);
+        s_ng = ng;
+        p.ngrp[a] = (uint32_t)ng;
     }
     __syncthreads();
     for (int j = t; j < s_ng; j += kGroupThreads) {
@@ -954,10 +995,10 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.a = (uint16_t)a;
         gr.b0 = (uint16_t)b0;
         gr.b1 = (uint16_t)b1;
-        gr.nR = s_pre[0][b1 - 1] + s_tot[0][b1 - 1] - s_pre[0][b0];
-        gr.nS = s_pre[1][b1 - 1] + s_tot[1][b1 - 1] - s_pre[1][b0];
-        gr.outR = p.bk[0][a].row_start + s_pre[0][b0];
-        gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_pre[1][b0] : 0u;
+        gr.nR = s_P[0][b1] - s_P[0][b0];
+        gr.nS = s_P[1][b1] - s_P[1][b0];
+        gr.outR = p.bk[0][a].row_start + s_P[0][b0];
+        gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_P[1][b0] : 0u;
         gr.flags = 0;
         if (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap)
             gr.flags = single_sub ? kGroupSingle : kGroupBig;
