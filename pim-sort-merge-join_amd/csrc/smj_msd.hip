@@ -228,7 +228,13 @@ __global__ __launch_bounds__(1024) void msd_sample_kernel(const MsdSampleParams 
         if (x < p.ntab && t.n > 0) {
             const int64_t ns = min(t.n, (int64_t)kSampleMax);
             if (jj < ns) {
-                const int64_t r = ((2 * (int64_t)jj + 1) * t.n) / (2 * ns);
+                // clusters of kSampleRun consecutive rows spread evenly over the
+                // table: 16x fewer distinct pages (TLB walks) than single rows
+                constexpr int kSampleRun = 16, kClusters = kSampleMax / kSampleRun;
+                const int64_t r = t.n <= kSampleMax
+                                      ? jj
+                                      : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
+                                                         jj % kSampleRun);
                 const int64_t *row = t.src + r * t.cols;
                 if (!t.use_sel || row[t.sel_col] > t.sel_val) {
                     k = row[t.key_col];
