@@ -2189,12 +2189,17 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
         FIN_STAMP(1);
         uint32_t mmask = 0, part[kStIt];
         const bool ok = st_sort(p, g, gi, cur, sm, wsb, mmask, part);  // cur is staged in LDS here
-        __syncthreads();
         FIN_STAMP(2);
-        if (nfit) {  // the next group's rows: in flight while this one is written out
+        // st_issue writes only the list region (unused by the sort) and the
+        // other wsum buffer, and its scan barrier orders the sort's last
+        // histogram reads before st_emit zeroes the histogram; st_emit writes
+        // `match` (aliasing the list) only after its own scan barrier, which
+        // every wave reaches after its st_issue reads.  Without st_issue one
+        // barrier does both.
+        if (nfit)  // the next group's rows: in flight while this one is written out
             st_issue(p, gn, o0, o1, cur, sm, wsb);
-            __syncthreads();  // list dead before the join reuses the region
-        }
+        else
+            __syncthreads();
         FIN_STAMP(3);
         if (ok) {
             st_emit(p, g, gi, sm, wsb, mmask, part);

@@ -216,3 +216,40 @@ def test_typed_pipeline_matches_oracle(gpu, oracle_built, kt, nr, ns, c1, c2, k1
     np.testing.assert_array_equal(bits(host(gS)), bits(Ss))
     assert len(J) > 0
     np.testing.assert_array_equal(bits(host(gJ)), bits(J))
+
+
+def test_fused_c2_matches_oracle(gpu, oracle_built):
+    """BASELINE C2 (1M x 1M uniform keys in [1, 3n], seeds 1/2) through the
+    fused pipeline, against the C oracle end to end."""
+    from smj import ops
+    n = 1_000_000
+    R = ops.gen_uniform(n, seed=1, key_range=3 * n)
+    S = ops.gen_uniform(n, seed=2, key_range=3 * n)
+    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000))
+    Rs, Ss, J = ref_pipeline(oracle.gen_uniform(n, 0, 1, 3 * n), oracle.gen_uniform(n, 0, 2, 3 * n), 0, 0,
+                             (0, 5000), (0, 5000))
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
+def test_fused_zipf_c5_shape(gpu, oracle_built):
+    """BASELINE C5's shape on one GPU: |R| = 1e7, |S| = 1e8, Zipf(0.9) keys over
+    1e8 values (the top key holds ~2 % of the rows: single-key groups far over
+    the LDS capacity stream without a sort).  Sorted tables against numpy's
+    stable argsort, joined rows against the C oracle's zip join of those."""
+    from smj import ops
+    R = ops.gen_zipf(10_000_000, seed=3, domain=100_000_000, theta=0.9)
+    S = ops.gen_zipf(100_000_000, seed=4, domain=100_000_000, theta=0.9)
+    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000))
+    assert ops.msd_stats()[0] > 0  # heavy keys took the streaming path
+    sorted_np = []
+    for T, got in ((R, gR), (S, gS)):
+        t = host(T)
+        keep = t[t[:, 0] > 5000]
+        ref = keep[np.argsort(keep[:, 0], kind="stable")]
+        np.testing.assert_array_equal(host(got), ref)
+        sorted_np.append(ref)
+    J = oracle.join(sorted_np[0], sorted_np[1])
+    assert len(J) > 0
+    np.testing.assert_array_equal(host(gJ), J)
