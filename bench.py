@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per table per GPU")
     p.add_argument("--cpu-sample", type=int, default=196608,
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
+    p.add_argument("--cpu-mt", type=int, default=1,
+                   help="time the multi-core CPU port (oracle/cpu_mt.cpp) on the full workload (0 = skip)")
     p.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field")
     return p.parse_args()
@@ -130,21 +132,37 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes / its event time
     dom = max(prof.items(), key=lambda kv: kv[1]["ms"]) if prof else (None, None)
     roof = None
+    pmc = None
+    if os.path.exists(a.pmc):
+        with open(a.pmc) as f:
+            pmc = json.load(f)
+        if pmc.get("rows_per_table") != n:
+            pmc = None
     if dom[0]:
         name, d = dom
         ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         traffic = None
-        if os.path.exists(a.pmc):
-            with open(a.pmc) as f:
-                pmc = json.load(f)
+        if pmc:
             k = pmc.get("kernels", {}).get(name)
-            if k and pmc.get("rows_per_table") == n:
+            if k:
                 traffic = k.get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "alg_bytes_per_launch": d["bytes"] / max(d["launches"], 1),
                 "avg_launch_ms": round(d["ms"] / max(d["launches"], 1), 4),
                 "share_of_step": round(d["ms"] / a.steps / ms_step, 3)}
+    # SURVEY 8(d) sort-phase figure: bytes the sort passes FETCH (PMC FETCH_SIZE x 2,
+    # profiles/pmc_traffic.json) per launch over their measured launch time
+    sort_passes = None
+    if pmc:
+        sort_passes = {}
+        for name in ("msd_part_a", "msd_part_b", "msd_final"):
+            k, d = pmc.get("kernels", {}).get(name), prof.get(name)
+            if k and d and d["launches"]:
+                fetched = 2.0 * k["fetch_kib_raw"] * 1024
+                gbs = fetched / (d["ms"] / d["launches"] * 1e-3) / 1e9
+                sort_passes[name] = {"fetched_bytes_per_launch": round(fetched), "fetch_GBps": round(gbs, 1),
+                                     "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
     # whole-pipeline roofline: 48 B per input row + 24 B per joined row
     b_alg = 48.0 * rows_step + 24.0 * joined
     pipe_gbs = b_alg / (dt / a.steps) / 1e9
@@ -161,6 +179,18 @@ def main():
                "sample": f"first {m} rows of R and of S of this workload (keys in [1,{key_range}]); "
                          f"cpu_app.c select + O(n^2) insertion sort + zip join, 1 thread, gcc -O2; "
                          f"{secs:.2f} s, {jrows} joined rows"}
+
+    cpu_mt = None
+    if rank == 0 and world == 1 and a.cpu_mt:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # CPU baseline leg only
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+        secs, rows = oracle.mt_pipeline(R.cpu().numpy(), S.cpu().numpy(), SELECT, KEYS, threads)
+        assert rows[2] == joined, "CPU port disagrees with the GPU join count"
+        cpu_mt = {"value": round(2 * n / secs, 1), "unit": "rows/s", "cores": threads, "kind": "port",
+                  "sample": f"the full workload ({n} x {n} rows): oracle/cpu_mt.cpp, cpu_app.c's select + "
+                            f"stable sort + zip join on {threads} threads (chunk sort + merge rounds), g++ -O3; "
+                            f"{secs:.2f} s, {rows[2]} joined rows (equal to the GPU's)"}
 
     if rank == 0:
         line = {
@@ -180,6 +210,8 @@ def main():
             "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / a.steps, 4),
                             "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in prof.items()},
             "cpu_baseline": cpu,
+            "cpu_baseline_mt": cpu_mt,
+            "sort_passes": sort_passes,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

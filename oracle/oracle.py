@@ -18,6 +18,7 @@ LIB = os.path.join(HERE, "build", "libsmj_oracle.so")
 TYPED_LIBS = {1: os.path.join(HERE, "build", "libsmj_oracle_u64.so"),
               2: os.path.join(HERE, "build", "libsmj_oracle_f64.so")}
 REF_LIB_U64 = os.path.join(HERE, "_ref", "libcpu_app_ref_u64.so")  # the real cpu_app.c, T = uint64_t
+MT_LIB = os.path.join(HERE, "build", "libsmj_oracle_mt.so")  # multi-core port (cpu_mt.cpp), CPU baseline
 CLI = os.path.join(HERE, "build", "cpu_ref")
 REF_LIB = os.path.join(HERE, "_ref", "libcpu_app_ref.so")   # the real cpu_app.c (when built)
 REF_DRIVER = os.path.join(HERE, "_ref", "ref_driver")
@@ -260,3 +261,40 @@ def join_t(R, S, ktype, key1=0, key2=0):
     res = res[: j * tc].reshape(j, tc).copy().view(dt)
     _libc.free(out)
     return res
+
+
+# ---- multi-core port (cpu_mt.cpp): the CPU baseline at full size ----------------
+_mt = None
+
+
+def mt_pipeline(R, S, sel=(0, 5000, 0, 5000), keys=(0, 0), threads=16, outputs=False):
+    """cpu_app.c's select -> stable sort -> zip join on `threads` cores
+    (cpu_mt.cpp).  Returns (seconds, (m_R, m_S, J)) and, with outputs=True,
+    the sorted tables and joined rows too."""
+    global _mt
+    if _mt is None:
+        if not os.path.exists(MT_LIB):
+            build()
+        _mt = ctypes.CDLL(MT_LIB)
+        _mt.smj_mt_pipeline.restype = ctypes.c_int
+        _mt.smj_mt_pipeline.argtypes = [_P, _L, ctypes.c_int, _P, _L, ctypes.c_int] + \
+            [ctypes.c_int, ctypes.c_int, _L] * 2 + [ctypes.c_int] * 3 + [_P, _P, _P, _P, _P]
+    R = np.ascontiguousarray(R, dtype=np.int64)
+    S = np.ascontiguousarray(S, dtype=np.int64)
+    Rs, Ss = np.empty_like(R), np.empty_like(S)
+    tc = R.shape[1] + S.shape[1] - 1
+    out = np.empty((max(min(len(R), len(S)), 1), tc), dtype=np.int64) if outputs else None
+    rows = (ctypes.c_int64 * 3)()
+    secs = ctypes.c_double()
+    sc1, sv1, sc2, sv2 = sel
+    rc = _mt.smj_mt_pipeline(R.ctypes.data_as(_P), R.shape[0], R.shape[1], S.ctypes.data_as(_P), S.shape[0],
+                             S.shape[1], int(sv1 is not None), sc1, int(sv1 or 0), int(sv2 is not None), sc2,
+                             int(sv2 or 0), keys[0], keys[1], threads, Rs.ctypes.data_as(_P),
+                             Ss.ctypes.data_as(_P), out.ctypes.data_as(_P) if outputs else None, rows,
+                             ctypes.byref(secs))
+    if rc != 0:
+        raise ValueError("mt pipeline arguments")
+    r = (int(rows[0]), int(rows[1]), int(rows[2]))
+    if outputs:
+        return secs.value, r, (Rs[: r[0]], Ss[: r[1]], out[: r[2]])
+    return secs.value, r

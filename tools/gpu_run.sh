@@ -27,7 +27,7 @@ for s in $STEPS; do
     msd)   run msd 600 python -u -m pytest tests/test_gpu_msd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     dist)  run dist 600 python -u -m pytest tests/test_dist_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    quick) run quick 300 python bench.py --cpu-sample 0 ;;
+    quick) run quick 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
@@ -35,14 +35,14 @@ for s in $STEPS; do
     typed) run typed 600 python -u -m pytest tests -m gpu -x -q -k "typed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0
+               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 --cpu-mt 0
            rm -f "$OUT/prof/run_kernel_trace.csv" ;;
     pmcf)  export TMPDIR=/tmp
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 ;;
+               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
     pmcw)  export TMPDIR=/tmp
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 ;;
+               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
