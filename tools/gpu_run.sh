@@ -40,6 +40,9 @@ for s in $STEPS; do
     pmcf)  export TMPDIR=/tmp
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
+    pmcsq) export TMPDIR=/tmp
+           run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
+               --output-format csv -d "$OUT/pmc_sq" -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
     pmcw)  export TMPDIR=/tmp
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
                python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
