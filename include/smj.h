@@ -176,7 +176,7 @@ int smj_dev_join(const int64_t *R, int64_t nr, int c1, const int64_t *S, int64_t
 
 /* Multi-GPU range partition, step 1: counts of selected rows
  * per destination bucket, bucket(k) = #{splitters < k} over n_split sorted
- * splitters (n_split + 1 <= 16 buckets), plus the min / max selected key.
+ * splitters (n_split + 1 <= 64 buckets), plus the min / max selected key.
  * Synchronises; h_counts gets n_split + 1 entries, h_minmax 2 (INT64_MAX /
  * INT64_MIN when nothing is selected). */
 int smj_dev_partition_count(const int64_t *in, int64_t n_rows, int col_num, int use_select,
@@ -188,6 +188,15 @@ int smj_dev_partition_count(const int64_t *in, int64_t n_rows, int col_num, int 
 int smj_dev_partition_scatter(const int64_t *in, int64_t n_rows, int col_num, int use_select,
                               int select_col, int64_t select_val, int key_col, const int64_t *d_splitters,
                               int n_split, const int64_t *h_counts, int64_t *out, void *stream);
+
+/* Steps 1 + 2 in one call (what smj/dist.py runs): stable scatter of the
+ * selected rows into bucket-contiguous `out` (room for n_rows rows), bucket
+ * starts computed on the device; h_counts gets the n_split + 1 bucket
+ * counts.  Reads the table twice (count + scatter) instead of three times.
+ * Synchronises. */
+int smj_dev_partition(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                      int64_t select_val, int key_col, const int64_t *d_splitters, int n_split, int64_t *out,
+                      int64_t *h_counts, void *stream);
 
 /* Synthetic 2-column table (key, payload) for rows [row0, row0 + rows):
  * key = 1 + floor(splitmix64(g + seed * 0xD1B54A32D192ED03) * key_range / 2^64),

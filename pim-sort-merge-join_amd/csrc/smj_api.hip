@@ -170,9 +170,9 @@ struct DevScratch {
     uint32_t *hist = nullptr;                        // kNumPos * kRadix
     SortPlan *plan = nullptr;                        // device
     Counters *ctr = nullptr;                         // device, 8 slots
-    int64_t *dcount = nullptr;                       // device scratch int64 x 32
+    int64_t *dcount = nullptr;                       // device scratch int64 x 256
     SortPlan *h_plan = nullptr;                      // pinned
-    int64_t *h_small = nullptr;                      // pinned, 64 int64
+    int64_t *h_small = nullptr;                      // pinned, 256 int64
 };
 std::map<int, DevScratch> g_scratch;
 int g_ngpus = 0;
@@ -198,11 +198,11 @@ int scratch(DevScratch **out) {
         HIP_TRY(hipMalloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
         HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
         HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
-        HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 32));
+        HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 256));
         HIP_TRY(hipMalloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
         HIP_TRY(hipMalloc(&s.trash, sizeof(int64_t) * kSortThreads * 16));
         HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 64, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 256, hipHostMallocDefault));
     }
     *out = &s;
     return SMJ_OK;
@@ -907,9 +907,10 @@ extern "C" int smj_dev_partition_count(const T *in, int64_t n, int cols, int use
         HIP_TRY(hipMemcpyAsync(spl, d_splitters, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
+    constexpr int kNB = 1 << kBucketBits;
     unsigned long long *gcount = (unsigned long long *)sc->dcount;
-    long long *gminmax = (long long *)(sc->dcount + 16);
-    HIP_TRY(hipMemsetAsync(gcount, 0, sizeof(int64_t) * 16, s));
+    long long *gminmax = (long long *)(sc->dcount + kNB);
+    HIP_TRY(hipMemsetAsync(gcount, 0, sizeof(int64_t) * kNB, s));
     const long long init[2] = {INT64_MAX, INT64_MIN};
     HIP_TRY(hipMemcpyAsync(gminmax, init, sizeof init, hipMemcpyHostToDevice, s));
     if (n > 0) {
@@ -917,11 +918,11 @@ extern "C" int smj_dev_partition_count(const T *in, int64_t n, int cols, int use
         HIP_TRY(launch_hist_bucket(in, n, cols, use_select, sel_col, sel_val, key_col, spl, n_split, gcount,
                                    gminmax, s));
     }
-    HIP_TRY(hipMemcpyAsync(sc->h_small, sc->dcount, sizeof(int64_t) * 18, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(sc->h_small, sc->dcount, sizeof(int64_t) * (kNB + 2), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     for (int b = 0; b <= n_split; b++) h_counts[b] = sc->h_small[b];
-    h_minmax[0] = sc->h_small[16];
-    h_minmax[1] = sc->h_small[17];
+    h_minmax[0] = sc->h_small[kNB];
+    h_minmax[1] = sc->h_small[kNB + 1];
     return SMJ_OK;
 }
 
@@ -966,6 +967,62 @@ extern "C" int smj_dev_partition_scatter(const T *in, int64_t n, int cols, int u
     SMJ_TRY(run_pass(sc, ps, d_base, &sc->ctr[3], false, total, s));
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_TRY(hipStreamSynchronize(s));
+    return SMJ_OK;
+}
+
+// One-call partition (the multi-GPU hot path): chunk_hist -> bases on the
+// device -> chunk_scatter; the bucket counts come back with the rows, so no
+// separate counting pass reads the table.
+extern "C" int smj_dev_partition(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                                 int key_col, const T *d_splitters, int n_split, T *out, int64_t *h_counts,
+                                 void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    if (n_split < 0 || n_split > kMaxSplitters || !h_counts) return SMJ_ERR_INVALID;
+    for (int b = 0; b <= n_split; b++) h_counts[b] = 0;
+    if (n == 0) return SMJ_OK;
+    if (!out || in == out || (n_split && !d_splitters)) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    int64_t spl[kMaxSplitters];
+    if (n_split) {
+        HIP_TRY(hipMemcpyAsync(spl, d_splitters, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    PassSpec ps{};
+    ps.src = in;
+    ps.nsrc = n;
+    ps.dst = out;
+    ps.cols = cols;
+    ps.use_select = use_select;
+    ps.sel_col = sel_col;
+    ps.key_col = key_col;
+    ps.sel_val = sel_val;
+    ps.kind = DIGIT_BUCKET;
+    ps.spl = spl;
+    ps.nspl = n_split;
+    ps.trash = sc->trash;
+    SMJ_TRY(grow(&sc->status, &sc->status_bytes, (size_t)pass_chunks(ps) * pass_radix(ps) * sizeof(uint32_t)));
+    uint32_t *table = (uint32_t *)sc->status;
+    uint32_t *d_base = (uint32_t *)sc->dcount;                                // [64] u32
+    unsigned long long *d_cnt = (unsigned long long *)(sc->dcount + 64);      // [64] u64
+    const double rowb = 8.0 * cols;
+    {
+        ProfScope p1("partition_hist", rowb * n, s);
+        HIP_TRY(launch_chunk_hist(ps, table, s));
+    }
+    {
+        ProfScope p2("partition_scan", 0, s);
+        HIP_TRY(launch_chunk_scan_dev(ps, table, sc->segsum, d_base, d_cnt, s));
+    }
+    HIP_TRY(hipMemsetAsync(&sc->ctr[3], 0, sizeof(Counters), s));
+    {
+        ProfScope p3("partition_scatter", rowb * 2 * n, s);  // bytes assume every row selected
+        HIP_TRY(launch_chunk_scatter(ps, table, &sc->ctr[3], s));
+    }
+    HIP_TRY(hipMemcpyAsync(sc->h_small, d_cnt, sizeof(int64_t) * (n_split + 1), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int b = 0; b <= n_split; b++) h_counts[b] = sc->h_small[b];
     return SMJ_OK;
 }
 

@@ -27,7 +27,7 @@ constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kRadixBits = SMJ_RADIX_BITS;       // digit width of the radix passes
 constexpr int kRadix = 1 << kRadixBits;          // 1024 bins
 constexpr int kNumPos = (64 + kRadixBits - 1) / kRadixBits;  // 7 digit positions
-constexpr int kBucketBits = 4;                   // multi-GPU partition: <= 16 buckets
+constexpr int kBucketBits = 6;                   // multi-GPU partition: <= 64 buckets
 constexpr int kMaxSplitters = (1 << kBucketBits) - 1;
 
 // rows per thread per tile: a tile is 64 KiB of rows whatever the row width
@@ -107,6 +107,10 @@ hipError_t launch_chunk_hist(const PassSpec &ps, uint32_t *table, hipStream_t s)
 hipError_t launch_chunk_scan(const PassSpec &ps, uint32_t *table, uint32_t *segsum, const uint32_t *base,
                              hipStream_t s);
 hipError_t launch_chunk_scatter(const PassSpec &ps, uint32_t *table, Counters *ctr, hipStream_t s);
+// chunk_scan with the digit bases computed on the device (exclusive prefix of
+// the digit totals, written to base[radix]); the totals go to counts[radix]
+hipError_t launch_chunk_scan_dev(const PassSpec &ps, uint32_t *table, uint32_t *segsum, uint32_t *base,
+                                 unsigned long long *counts, hipStream_t s);
 hipError_t launch_hist_bucket(const int64_t *src, int64_t n, int cols, int use_select, int sel_col,
                               int64_t sel_val, int key_col, const int64_t *spl, int nspl,
                               unsigned long long *gcount, long long *gminmax, hipStream_t s);

@@ -64,9 +64,32 @@ struct BucketDigit {  // multi-GPU range partition: #splitters < key
     int64_t spl[kMaxSplitters];
     int nspl;
     __device__ __forceinline__ uint32_t operator()(int64_t key) const {
+        uint32_t b = 0;  // unused entries are INT64_MAX (make_bucket): never < key
+#pragma unroll
+        for (int i = 0; i < kMaxSplitters; i++) b += spl[i] < key ? 1u : 0u;
+        return b;
+    }
+};
+// A digit functor as the pass kernels evaluate it.  BucketDigit's splitters
+// are staged in LDS (padded to 64 with INT64_MAX) and searched branch-free in
+// 6 probes instead of 63 64-bit compares per key.
+static_assert(kMaxSplitters == 63, "the staged bucket search assumes 2^6 - 1 splitters");
+template <class DigitF>
+struct DigitLds {
+    static constexpr int N = 1;
+    __device__ static void stage(const DigitF &, int64_t *, int) {}
+    __device__ static uint32_t eval(const DigitF &f, const int64_t *, int64_t key) { return f(key); }
+};
+template <>
+struct DigitLds<BucketDigit> {
+    static constexpr int N = 64;
+    __device__ static void stage(const BucketDigit &f, int64_t *sp, int tid) {
+        if (tid < 64) sp[tid] = tid < kMaxSplitters ? f.spl[tid] : INT64_MAX;
+    }
+    __device__ static uint32_t eval(const BucketDigit &, const int64_t *sp, int64_t key) {
         uint32_t b = 0;
 #pragma unroll
-        for (int i = 0; i < kMaxSplitters; i++) b += (i < nspl && spl[i] < key) ? 1u : 0u;
+        for (uint32_t step = 32; step; step >>= 1) b += sp[b + step - 1] < key ? step : 0u;
         return b;
     }
 };
@@ -133,8 +156,10 @@ __global__ __launch_bounds__(512) void chunk_hist_kernel(const PassParams<DigitF
     constexpr int64_t CH = chunk_rows(COLS);
     constexpr int U = 8;
     __shared__ uint32_t sh[RADIX];
+    __shared__ int64_t s_dspl[DigitLds<DigitF>::N];
     const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < RADIX; i += 512) sh[i] = 0;
+    DigitLds<DigitF>::stage(p.digit, s_dspl, tid);
     __syncthreads();
     const int64_t begin = (int64_t)blockIdx.x * CH;
     const int64_t end = min(begin + CH, p.nsrc);
@@ -152,7 +177,7 @@ __global__ __launch_bounds__(512) void chunk_hist_kernel(const PassParams<DigitF
             const bool ok = r < end && (!p.use_select || sv[u] > p.sel_val);
             const uint64_t act = __ballot(ok);
             if (act == 0) continue;
-            const uint32_t d = p.digit(key[u]) & MASK;
+            const uint32_t d = DigitLds<DigitF>::eval(p.digit, s_dspl, key[u]) & MASK;
             const int leader = __ffsll((unsigned long long)act) - 1;
             const uint32_t dl = __shfl(d, leader, 64);
             if (__ballot(ok && d == dl) == act) {
@@ -225,6 +250,23 @@ __global__ __launch_bounds__(256) void chunk_scan_apply_kernel(uint32_t *__restr
     }
 }
 
+// Bases of a pass whose digit totals are not known on the host (the
+// multi-GPU partition): totals = sum of the scan segments, bases = their
+// exclusive prefix in digit order.  One wave, lane = digit (radix <= 64).
+__global__ __launch_bounds__(64) void digit_base_kernel(const uint32_t *__restrict__ segsum, int radix,
+                                                        uint32_t *__restrict__ base,
+                                                        unsigned long long *__restrict__ counts) {
+    const int lane = threadIdx.x;
+    uint32_t tot = 0;
+    if (lane < radix)
+        for (int sg = 0; sg < kScanSegs; sg++) tot += segsum[(size_t)sg * radix + lane];
+    const uint32_t incl = wave_incl_scan(tot, lane);
+    if (lane < radix) {
+        base[lane] = incl - tot;
+        counts[lane] = tot;
+    }
+}
+
 // ---- chunk_scatter: stable scatter of one chunk per workgroup ---------------
 // Tiles of the chunk are taken in order; the next tile's rows are loaded into
 // registers while the current one is ranked and scattered.  Per tile:
@@ -261,6 +303,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
     constexpr int BPT = RADIX > kSortThreads ? RADIX / kSortThreads : 1;  // digits d = tid + j*kSortThreads
 
     __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
+    __shared__ int64_t s_dspl[DigitLds<DigitF>::N];
     int64_t *s_rows = reinterpret_cast<int64_t *>(smem);          // staging tile (after ranking)
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(smem);        // [wave][digit] counters (ranking)
     uint16_t *s_dig = reinterpret_cast<uint16_t *>(smem + L::OFF_DIG);
@@ -283,6 +326,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
         if (d < RADIX) s_run[d] = (int32_t)p.table[(size_t)blockIdx.x * RADIX + d];
     }
     zero_counters<RADIX>(wc, lane);
+    DigitLds<DigitF>::stage(p.digit, s_dspl, tid);
     int64_t rows[ITEMS][COLS];
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) load_row<COLS>(src + (int64_t)min(lane_row + it * 64, clen - 1) * COLS, rows[it]);
@@ -314,7 +358,7 @@ __global__ __launch_bounds__(kSortThreads, 4) void chunk_scatter_kernel(const Pa
             const bool inb = row0 + it * 64 < clen;
             const bool pass = !p.use_select | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
             const bool v = inb & pass;
-            dig[it] = v ? (p.digit(pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
+            dig[it] = v ? (DigitLds<DigitF>::eval(p.digit, s_dspl, pick<COLS>(rows[it], p.key_col)) & MASK) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
         // ---- stable rank within the tile; dig[it] becomes (rank << 16) | digit
@@ -605,15 +649,17 @@ __global__ __launch_bounds__(512) void hist_bucket_kernel(const int64_t *__restr
                                                           long long *gminmax) {
     __shared__ uint32_t sh[1 << kBucketBits];
     __shared__ long long smin[8], smax[8];
+    __shared__ int64_t s_dspl[DigitLds<BucketDigit>::N];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < (1 << kBucketBits)) sh[tid] = 0;
+    DigitLds<BucketDigit>::stage(dg, s_dspl, tid);
     __syncthreads();
     long long mn = INT64_MAX, mx = INT64_MIN;
     for (int64_t r = (int64_t)blockIdx.x * 512 + tid; r < n; r += (int64_t)gridDim.x * 512) {
         const int64_t key = src[r * COLS + key_col];
         const bool ok = !use_select || src[r * COLS + sel_col] > sel_val;
         if (ok) {
-            atomicAdd(&sh[dg(key)], 1u);
+            atomicAdd(&sh[DigitLds<BucketDigit>::eval(dg, s_dspl, key)], 1u);
             mn = min(mn, (long long)key);
             mx = max(mx, (long long)key);
         }
@@ -1085,6 +1131,18 @@ hipError_t launch_chunk_scan(const PassSpec &ps, uint32_t *table, uint32_t *segs
     const int64_t nch = pass_chunks(ps);
     const dim3 grid((radix + 63) / 64, kScanSegs);
     hipLaunchKernelGGL(chunk_scan_seg_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum);
+    hipLaunchKernelGGL(chunk_scan_apply_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_scan_dev(const PassSpec &ps, uint32_t *table, uint32_t *segsum, uint32_t *base,
+                                 unsigned long long *counts, hipStream_t s) {
+    const int radix = pass_radix(ps);
+    if (radix > 64) return hipErrorInvalidValue;
+    const int64_t nch = pass_chunks(ps);
+    const dim3 grid((radix + 63) / 64, kScanSegs);
+    hipLaunchKernelGGL(chunk_scan_seg_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum);
+    hipLaunchKernelGGL(digit_base_kernel, dim3(1), dim3(64), 0, s, segsum, radix, base, counts);
     hipLaunchKernelGGL(chunk_scan_apply_kernel, grid, dim3(256), 0, s, table, nch, radix, segsum, base);
     return hipGetLastError();
 }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "smj_dev_join": (_I, [_P, _L, _I, _P, _L, _I, _I, _I, _P, _P, _PL, _P]),
     "smj_dev_partition_count": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _PL, _PL, _P]),
     "smj_dev_partition_scatter": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _PL, _P, _P]),
+    "smj_dev_partition": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _PL, _P]),
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),

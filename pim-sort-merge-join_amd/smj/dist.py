@@ -23,11 +23,21 @@ contiguous slice of R and of S (rank order = input order) and:
      the received R and S slices + zip join) with no select -- the partition
      step already applied the WHERE clause.
 
+Stages (exchange / compute overlap): each rank's key range is cut into K
+consecutive sub-ranges (W*K balanced segments instead of W).  Segment
+d*K + k goes to rank d in stage k.  Stage k's rows travel as one batch of
+point-to-point sends / receives (RCCL group over xGMI; received chunks
+placed in source-rank order) while the local pipeline sorts and joins stage
+k - 1's sub-range: sort and zip join are per-key operations, so the stage
+outputs concatenated in stage order are the rank's slice of the result.
+
 Concatenating the per-rank outputs in rank order is exactly cpu_app.c's
 result (stable sort + zip join are per-key operations on disjoint key ranges).
 The local operators come from an `ops` object: HipOps (the product path) or,
 in the gloo CPU tests only, an oracle-backed stand-in.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -35,14 +45,15 @@ from . import ops as hip_ops
 
 INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
-MAX_BOUNDS = 15  # smj_dev_partition_*: <= 16 buckets
+MAX_BOUNDS = 63  # smj_dev_partition*: <= 64 buckets
+DEFAULT_STAGES = int(os.environ.get("SMJ_DIST_STAGES", "2"))
 
 
 class HipOps:
     """The product operators: HIP kernels behind libsmj_hip.so."""
     sort_merge_join = staticmethod(hip_ops.sort_merge_join)
-    partition_count = staticmethod(hip_ops.partition_count)
-    partition_scatter = staticmethod(hip_ops.partition_scatter)
+    partition = staticmethod(hip_ops.partition)
+    writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
 def _sample_keys(table, key_col, samples):
@@ -62,8 +73,10 @@ def _wire_device(t, group=None):
     return t.device
 
 
-def choose_splitters(tables_and_keys, world, group=None, samples=4096):
-    """W-1 sorted key splitters, identical on every rank (one all_gather)."""
+def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None):
+    """parts - 1 (default W - 1) sorted key splitters, identical on every rank
+    (one all_gather)."""
+    parts = parts or world
     local = torch.cat([_sample_keys(t, k, samples) for t, k in tables_and_keys])
     home = local.device
     dev = _wire_device(local, group)
@@ -79,10 +92,10 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096):
     dist.all_gather(all_buf, buf, group=group)
     keys = torch.cat([b[: int(c.item())] for b, c in zip(all_buf, all_cnt)])
     if keys.numel() == 0:
-        return torch.zeros(world - 1, dtype=torch.int64, device=home)
+        return torch.zeros(parts - 1, dtype=torch.int64, device=home)
     keys = torch.sort(keys).values
     L = keys.numel()
-    pos = torch.tensor([max((i + 1) * L // world - 1, 0) for i in range(world - 1)], device=dev)
+    pos = torch.tensor([max((i + 1) * L // parts - 1, 0) for i in range(parts - 1)], device=dev)
     return keys[pos].contiguous().to(home)
 
 
@@ -163,30 +176,66 @@ def gather_counts(counts, world, group=None, device=None):
     return [[int(v) for v in o.tolist()] for o in out]
 
 
-def exchange_rows(send, counts, group=None):
-    """all_to_all_single of bucket-contiguous rows; returns rows received in
-    source-rank order."""
-    home = send.device
-    dev = _wire_device(send, group)
-    send = send.to(dev)
-    world = len(counts)
-    send_counts = torch.tensor(counts, dtype=torch.int64, device=dev)
-    recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    rc = [int(x) for x in recv_counts.tolist()]
-    recv = torch.empty((sum(rc), send.shape[1]), dtype=send.dtype, device=dev)
-    dist.all_to_all_single(recv, send[: sum(counts)].contiguous(), output_split_sizes=rc,
-                           input_split_sizes=list(counts),
-                           group=group)
-    return recv.to(home)
+def stage_count(world, stages):
+    """Stages K such that the W*K - 1 splitters, each with a single-key
+    bucket, fit the partition kernel: 2 (W K - 1) <= MAX_BOUNDS."""
+    k = max(1, int(stages))
+    while k > 1 and 2 * (world * k - 1) > MAX_BOUNDS:
+        k -= 1
+    return k
+
+
+class _Stage:
+    """One stage's receives in flight: wait() returns the (R, S) rows of this
+    rank's sub-range, chunks in source-rank order."""
+
+    def __init__(self, works, recvs, home):
+        self.works, self.recvs, self.home = works, recvs, home
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return [r.to(self.home) for r in self.recvs]
+
+
+def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
+    """Post stage k's exchange: segment d*K + k of every table goes to rank d.
+    seg[t][r][j] = rows of src rank r's table-t buffer in segment j (known on
+    every rank from the gathered counts, so no count exchange is needed);
+    offs[t][j] = start of segment j in this rank's buffer.  sends are on the
+    wire device (_wire_device); received rows are returned on `home`."""
+    p2p, recvs = [], []
+    for t, wire in enumerate(sends):
+        me = rank * K + k
+        rc = [seg[t][r][me] for r in range(world)]
+        recv = torch.empty((sum(rc), wire.shape[1]), dtype=wire.dtype, device=wire.device)
+        at = 0
+        for r in range(world):
+            if rc[r] and r == rank:
+                recv[at: at + rc[r]].copy_(wire[offs[t][me]: offs[t][me] + rc[r]])
+            elif rc[r]:
+                p2p.append(dist.P2POp(dist.irecv, recv[at: at + rc[r]], r, group, tag=t * 4096 + k))
+            at += rc[r]
+        for d in range(world):
+            j = d * K + k
+            c = seg[t][rank][j]
+            if c and d != rank:
+                p2p.append(dist.P2POp(dist.isend, wire[offs[t][j]: offs[t][j] + c], d, group, tag=t * 4096 + k))
+        recvs.append(recv)
+    works = dist.batch_isend_irecv(p2p) if p2p else []
+    return _Stage(works, recvs, home)
 
 
 def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, ops=None, samples=4096,
-                    stats=None):
+                    stats=None, stages=None):
     """The distributed pipeline; returns this rank's slice of the result (the
     global result is the concatenation over ranks in rank order).  stats
     (optional dict) gets the rows this rank received per table and the
-    max / mean load over ranks (load-balance report)."""
+    max / mean load over ranks (load-balance report).  stages: key sub-ranges
+    per rank whose exchange overlaps the previous one's sort + join
+    (default SMJ_DIST_STAGES or 2; 1 = exchange everything, then compute).
+    The local pipeline has a fixed cost per call: 1e8 rows per table take
+    6.03 ms in one call, 6.37 ms in 2 and 8.53 ms in 4 (tools/part_probe.py)."""
     ops = ops or HipOps
     sc1, sv1, sc2, sv2 = select
     k1, k2 = keys
@@ -194,28 +243,61 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if world == 1:
         return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
+    K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
+    nseg = world * K
 
-    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples)
+    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg)
     bounds, single = bucket_bounds(spl)
     bt = torch.tensor(bounds, dtype=torch.int64, device=R.device)
     nb = len(bounds) + 1
     counts, sends = [], []
     for T, key, sc, sv in ((R, k1, sc1, sv1), (S, k2, sc2, sv2)):
-        c, _ = ops.partition_count(T, bt, key, sc, sv)
+        c, rows = ops.partition(T, bt, key, sc, sv)
         counts.append(c)
-        sends.append(ops.partition_scatter(T, bt, c, key, sc, sv))
+        sends.append(rows.to(_wire_device(rows, group)))
     allc = gather_counts(counts[0] + counts[1], world, group, _wire_device(R, group))
     G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
-    cuts = choose_cuts(G[0], G[1], single, world)
-    local = []
+    cuts = choose_cuts(G[0], G[1], single, nseg)
+    # every source rank's rows per segment, from the gathered counts
+    seg = [[slice_counts(allc[r][t * nb:(t + 1) * nb],
+                         [sum(allc[q][t * nb + b] for q in range(r)) for b in range(nb)], cuts, nb)
+            for r in range(world)] for t in range(2)]
+    offs = []
     for t in range(2):
-        prefix = [sum(allc[r][t * nb + b] for r in range(rank)) for b in range(nb)]
-        local.append(exchange_rows(sends[t], slice_counts(counts[t], prefix, cuts, nb), group))
+        o, acc = [], 0
+        for c in seg[t][rank]:
+            o.append(acc)
+            acc += c
+        offs.append(o)
+    rows_in = [sum(seg[t][r][rank * K + k] for r in range(world) for k in range(K)) for t in range(2)]
+    bound = sum(min(sum(seg[0][r][rank * K + k] for r in range(world)),
+                    sum(seg[1][r][rank * K + k] for r in range(world))) for k in range(K))
+    into = getattr(ops, "writes_into", False)
+    ncols = R.shape[1] + S.shape[1] - 1
+    J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
+    parts, at = [], 0
+    pending = post_stage(0, K, sends, offs, seg, rank, world, R.device, group)
+    for k in range(K):
+        Rk, Sk = pending.wait()
+        if k + 1 < K:
+            pending = post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group)
+        if Rk.shape[0] == 0 or Sk.shape[0] == 0:
+            continue
+        if into:
+            b = min(Rk.shape[0], Sk.shape[0])
+            got = ops.sort_merge_join(Rk, Sk, k1, k2, None, None, out=J[at: at + b])[2]
+            at += got.shape[0]
+        else:
+            parts.append(ops.sort_merge_join(Rk, Sk, k1, k2, None, None)[2])
+        del Rk, Sk
     del sends
     if stats is not None:
-        rows = [int(local[0].shape[0]), int(local[1].shape[0])]
-        loads = gather_counts([rows[0] + rows[1]], world, group, _wire_device(R, group))
+        loads = gather_counts([rows_in[0] + rows_in[1]], world, group, _wire_device(R, group))
         mean = sum(l[0] for l in loads) / world
-        stats.update(rows_in=rows, load_max_over_mean=(max(l[0] for l in loads) / mean) if mean else 1.0,
-                     cuts=cuts, buckets=nb)
-    return ops.sort_merge_join(local[0], local[1], k1, k2, None, None)[2]
+        stats.update(rows_in=rows_in, load_max_over_mean=(max(l[0] for l in loads) / mean) if mean else 1.0,
+                     cuts=cuts, buckets=nb, stages=K)
+    if into:
+        return J[:at]
+    if not parts:
+        return R.new_empty((0, ncols))
+    return torch.cat(parts) if len(parts) > 1 else parts[0]

@@ -226,6 +226,24 @@ def partition_scatter(table, splitters, counts, key_col=0, select_col=0, select_
     return out[:total]
 
 
+def partition(table, splitters, key_col=0, select_col=0, select_val=None, out=None, stream=None):
+    """Stable select + bucket scatter in one call (smj_dev_partition): returns
+    (bucket counts, the selected rows in bucket-contiguous order)."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    ns = int(splitters.numel())
+    if out is None:
+        out = torch.empty((max(n, 1), cols), dtype=torch.int64, device=table.device)
+    counts = (ctypes.c_int64 * (ns + 1))()
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition(_ptr(table), n, cols, int(use), select_col, int(select_val) if use else 0,
+                                     key_col, _ptr(splitters), ns, _ptr(out), counts, _stream(stream)),
+               "smj_dev_partition")
+    counts = [int(c) for c in counts]
+    return counts, out[: sum(counts)]
+
+
 def gen_uniform(rows, row0=0, seed=1, key_range=None, device="cuda", out=None, stream=None):
     """Synthetic (key, payload) table: keys iid uniform in [1, key_range],
     payload = global row index."""

@@ -59,6 +59,11 @@ class OracleOps:
         keep, bucket = OracleOps._keep(T, key, sc, sv, spl)
         return torch.from_numpy(keep[np.argsort(bucket, kind="stable")].copy())
 
+    @staticmethod
+    def partition(T, spl, key=0, sc=0, sv=None):
+        counts, _ = OracleOps.partition_count(T, spl, key, sc, sv)
+        return counts, OracleOps.partition_scatter(T, spl, counts, key, sc, sv)
+
 
 def free_port():
     with socket.socket() as s:
@@ -88,7 +93,7 @@ def _worker(rank, world, port, R, S, cfg, outdir):
         r, s, ops = r.cuda(), s.cuda(), None
     stats = {}
     out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=ops, samples=cfg["samples"],
-                                stats=stats)
+                                stats=stats, stages=cfg.get("stages"))
     np.save(os.path.join(outdir, f"rank{rank}.npy"), out.cpu().numpy())
     if rank == 0:
         np.save(os.path.join(outdir, "load.npy"), np.array([stats["load_max_over_mean"]]))
@@ -120,6 +125,9 @@ def make_tables(kind, n):
     (3, "uniform", {"select": (0, 100, 0, 20000), "keys": (0, 0), "samples": 16}),
     (2, "dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 32}),
     (3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8}),
+    (2, "uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 64, "stages": 1}),
+    (3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8, "stages": 1}),
+    (4, "dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 32, "stages": 8}),
 ])
 def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
     _run_and_check(tmp_path, world, kind, cfg, 30_000)
@@ -130,9 +138,10 @@ def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
     ("dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 256, "gpu": True}),
     ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True}),
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "stages": 1}),
 ])
 def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
-    """The product path of smj/dist.py -- HIP partition_count/scatter and the
+    """The product path of smj/dist.py -- HIP smj_dev_partition and the
     fused local smj_dev_sort_merge_join -- with 2 ranks sharing cuda:0 and the
     all_to_all staged through gloo (RCCL needs one GPU per rank)."""
     _run_and_check(tmp_path, 2, kind, cfg, 400_000)
@@ -146,6 +155,13 @@ def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):
     load = _run_and_check(tmp_path, 4, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 64},
                           40_000)
     assert load < 1.10, load
+
+
+def test_stage_count():
+    from smj import dist as sdist
+    # 2 (W K - 1) boundaries must fit the 64-bucket partition kernel
+    assert [sdist.stage_count(w, 4) for w in (2, 4, 8, 16)] == [4, 4, 4, 2]
+    assert sdist.stage_count(8, 1) == 1 and sdist.stage_count(32, 4) == 1
 
 
 def test_choose_cuts_pure():

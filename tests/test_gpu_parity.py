@@ -134,6 +134,27 @@ def test_partition_matches_numpy(gpu):
     np.testing.assert_array_equal(host(got), keep[np.argsort(bucket, kind="stable")])
 
 
+@pytest.mark.parametrize("n,cols,nspl,sv", [(200_001, 3, 63, -900), (1_000_000, 2, 31, None), (1, 2, 5, None),
+                                             (50_000, 5, 63, 2000), (3_000_000, 2, 0, -5000)])
+def test_partition_fused_matches_numpy(gpu, n, cols, nspl, sv):
+    """smj_dev_partition (what smj/dist.py runs): counts + stable scatter in one
+    call, up to 63 splitters (64 buckets), duplicate splitters, empty
+    selection (sv = 2000 keeps nothing)."""
+    from smj import ops
+    rng = np.random.default_rng(n + nspl)
+    t = rng.integers(-1000, 1000, size=(n, cols), dtype=np.int64)
+    t[:, 1] = np.arange(n)
+    spl = np.sort(rng.integers(-1100, 1100, size=nspl)).astype(np.int64)
+    if nspl > 3:
+        spl[2] = spl[1]
+    sc = cols - 1
+    counts, got = ops.partition(dev(t), dev(spl), key_col=0, select_col=sc, select_val=sv)
+    keep = t if sv is None else t[t[:, sc] > sv]
+    bucket = np.searchsorted(spl, keep[:, 0], side="left")
+    assert counts == np.bincount(bucket, minlength=nspl + 1).tolist()
+    np.testing.assert_array_equal(host(got), keep[np.argsort(bucket, kind="stable")])
+
+
 def test_gen_uniform_matches_oracle(gpu, oracle_built):
     from smj import ops
     got = ops.gen_uniform(1_000_003, row0=12345, seed=2, key_range=3_000_000)

@@ -32,6 +32,8 @@ for s in $STEPS; do
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     h2d)   run h2d 300 python tools/h2d_probe.py ;;
+    part)  run part 300 python tools/part_probe.py ;;
+    ptest) run ptest 600 python -u -m pytest tests -m gpu -x -v -k "partition or distributed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     typed) run typed 600 python -u -m pytest tests -m gpu -x -q -k "typed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
