@@ -11,7 +11,9 @@ reference's user.h WHERE col0 > 5000 and JOIN_KEY 0.  Inputs are generated
 on the device and resident in HBM before timing.  One step = the whole hot
 path: select + stable sort of R and of S, then the 1:1 zip join (N = 1);
 for N > 1 the range partition + RCCL all-to-all exchange comes first and
-per-GPU work is fixed (weak scaling: the N=8 job is 8e8 x 8e8).
+per-GPU work is fixed (weak scaling: the N=8 job is 8e8 x 8e8); the
+exchange runs in stages (key sub-ranges) overlapping the local sort + join
+of the previous stage (smj/dist.py).
 
 value = (|R| + |S| over all ranks) / max-over-ranks seconds per step.
 """
@@ -202,7 +204,8 @@ def main():
                                    "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
                        "rows_per_table_per_gpu": n, "rows_per_table_total": total, "key_range": key_range,
                        "joined_rows": joined, "parallelism": f"range-partition x{world}",
-                       "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4)},
+                       "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
+                       "exchange_stages": lb.get("stages", 0)},
             "roofline": roof,
             "pipeline_roofline": {"alg_bytes_per_step": b_alg, "achieved": round(pipe_gbs, 1),
                                   "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
