@@ -30,6 +30,8 @@ point-to-point sends / receives (RCCL group over xGMI; received chunks
 placed in source-rank order) while the local pipeline sorts and joins stage
 k - 1's sub-range: sort and zip join are per-key operations, so the stage
 outputs concatenated in stage order are the rank's slice of the result.
+S is counted first (a read-only pass), so the cuts are known once R is
+partitioned and R's stage-0 rows travel while S is being partitioned.
 
 Concatenating the per-rank outputs in rank order is exactly cpu_app.c's
 result (stable sort + zip join are per-key operations on disjoint key ranges).
@@ -53,6 +55,7 @@ class HipOps:
     """The product operators: HIP kernels behind libsmj_hip.so."""
     sort_merge_join = staticmethod(hip_ops.sort_merge_join)
     partition = staticmethod(hip_ops.partition)
+    partition_count = staticmethod(hip_ops.partition_count)
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
@@ -186,8 +189,9 @@ def stage_count(world, stages):
 
 
 class _Stage:
-    """One stage's receives in flight: wait() returns the (R, S) rows of this
-    rank's sub-range, chunks in source-rank order."""
+    """One stage's receives in flight: wait() returns the [R, S] rows of this
+    rank's sub-range (None for a table not posted), chunks in source-rank
+    order."""
 
     def __init__(self, works, recvs, home):
         self.works, self.recvs, self.home = works, recvs, home
@@ -195,7 +199,16 @@ class _Stage:
     def wait(self):
         for w in self.works:
             w.wait()
-        return [r.to(self.home) for r in self.recvs]
+        return [None if r is None else r.to(self.home) for r in self.recvs]
+
+
+def _wait_all(pending):
+    out = [None, None]
+    for st in pending:
+        for t, r in enumerate(st.wait()):
+            if r is not None:
+                out[t] = r
+    return out
 
 
 def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
@@ -203,9 +216,13 @@ def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
     seg[t][r][j] = rows of src rank r's table-t buffer in segment j (known on
     every rank from the gathered counts, so no count exchange is needed);
     offs[t][j] = start of segment j in this rank's buffer.  sends are on the
-    wire device (_wire_device); received rows are returned on `home`."""
+    wire device (_wire_device), None for a table not posted in this call;
+    received rows are returned on `home`."""
     p2p, recvs = [], []
     for t, wire in enumerate(sends):
+        if wire is None:
+            recvs.append(None)
+            continue
         me = rank * K + k
         rc = [seg[t][r][me] for r in range(world)]
         recv = torch.empty((sum(rc), wire.shape[1]), dtype=wire.dtype, device=wire.device)
@@ -250,12 +267,14 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     bounds, single = bucket_bounds(spl)
     bt = torch.tensor(bounds, dtype=torch.int64, device=R.device)
     nb = len(bounds) + 1
-    counts, sends = [], []
-    for T, key, sc, sv in ((R, k1, sc1, sv1), (S, k2, sc2, sv2)):
-        c, rows = ops.partition(T, bt, key, sc, sv)
-        counts.append(c)
-        sends.append(rows.to(_wire_device(rows, group)))
-    allc = gather_counts(counts[0] + counts[1], world, group, _wire_device(R, group))
+    # exact S counts first (a read-only counting pass), so that R's stage-0
+    # rows can leave while S is being partitioned
+    cS, _ = ops.partition_count(S, bt, k2, sc2, sv2)
+    cR, rowsR = ops.partition(R, bt, k1, sc1, sv1)
+    wire = _wire_device(rowsR, group)
+    sends = [rowsR.to(wire), None]
+    del rowsR
+    allc = gather_counts(cR + cS, world, group, _wire_device(R, group))
     G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
     cuts = choose_cuts(G[0], G[1], single, nseg)
     # every source rank's rows per segment, from the gathered counts
@@ -276,11 +295,17 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     ncols = R.shape[1] + S.shape[1] - 1
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
-    pending = post_stage(0, K, sends, offs, seg, rank, world, R.device, group)
+    pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group)]  # R's stage 0
+    cS2, rowsS = ops.partition(S, bt, k2, sc2, sv2)  # overlaps R's stage-0 exchange
+    if list(cS2) != list(cS):
+        raise RuntimeError("smj.dist: partition counts disagree with the counting pass")
+    sends[1] = rowsS.to(wire)
+    del rowsS
+    pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group))
     for k in range(K):
-        Rk, Sk = pending.wait()
+        Rk, Sk = _wait_all(pending)
         if k + 1 < K:
-            pending = post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group)
+            pending = [post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group)]
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
             continue
         if into:
