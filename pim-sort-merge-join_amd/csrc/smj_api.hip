@@ -446,6 +446,7 @@ struct MsdScratch {
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
+int64_t g_msd_groups[3] = {0, 0, 0};  // last pipeline: dense groups, radix-tier groups, wide-tier groups
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -630,6 +631,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             bp.bk[x] = (MsdBucket *)ms->t[x].bk;
         }
         bp.ntab = ntab;
+        bp.full_radix = getenv("SMJ_PASSB_FULL") && atoi(getenv("SMJ_PASSB_FULL")) == 1;
         bp.spl = ms->spl;
         bp.plan = ms->plan;
         HIP_TRY(launch_msd_bases(bp, s));
@@ -712,6 +714,9 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     g_msd_stats[1] = ms->h_plan->nbig;
     g_msd_stats[2] = ms->h_plan->m[0];
     g_msd_stats[3] = ms->h_plan->m[1];
+    g_msd_groups[0] = ms->h_plan->ngroups;
+    g_msd_groups[1] = ms->h_plan->nradix;
+    g_msd_groups[2] = ms->h_plan->nwide;
     bool redo = false;
     SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
     if (redo) {
@@ -788,6 +793,11 @@ extern "C" int smj_debug_final_time(int dbg, int reps, float *ms) {
     hipEventDestroy(a);
     hipEventDestroy(b);
     return SMJ_OK;
+}
+
+// Diagnostic only (not part of smj.h): group counts of the last MSD pipeline.
+extern "C" void smj_debug_msd_groups(int64_t *out3) {
+    for (int i = 0; i < 3; i++) out3[i] = g_msd_groups[i];
 }
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {

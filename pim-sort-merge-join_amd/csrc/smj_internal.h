@@ -222,6 +222,7 @@ struct MsdBasesParams {
     int64_t ntiles[2];
     int tile[2];
     int ntab;
+    int full_radix;            // ablation (SMJ_PASSB_FULL=1): D = kRadB pass-B sub-buckets in every bucket
     const int64_t *spl;
     MsdBucket *bk[2];
     MsdPlan *plan;

@@ -457,9 +457,16 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
         mn = min(mn, s_mm[w]);
         mx = max(mx, s_mm[4 + w]);
     }
+    // rows of bucket a per table
+    uint32_t Lt[2] = {0u, 0u};
+    if (a < kBucketsA)
+        for (int x = 0; x < p.ntab; x++)
+            for (int s = 0; s < kMsdSegs; s++) Lt[x] += p.segL[x][s * kOffsA + a];
     // pass-B digit of bucket a over the bucket's key interval [lo, hi]:
-    // floor((key - lo) * kRadB / (hi - lo + 1)) as one mulhi, or key - lo
-    // when the interval holds fewer than kRadB keys
+    // floor((key - lo) * D / (hi - lo + 1)) as one mulhi, or key - lo
+    // when the interval holds fewer than kRadB keys.  D <= kRadB sub-buckets
+    // are sized so that whole numbers of them fill a final group: at C3
+    // 2 x 448 = 896 of 1024 rows instead of 2 x 381 = 762 with D = kRadB.
     int64_t lo = 0;
     uint64_t scale = 0;
     uint32_t maxspan = kRadB;
@@ -474,13 +481,24 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
         }
         const uint64_t range = hi > lo ? (uint64_t)hi - (uint64_t)lo : 0u;  // interval = range + 1 keys
         if (range >= (uint64_t)kRadB) {
-            const unsigned __int128 one73 = (unsigned __int128)1 << (64 + kBitsB);
-            const unsigned __int128 q = one73 / ((unsigned __int128)range + 1u);
+            // k sub-buckets of ~kFill / k rows fill a group; a bucket too big for
+            // k >= 2 gets lone sub-buckets of ~kOne rows, 6 standard deviations
+            // (uniform keys) below the cap: a multi-key sub-bucket over the cap
+            // would leave the LDS path for the (slow) LSD fallback
+            constexpr uint64_t kFill = (uint64_t)kGroupCap * 15 / 16, kOne = (uint64_t)kGroupCap * 13 / 16;
+            const uint64_t Lm = max(Lt[0], Lt[1]);
+            uint64_t D = kRadB;
+            if (Lm > 0 && !p.full_radix) {
+                const uint64_t k = (uint64_t)kRadB * kFill / Lm;
+                D = k >= 2 ? (Lm * k + kFill - 1) / kFill : (Lm + kOne - 1) / kOne;
+                D = min<uint64_t>(kRadB, max<uint64_t>(kRadB / 2, D));
+            }
+            const unsigned __int128 q = ((unsigned __int128)D << 64) / ((unsigned __int128)range + 1u);
             scale = q >> 64 ? ~0ull : (uint64_t)q;
-            // keys per sub-bucket <= ceil((range + 1) / kRadB) + 1 =: w.  Group spans stay
-            // within the final kernel's counting range when one sub-bucket fits it,
+            // keys per sub-bucket <= ceil((range + 1) / D) + 1 <= range / D + 2 =: w.  Group spans
+            // stay within the final kernel's counting range when one sub-bucket fits it,
             // else below 2^48 (the radix tiers' sort word)
-            const uint64_t w = (range >> kBitsB) + 2u;
+            const uint64_t w = range / D + 2u;
             const uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
             maxspan = span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
         }

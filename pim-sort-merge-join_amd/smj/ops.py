@@ -139,6 +139,13 @@ def msd_stats():
     return tuple(int(v) for v in out)
 
 
+def msd_groups():
+    """(dense groups, radix-tier groups, wide-tier groups) of the last MSD pipeline call."""
+    out = (ctypes.c_int64 * 3)()
+    _lib.load().smj_debug_msd_groups(out)
+    return tuple(int(v) for v in out)
+
+
 def biased_base(key_base):
     return int(key_base) & ((1 << 64) - 1)
 

@@ -28,6 +28,7 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     dist)  run dist 600 python -u -m pytest tests/test_dist_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     quick) run quick 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
+    qfull) SMJ_PASSB_FULL=1 run qfull 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
