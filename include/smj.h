@@ -276,6 +276,9 @@ static inline int smj_T_dev_sort_merge_join(const T *R, int64_t nr, int c1, int 
  * streamed without a sort, out4[1] = groups sorted / joined by the LSD
  * fallback, out4[2] / out4[3] = selected rows of R / S. */
 void smj_debug_msd_stats(int64_t *out4);
+/* Final-stage group counts of the last MSD pipeline call: out3[0] = LDS
+ * (dense) groups, out3[1] = radix-tier groups, out3[2] = 64-bit-tier groups. */
+void smj_debug_msd_groups(int64_t *out3);
 
 /* ---- profiling ---------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by hipEvents recorded on

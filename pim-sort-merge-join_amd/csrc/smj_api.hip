@@ -795,7 +795,7 @@ extern "C" int smj_debug_final_time(int dbg, int reps, float *ms) {
     return SMJ_OK;
 }
 
-// Diagnostic only (not part of smj.h): group counts of the last MSD pipeline.
+// Diagnostic: final-stage group counts of the last MSD pipeline (smj.h).
 extern "C" void smj_debug_msd_groups(int64_t *out3) {
     for (int i = 0; i < 3; i++) out3[i] = g_msd_groups[i];
 }
