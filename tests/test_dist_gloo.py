@@ -128,6 +128,7 @@ def make_tables(kind, n):
     (2, "uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 64, "stages": 1}),
     (3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8, "stages": 1}),
     (4, "dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 32, "stages": 8}),
+    (8, "uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 64}),
 ])
 def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
     _run_and_check(tmp_path, world, kind, cfg, 30_000)
@@ -145,6 +146,18 @@ def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, ki
     fused local smj_dev_sort_merge_join -- with 2 ranks sharing cuda:0 and the
     all_to_all staged through gloo (RCCL needs one GPU per rank)."""
     _run_and_check(tmp_path, 2, kind, cfg, 400_000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,cfg", [
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
+    ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True}),
+])
+def test_distributed_hip_eight_ranks_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
+    """The bench's N = 8 configuration (8 ranks, the default stage count:
+    W K - 1 = 15 splitters, 2 stages per rank) on the product operators, the
+    8 ranks sharing cuda:0 and the exchange staged through gloo."""
+    _run_and_check(tmp_path, 8, kind, cfg, 800_000)
 
 
 def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):
