@@ -432,7 +432,7 @@ struct MsdTabScratch {
 struct MsdScratch {
     int dev = -1;
     MsdTabScratch t[2];
-    int64_t *spl = nullptr;
+    int64_t *spl = nullptr, *samp = nullptr;
     MsdGroup *groups = nullptr, *slot_groups = nullptr;
     uint32_t *gpart = nullptr;  // group_sum partials
     uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr,
@@ -463,6 +463,7 @@ int msd_scratch(MsdScratch **out) {
     if (m.dev < 0) {
         m.dev = dev;
         HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
+        HIP_TRY(hipMalloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
         HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
@@ -488,7 +489,7 @@ void msd_free_all() {
         for (auto &t : m.t)
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
-        for (void *p : {(void *)m.spl, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
             hipFree(p);
         hipHostFree(m.h_plan);
@@ -588,7 +589,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
         SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
         SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * sizeof(uint16_t)));
-        SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4 + kMsdSegs * 4 * 16));
+        SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4 + kMsdSegs * 4 * 16 + 2 * kOffsA * 4));
         SMJ_TRY(grow(&ts.bk, &ts.c_bk, 256 * sizeof(MsdBucket)));
     }
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
@@ -597,12 +598,16 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     auto segL = [&](int x) { return (uint32_t *)ms->t[x].seg; };
     auto segC = [&](int x) { return (uint32_t *)ms->t[x].seg + kMsdSegs * kOffsA; };
     auto segMM = [&](int x) { return (int64_t *)((uint32_t *)ms->t[x].seg + 2 * kMsdSegs * kOffsA); };
+    auto segT = [&](int x, int c) {  // bucket totals (rows, runs), after the min / max partials
+        return (uint32_t *)(segMM(x) + 2 * kMsdSegs * 4) + c * kOffsA;
+    };
     {
         MsdSampleParams sp{};
         for (int x = 0; x < ntab; x++)
             sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val};
         sp.ntab = ntab;
         sp.spl = ms->spl;
+        sp.samp = ms->samp;
         ProfScope ps("msd_sample", 0, s);
         HIP_TRY(launch_msd_sample(sp, s));
     }
@@ -621,10 +626,18 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         for (int x = 0; x < ntab; x++)
             HIP_TRY(launch_msd_runs_seg((const uint32_t *)ms->t[x].offsA, tilesA[x], segL(x), segC(x),
                                         (const int64_t *)ms->t[x].tmm, segMM(x), s));
+        uint32_t *sa[4], *ta[4];
+        for (int x = 0; x < ntab; x++) {
+            sa[2 * x] = segL(x);
+            sa[2 * x + 1] = segC(x);
+            ta[2 * x] = segT(x, 0);
+            ta[2 * x + 1] = segT(x, 1);
+        }
+        HIP_TRY(launch_msd_seg_scan(sa, ta, 2 * ntab, s));
         MsdBasesParams bp{};
         for (int x = 0; x < ntab; x++) {
-            bp.segL[x] = segL(x);
-            bp.segC[x] = segC(x);
+            bp.totL[x] = segT(x, 0);
+            bp.totC[x] = segT(x, 1);
             bp.segmm[x] = segMM(x);
             bp.ntiles[x] = tilesA[x];
             bp.tile[x] = TB_[x];

@@ -182,6 +182,7 @@ struct MsdSampleParams {
     MsdTable tab[2];
     int ntab;
     int64_t *spl;        // out: kSplA splitters
+    int64_t *samp;       // scratch: 2 kSampleMax samples + per-block valid counts
 };
 struct MsdPartAParams {
     const int64_t *src;
@@ -216,8 +217,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t pad2;
 };
 struct MsdBasesParams {
-    const uint32_t *segL[2];
-    const uint32_t *segC[2];
+    const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)
+    const uint32_t *totC[2];
     const int64_t *segmm[2];   // [kMsdSegs * 4][2] min / max partials
     int64_t ntiles[2];
     int tile[2];
@@ -285,6 +286,7 @@ hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
 // per (segment, wave): segmm[kMsdSegs * 4][2] (256 entries, INT64_MAX / MIN when empty)
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
                                const int64_t *tmm, int64_t *segmm, hipStream_t s);
+hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int narr, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
 hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
                                  const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,

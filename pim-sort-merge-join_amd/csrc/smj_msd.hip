@@ -190,111 +190,87 @@ __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
 // ---------------------------------------------------------------------------
 // sample -> splitters
 // ---------------------------------------------------------------------------
-// bitonic compare-exchange step of distance J (< E: both elements in this
-// thread's registers) for sequence size k; element e of thread t is t*E + e
-template <int E, int J>
-__device__ __forceinline__ void bitonic_regs(int64_t (&v)[E], int tid, int k) {
-#pragma unroll
-    for (int e = 0; e < E; e++)
-        if ((e & J) == 0) {
-            const bool up = (((tid * E + e) & k) == 0);
-            const int64_t a = v[e], b = v[e | J];
-            if ((a > b) == up) {
-                v[e] = b;
-                v[e | J] = a;
-            }
+// Splitters in two launches.  Gather: sample j of table x (clusters of 16
+// consecutive rows spread evenly over the table: 16x fewer distinct pages,
+// i.e. TLB walks, than single rows) -> samp[x * kSampleMax + j], INT64_MAX
+// for a row the select drops or a missing row; per-block valid counts at
+// samp[kSampleN + block].  grid kSampleN / 256 x 256.
+constexpr int kSampleN = 2 * kSampleMax, kSampleGatherBlocks = kSampleN / 256;
+__global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleParams p) {
+    __shared__ uint32_t s_c[4];
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int x = j >= kSampleMax ? 1 : 0, jj = j - x * kSampleMax;
+    const MsdTable &t = p.tab[x];
+    int64_t k = INT64_MAX;
+    uint32_t valid = 0;
+    if (x < p.ntab && t.n > 0 && jj < min(t.n, (int64_t)kSampleMax)) {
+        constexpr int kSampleRun = 16, kClusters = kSampleMax / kSampleRun;
+        const int64_t r = t.n <= kSampleMax
+                              ? jj
+                              : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
+                                                 jj % kSampleRun);
+        const int64_t *row = t.src + r * t.cols;
+        const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
+        if (!t.use_sel || sv > t.sel_val) {
+            k = kv;
+            valid = 1;
         }
+    }
+    p.samp[j] = k;
+    uint32_t c = valid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) p.samp[kSampleN + blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
 }
 
-__global__ __launch_bounds__(1024) void msd_sample_kernel(const MsdSampleParams p) {
-    // bitonic sort of 2 x kSampleMax keys, E per thread in registers: steps
-    // with the partner in the same thread use registers, in the same wave
-    // __shfl_xor, and only those across waves (distance >= 64 E) go through
-    // LDS with barriers (10 of the 91 steps)
-    constexpr int N = 2 * kSampleMax, E = N / 1024;
-    static_assert(E == 8, "8 keys per thread");
-    __shared__ int64_t s_key[N];
-    __shared__ uint32_t s_wsum[16];
-    const int tid = threadIdx.x;
-    uint32_t valid = 0;
-    int64_t v[E];
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        const int j = tid * E + e;
-        int64_t k = INT64_MAX;
-        const int x = j >= kSampleMax ? 1 : 0;
-        const int jj = j - x * kSampleMax;
-        const MsdTable &t = p.tab[x];
-        if (x < p.ntab && t.n > 0) {
-            const int64_t ns = min(t.n, (int64_t)kSampleMax);
-            if (jj < ns) {
-                // clusters of kSampleRun consecutive rows spread evenly over the
-                // table: 16x fewer distinct pages (TLB walks) than single rows
-                constexpr int kSampleRun = 16, kClusters = kSampleMax / kSampleRun;
-                const int64_t r = t.n <= kSampleMax
-                                      ? jj
-                                      : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
-                                                         jj % kSampleRun);
-                const int64_t *row = t.src + r * t.cols;
-                if (!t.use_sel || row[t.sel_col] > t.sel_val) {
-                    k = row[t.key_col];
-                    valid++;
-                }
-            }
-        }
-        v[e] = k;
-    }
-    // valid sample count
+// Select: splitter i = the sample of sorted position at(i) = min(M - 1,
+// (i + 1) M / (kSplA + 1)) (M valid samples; the dropped ones hold INT64_MAX
+// and sort behind every valid key).  Sample i's position is its rank under
+// (key, index) -- a permutation -- counted against all kSampleN samples in
+// LDS: block b ranks samples [128 b, 128 b + 128), wave w = 64 of them (w & 1)
+// against 1/8 of the samples (w >> 1), every lane reading the same LDS word
+// (broadcast).  grid kSampleN / 128 x 1024.
+__global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSampleParams p) {
+    __shared__ int64_t s_key[kSampleN];
+    __shared__ uint32_t s_rank[8][128];
+    __shared__ uint32_t s_m;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     {
-        uint32_t c = valid;
+        const int4 *src = reinterpret_cast<const int4 *>(p.samp);
+        int4 *dst = reinterpret_cast<int4 *>(s_key);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if ((tid & 63) == 0) s_wsum[tid >> 6] = c;
+        for (int i = 0; i < kSampleN / 2 / 1024; i++) dst[tid + i * 1024] = src[tid + i * 1024];
+    }
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (int b = 0; b < kSampleGatherBlocks; b++) m += (uint32_t)p.samp[kSampleN + b];
+        s_m = m;
     }
     __syncthreads();
-    uint32_t M = 0;
-#pragma unroll
-    for (int w = 0; w < 16; w++) M += s_wsum[w];
-    // bitonic sort ascending (invalid samples are INT64_MAX: they sort behind every valid key)
-    for (int k = 2; k <= N; k <<= 1) {
-        for (int j = k >> 1; j >= E; j >>= 1) {
-            const int m = j / E;  // partner thread tid ^ m
-            const bool lower = (tid & m) == 0;
-            if (m >= 64) {
-#pragma unroll
-                for (int e = 0; e < E; e++) s_key[tid * E + e] = v[e];
-                __syncthreads();
-#pragma unroll
-                for (int e = 0; e < E; e++) {
-                    const int64_t o = s_key[(tid ^ m) * E + e];
-                    const bool up = (((tid * E + e) & k) == 0);
-                    v[e] = (lower == up) ? min(v[e], o) : max(v[e], o);
-                }
-                __syncthreads();
-            } else {
-#pragma unroll
-                for (int e = 0; e < E; e++) {
-                    const int64_t o = (int64_t)__shfl_xor((long long)v[e], m, 64);
-                    const bool up = (((tid * E + e) & k) == 0);
-                    v[e] = (lower == up) ? min(v[e], o) : max(v[e], o);
-                }
-            }
-        }
-        if (k >= 8) bitonic_regs<E, 4>(v, tid, k);
-        if (k >= 4) bitonic_regs<E, 2>(v, tid, k);
-        bitonic_regs<E, 1>(v, tid, k);
+    const uint32_t M = s_m;
+    const int li = 64 * (w & 1) + lane, i = blockIdx.x * 128 + li, part = w >> 1;
+    const int64_t my = s_key[i];
+    uint32_t r = 0;
+    const int j0 = part * (kSampleN / 8);
+#pragma unroll 8
+    for (int j = j0; j < j0 + kSampleN / 8; j++) {
+        const int64_t o = s_key[j];
+        r += (o < my || (o == my && j < i)) ? 1u : 0u;
     }
-#pragma unroll
-    for (int e = 0; e < E; e++) s_key[tid * E + e] = v[e];
+    s_rank[part][li] = r;
     __syncthreads();
-    if (tid < kSplA) {
-        int64_t s = INT64_MAX;
-        if (M > 0) {
-            const uint32_t at = min(M - 1, (uint32_t)(((uint64_t)(tid + 1) * M) / (kSplA + 1)));
-            s = s_key[at];
-        }
-        p.spl[tid] = s;
+    if (tid < 128) {
+        uint32_t rank = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) rank += s_rank[q][tid];
+        const int64_t key = s_key[blockIdx.x * 128 + tid];
+        if (M > 0 && rank < M)
+            for (int q = 0; q < kSplA; q++)
+                if (min(M - 1, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))) == rank) p.spl[q] = key;
     }
+    if (M == 0 && blockIdx.x == 0 && tid < kSplA) p.spl[tid] = INT64_MAX;
 }
 
 // ---------------------------------------------------------------------------
@@ -430,6 +406,44 @@ __global__ __launch_bounds__(256) void msd_runs_seg_kernel(const uint32_t *__res
     }
 }
 
+// The per-segment bucket partials of msd_runs_seg_kernel ([kMsdSegs][kOffsA],
+// rows or runs) become exclusive prefixes over the segments, in place, and
+// tot[a] = the bucket's total.  grid (kOffsA / 64, arrays) x 1024: lane =
+// bucket (coalesced), wave w = segments [w S, w S + S), S = kMsdSegs / 16,
+// all S loads of a lane in flight at once.
+struct MsdSegScanParams {
+    uint32_t *seg[4];
+    uint32_t *tot[4];
+};
+__global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanParams p) {
+    constexpr int NW = 16, S = kMsdSegs / NW;
+    static_assert(kMsdSegs % NW == 0 && kOffsA % 64 == 0, "segment / bucket split");
+    __shared__ uint32_t s_part[NW][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int a = blockIdx.x * 64 + lane;
+    uint32_t *seg = p.seg[blockIdx.y];
+    uint32_t v[S], sum = 0;
+#pragma unroll
+    for (int i = 0; i < S; i++) v[i] = seg[(w * S + i) * kOffsA + a];
+#pragma unroll
+    for (int i = 0; i < S; i++) sum += v[i];
+    s_part[w][lane] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+#pragma unroll
+    for (int u = 0; u < NW; u++) {
+        const uint32_t q = s_part[u][lane];
+        run += u < w ? q : 0u;
+        tot += q;
+    }
+#pragma unroll
+    for (int i = 0; i < S; i++) {
+        seg[(w * S + i) * kOffsA + a] = run;
+        run += v[i];
+    }
+    if (w == 0) p.tot[blockIdx.y][a] = tot;
+}
+
 // one workgroup of 256: thread = bucket.  Bucket sizes / bases of both
 // tables, the global key range, and the pass-B digit of every bucket.
 __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) {
@@ -460,8 +474,7 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
     // rows of bucket a per table
     uint32_t Lt[2] = {0u, 0u};
     if (a < kBucketsA)
-        for (int x = 0; x < p.ntab; x++)
-            for (int s = 0; s < kMsdSegs; s++) Lt[x] += p.segL[x][s * kOffsA + a];
+        for (int x = 0; x < p.ntab; x++) Lt[x] = p.totL[x][a];
     // pass-B digit of bucket a over the bucket's key interval [lo, hi]:
     // floor((key - lo) * D / (hi - lo + 1)) as one mulhi, or key - lo
     // when the interval holds fewer than kRadB keys.  D <= kRadB sub-buckets
@@ -504,12 +517,7 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
         }
     }
     for (int x = 0; x < p.ntab; x++) {
-        uint32_t L = 0, C = 0;
-        if (a < kBucketsA)
-            for (int s = 0; s < kMsdSegs; s++) {
-                L += p.segL[x][s * kOffsA + a];
-                C += p.segC[x][s * kOffsA + a];
-            }
+        const uint32_t L = a < kBucketsA ? p.totL[x][a] : 0u, C = a < kBucketsA ? p.totC[x][a] : 0u;
         const uint32_t K = (L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
         uint32_t totL, totC, totK;
         const uint32_t rs = block_excl_scan<4>(L, s_wsum, &totL);
@@ -563,11 +571,7 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
     partC[w][lane] = C;
     __syncthreads();
     if (!ok) return;
-    uint32_t P = 0, Q = 0;
-    for (int s = 0; s < (int)blockIdx.y; s++) {
-        P += segL[s * kOffsA + a];
-        Q += segC[s * kOffsA + a];
-    }
+    uint32_t P = segL[blockIdx.y * kOffsA + a], Q = segC[blockIdx.y * kOffsA + a];  // exclusive prefixes
     for (int v = 0; v < w; v++) {
         P += partL[v][lane];
         Q += partC[v][lane];
@@ -2420,7 +2424,8 @@ __global__ __launch_bounds__(1024) void msd_count_scan_kernel(const uint32_t *__
 // launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(msd_sample_kernel, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(msd_sample_gather_kernel, dim3(kSampleGatherBlocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(msd_sample_select_kernel, dim3(kSampleN / 128), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2436,6 +2441,16 @@ hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *s
     const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
     hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsA, kBucketsA, segL, segC, tmm,
                        segmm);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int narr, hipStream_t s) {
+    MsdSegScanParams p{};
+    for (int i = 0; i < narr; i++) {
+        p.seg[i] = seg[i];
+        p.tot[i] = tot[i];
+    }
+    hipLaunchKernelGGL(msd_seg_scan_kernel, dim3(kOffsA / 64, narr), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
