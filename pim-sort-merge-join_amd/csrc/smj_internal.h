@@ -158,7 +158,7 @@ constexpr int kBucketsA = 2 * kSplA + 1;   // 255 pass-A buckets (odd = one key 
 constexpr int kOffsA = 256;                // offsA row: 255 bucket starts + the tile's row count
 constexpr int kBitsB = 11;
 constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
-constexpr int kOffsB = kRadB + 1;          // offsB row (u16): 2048 starts + the tile's row count
+constexpr int kOffsB = kRadB + 8;          // offsB row (u16): 2048 starts + the tile's row count, padded to 16 B
 constexpr int kGroupCap = 1024;            // rows per table in one final group (LDS)
 constexpr int kStageRange = 4096;          // key range of the staged final path's counting sort
 constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots

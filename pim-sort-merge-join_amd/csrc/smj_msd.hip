@@ -881,13 +881,16 @@ __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams
         const uint32_t K = (bk.L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
         const uint32_t k0 = (uint32_t)(((uint64_t)K * sl) / kGroupSlices), k1 = (uint32_t)(((uint64_t)K * (sl + 1)) / kGroupSlices);
         const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
+        static_assert(SB == 8 && kOffsB % 8 == 0, "one 16-B load of 8 starts per row (rows 16-B aligned)");
 #pragma unroll 4
         for (uint32_t k = k0; k < k1; k++) {
             const uint16_t *r = o + (int64_t)k * kOffsB;
-            uint32_t prev = r[0];
+            const uint4 q = *reinterpret_cast<const uint4 *>(r);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint32_t prev = w[0] & 0xffffu;
 #pragma unroll
             for (int i = 0; i < SB; i++) {
-                const uint32_t nx = r[i + 1];
+                const uint32_t nx = i + 1 < SB ? (w[(i + 1) >> 1] >> (16 * ((i + 1) & 1))) & 0xffffu : (uint32_t)r[SB];
                 tot[i] += nx - prev;
                 prev = nx;
             }
@@ -2333,22 +2336,49 @@ __global__ __launch_bounds__(kMsdThreads) void msd_gather_kernel(const MsdTab tb
     });
 }
 
-// pack the join slots: dense group g has counts[g] rows at slot row outR
-// (persistent over the groups)
+// pack the join slots: dense group g has counts[g] rows at slot row outR.
+// One wave per group (persistent over the groups), 8 words per lane in
+// flight per round; the next group's count / slot / offset are loaded while
+// this one is copied.
 __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restrict__ slots,
                                                           const MsdGroup *__restrict__ groups,
                                                           const uint32_t *__restrict__ counts,
                                                           const uint32_t *__restrict__ offs,
                                                           const MsdPlan *__restrict__ plan, int tc,
                                                           int64_t *__restrict__ out) {
-    const int64_t ng = plan->ngroups;
-    for (int64_t g = blockIdx.x; g < ng; g += gridDim.x) {
-        const uint32_t c = counts[g];
-        if (c == 0) continue;
+    constexpr int U = 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t ng = plan->ngroups, step = (int64_t)gridDim.x * 4;
+    int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= ng) return;
+    uint32_t c = counts[g], o = offs[g], r = groups[g].outR;
+    for (; g < ng; g += step) {
+        const int64_t gn = g + step;
+        uint32_t cn = 0, on = 0, rn = 0;
+        if (gn < ng) {
+            cn = counts[gn];
+            on = offs[gn];
+            rn = groups[gn].outR;
+        }
         const int64_t nw = (int64_t)c * tc;
-        const int64_t *src = slots + (int64_t)groups[g].outR * tc;
-        int64_t *dst = out + (int64_t)offs[g] * tc;
-        for (int64_t i = threadIdx.x; i < nw; i += 256) dst[i] = src[i];
+        const int64_t *src = slots + (int64_t)r * tc;
+        int64_t *dst = out + (int64_t)o * tc;
+        for (int64_t i0 = 0; i0 < nw; i0 += 64 * U) {
+            int64_t v[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const int64_t i = i0 + k * 64 + lane;
+                if (i < nw) v[k] = src[i];
+            }
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const int64_t i = i0 + k * 64 + lane;
+                if (i < nw) dst[i] = v[k];
+            }
+        }
+        c = cn;
+        o = on;
+        r = rn;
     }
 }
 
