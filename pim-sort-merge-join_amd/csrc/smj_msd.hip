@@ -196,6 +196,7 @@ __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
 // for a row the select drops or a missing row; per-block valid counts at
 // samp[kSampleN + block].  grid kSampleN / 256 x 256.
 constexpr int kSampleN = 2 * kSampleMax, kSampleGatherBlocks = kSampleN / 256;
+static_assert(kSampleGatherBlocks <= 64, "one wave sums the gather blocks' valid counts");
 __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleParams p) {
     __shared__ uint32_t s_c[4];
     const int j = blockIdx.x * 256 + threadIdx.x;
@@ -229,12 +230,14 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
 // (i + 1) M / (kSplA + 1)) (M valid samples; the dropped ones hold INT64_MAX
 // and sort behind every valid key).  Sample i's position is its rank under
 // (key, index) -- a permutation -- counted against all kSampleN samples in
-// LDS: block b ranks samples [128 b, 128 b + 128), wave w = 64 of them (w & 1)
-// against 1/8 of the samples (w >> 1), every lane reading the same LDS word
-// (broadcast).  grid kSampleN / 128 x 1024.
+// LDS: block b ranks samples [32 b, 32 b + 32); lane & 31 picks the sample,
+// and 2 wave + (lane >> 5) one of 32 slices of kSampleN / 32 samples to
+// count against (two LDS words per wave read: broadcast).
+// grid kSampleN / 32 x 1024.
+constexpr int kSelSamples = 32, kSelSlices = 32;
 __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSampleParams p) {
     __shared__ int64_t s_key[kSampleN];
-    __shared__ uint32_t s_rank[8][128];
+    __shared__ uint32_t s_rank[kSelSlices][kSelSamples];
     __shared__ uint32_t s_m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     {
@@ -243,29 +246,31 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 #pragma unroll
         for (int i = 0; i < kSampleN / 2 / 1024; i++) dst[tid + i * 1024] = src[tid + i * 1024];
     }
-    if (tid == 0) {
-        uint32_t m = 0;
-        for (int b = 0; b < kSampleGatherBlocks; b++) m += (uint32_t)p.samp[kSampleN + b];
-        s_m = m;
+    if (tid < 64) {
+        uint32_t m = tid < kSampleGatherBlocks ? (uint32_t)p.samp[kSampleN + tid] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
+        if (tid == 0) s_m = m;
     }
     __syncthreads();
     const uint32_t M = s_m;
-    const int li = 64 * (w & 1) + lane, i = blockIdx.x * 128 + li, part = w >> 1;
+    const int li = lane & 31, i = blockIdx.x * kSelSamples + li, part = 2 * w + (lane >> 5);
     const int64_t my = s_key[i];
     uint32_t r = 0;
-    const int j0 = part * (kSampleN / 8);
+    constexpr int SL = kSampleN / kSelSlices;
+    const int j0 = part * SL;
 #pragma unroll 8
-    for (int j = j0; j < j0 + kSampleN / 8; j++) {
+    for (int j = j0; j < j0 + SL; j++) {
         const int64_t o = s_key[j];
         r += (o < my || (o == my && j < i)) ? 1u : 0u;
     }
     s_rank[part][li] = r;
     __syncthreads();
-    if (tid < 128) {
+    if (tid < kSelSamples) {
         uint32_t rank = 0;
 #pragma unroll
-        for (int q = 0; q < 8; q++) rank += s_rank[q][tid];
-        const int64_t key = s_key[blockIdx.x * 128 + tid];
+        for (int q = 0; q < kSelSlices; q++) rank += s_rank[q][tid];
+        const int64_t key = s_key[blockIdx.x * kSelSamples + tid];
         if (M > 0 && rank < M)
             for (int q = 0; q < kSplA; q++)
                 if (min(M - 1, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))) == rank) p.spl[q] = key;
@@ -829,12 +834,10 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         if (gn < ntl && (uint32_t)tid < runs_of(tin, bn, gn)) le = list64[tin.y + tid];  // prefetch 3: its runs
         if (!(p.dbg & 8)) {
             uint16_t *o = p.offs + g * kOffsB;
+            static_assert(kOffsB % 2 == 0, "offsB rows 4-B aligned: packed starts leave as u32 words");
 #pragma unroll
-            for (int k = 0; k < DPT / 2; k++) {  // thread t's starts
-                const uint32_t w = s_hist[DPT / 2 * tid + k];
-                o[DPT * tid + 2 * k] = (uint16_t)w;
-                o[DPT * tid + 2 * k + 1] = (uint16_t)(w >> 16);
-            }
+            for (int k = 0; k < DPT / 2; k++)  // thread t's starts, two per word as packed in s_hist
+                reinterpret_cast<uint32_t *>(o)[DPT / 2 * tid + k] = s_hist[DPT / 2 * tid + k];
             if (tid == 0) o[RADIX] = (uint16_t)nrows;
         }
         __syncthreads();
@@ -2455,7 +2458,7 @@ __global__ __launch_bounds__(1024) void msd_count_scan_kernel(const uint32_t *__
 // ---------------------------------------------------------------------------
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s) {
     hipLaunchKernelGGL(msd_sample_gather_kernel, dim3(kSampleGatherBlocks), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(msd_sample_select_kernel, dim3(kSampleN / 128), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(msd_sample_select_kernel, dim3(kSampleN / kSelSamples), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
