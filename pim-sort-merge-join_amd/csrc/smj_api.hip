@@ -435,6 +435,7 @@ struct MsdScratch {
     int64_t *spl = nullptr, *samp = nullptr;
     MsdGroup *groups = nullptr, *slot_groups = nullptr;
     uint32_t *gpart = nullptr;  // group_sum partials
+    uint32_t *cpart = nullptr;  // count_scan chunk sums
     uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr,
              *wide_list = nullptr, *radix_list = nullptr;
     MsdPlan *plan = nullptr, *h_plan = nullptr;
@@ -468,6 +469,7 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
         HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * 256));
+        HIP_TRY(hipMalloc(&m.cpart, sizeof(uint32_t) * 256));
         HIP_TRY(hipMalloc(&m.counts, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.single_list, sizeof(uint32_t) * kSlots));
@@ -489,7 +491,7 @@ void msd_free_all() {
         for (auto &t : m.t)
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
-        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
             hipFree(p);
         hipHostFree(m.h_plan);
@@ -709,7 +711,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     auto compact = [&]() -> int {
         {
             ProfScope ps("msd_count_scan", 0, s);
-            HIP_TRY(launch_msd_count_scan(ms->counts, ms->offs, ms->plan, s));
+            HIP_TRY(launch_msd_count_scan(ms->counts, ms->cpart, ms->offs, ms->plan, s));
         }
         ProfScope ps("msd_compact", 0, s);
         HIP_TRY(launch_msd_compact((const int64_t *)ms->slots, ms->groups, ms->counts, ms->offs, ms->plan, tc, out_j,

@@ -301,7 +301,8 @@ hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, cons
                               const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, hipStream_t s);
 hipError_t read_msd_phases(unsigned long long *out16);  // diagnostic (SMJ_DEBUG_MSD=1)
 // exclusive scan of the plan->ngroups dense group counts -> offs, total -> plan->joined
-hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *offs, MsdPlan *plan, hipStream_t s);
+hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *part, uint32_t *offs, MsdPlan *plan,
+                                 hipStream_t s);
 // exclusive scan of n u32 counts -> offs, total -> *total (one workgroup)
 hipError_t launch_count_scan(const uint32_t *counts, int64_t n, uint32_t *offs, int64_t *total, hipStream_t s);
 

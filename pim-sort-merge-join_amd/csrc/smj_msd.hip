@@ -2385,72 +2385,92 @@ __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restr
     }
 }
 
-// exclusive scan of the dense group counts (one workgroup of 1024, rounds of
-// 16 Ki staged through LDS); plan->joined = total
-__global__ __launch_bounds__(1024) void msd_count_scan_kernel(const uint32_t *__restrict__ counts,
-                                                              uint32_t *__restrict__ offs, MsdPlan *plan) {
-    // one workgroup; thread t owns 16 consecutive counts of a 16 Ki round,
-    // loaded / stored as 4 x 16 B, the next round's loads in flight during
-    // this round's scan
-    constexpr int PER = 16, ROUND = 1024 * PER;
-    __shared__ uint32_t s_w[16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t ng = plan->ngroups;
-    auto load = [&](int64_t base, uint32_t (&v)[PER]) {
-        const int64_t i0 = base + (int64_t)tid * PER;
-        if (i0 + PER <= ng) {
-            const uint4 *c4 = reinterpret_cast<const uint4 *>(counts + i0);
+// exclusive scan of the dense group counts in two launches over chunks of
+// kCountChunk groups (256 threads x 16): msd_count_part_kernel sums each
+// chunk, msd_count_scan_kernel adds the sums of the chunks before its own
+// (one wave) and scans its chunk; the chunk holding the last group writes
+// plan->joined = total.  grid kCountChunks x 256 (chunks past ngroups exit).
+constexpr int kCountPer = 16, kCountChunk = 256 * kCountPer;
+constexpr int kCountChunks = (kSlots + kCountChunk - 1) / kCountChunk;
+static_assert(kCountChunks <= 128, "one wave (2 sums per lane) adds the earlier chunks");
+__device__ __forceinline__ void count_load(const uint32_t *counts, int64_t ng, int64_t i0, uint32_t (&v)[kCountPer]) {
+    if (i0 + kCountPer <= ng) {
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(counts + i0);
 #pragma unroll
-            for (int q = 0; q < PER / 4; q++) {
-                const uint4 u = c4[q];
-                v[4 * q] = u.x;
-                v[4 * q + 1] = u.y;
-                v[4 * q + 2] = u.z;
-                v[4 * q + 3] = u.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < PER; k++) v[k] = i0 + k < ng ? counts[i0 + k] : 0u;
+        for (int q = 0; q < kCountPer / 4; q++) {
+            const uint4 u = c4[q];
+            v[4 * q] = u.x;
+            v[4 * q + 1] = u.y;
+            v[4 * q + 2] = u.z;
+            v[4 * q + 3] = u.w;
         }
-    };
-    uint32_t carry = 0, v[PER], nx[PER];
-    if (ng > 0) load(0, v);
-    for (int64_t base = 0; base < ng; base += ROUND) {
-        if (base + ROUND < ng) load(base + ROUND, nx);
-        uint32_t sum = 0;
+    } else {
 #pragma unroll
-        for (int k = 0; k < PER; k++) sum += v[k];
-        const uint32_t incl = wave_incl_scan(sum, lane);
-        if (lane == 63) s_w[wave] = incl;
-        __syncthreads();
-        uint32_t run = carry + incl - sum, all = 0;
-#pragma unroll
-        for (int w = 0; w < 16; w++) {
-            run += (w < wave) ? s_w[w] : 0u;
-            all += s_w[w];
-        }
-        __syncthreads();  // s_w reused next round
-        const int64_t i0 = base + (int64_t)tid * PER;
-        uint32_t o[PER];
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            o[k] = run;
-            run += v[k];
-        }
-        if (i0 + PER <= ng) {
-            uint4 *o4 = reinterpret_cast<uint4 *>(offs + i0);
-#pragma unroll
-            for (int q = 0; q < PER / 4; q++) o4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-        } else {
-#pragma unroll
-            for (int k = 0; k < PER; k++)
-                if (i0 + k < ng) offs[i0 + k] = o[k];
-        }
-        carry += all;
-#pragma unroll
-        for (int k = 0; k < PER; k++) v[k] = nx[k];
+        for (int k = 0; k < kCountPer; k++) v[k] = i0 + k < ng ? counts[i0 + k] : 0u;
     }
-    if (tid == 0) plan->joined = (int64_t)carry;
+}
+
+__global__ __launch_bounds__(256) void msd_count_part_kernel(const uint32_t *__restrict__ counts,
+                                                             uint32_t *__restrict__ part, const MsdPlan *plan) {
+    __shared__ uint32_t s_w[4];
+    const int64_t ng = plan->ngroups, c0 = (int64_t)blockIdx.x * kCountChunk;
+    if (c0 >= ng) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t v[kCountPer], sum = 0;
+    count_load(counts, ng, c0 + (int64_t)tid * kCountPer, v);
+#pragma unroll
+    for (int k = 0; k < kCountPer; k++) sum += v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) s_w[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0) part[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ __launch_bounds__(256) void msd_count_scan_kernel(const uint32_t *__restrict__ counts,
+                                                             const uint32_t *__restrict__ part,
+                                                             uint32_t *__restrict__ offs, MsdPlan *plan) {
+    __shared__ uint32_t s_w[4], s_base;
+    const int64_t ng = plan->ngroups, c0 = (int64_t)blockIdx.x * kCountChunk;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (ng == 0) {
+        if (blockIdx.x == 0 && tid == 0) plan->joined = 0;
+        return;
+    }
+    if (c0 >= ng) return;
+    const int64_t i0 = c0 + (int64_t)tid * kCountPer;
+    uint32_t v[kCountPer], sum = 0;
+    count_load(counts, ng, i0, v);
+    if (wave == 0) {
+        const int b = (int)blockIdx.x;
+        uint32_t e = (lane < b ? part[lane] : 0u) + (lane + 64 < b ? part[lane + 64] : 0u);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+        if (lane == 0) s_base = e;
+    }
+#pragma unroll
+    for (int k = 0; k < kCountPer; k++) sum += v[k];
+    const uint32_t incl = wave_incl_scan(sum, lane);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t run = s_base + incl - sum;
+    for (int w = 0; w < wave; w++) run += s_w[w];
+    uint32_t o[kCountPer];
+#pragma unroll
+    for (int k = 0; k < kCountPer; k++) {
+        o[k] = run;
+        run += v[k];
+    }
+    if (i0 + kCountPer <= ng) {
+        uint4 *o4 = reinterpret_cast<uint4 *>(offs + i0);
+#pragma unroll
+        for (int q = 0; q < kCountPer / 4; q++) o4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kCountPer; k++)
+            if (i0 + k < ng) offs[i0 + k] = o[k];
+    }
+    if (c0 + kCountChunk >= ng && tid == 255) plan->joined = (int64_t)run;  // thread 255 ends the chunk
 }
 
 // ---------------------------------------------------------------------------
@@ -2585,8 +2605,10 @@ hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, cons
     return hipGetLastError();
 }
 
-hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *offs, MsdPlan *plan, hipStream_t s) {
-    hipLaunchKernelGGL(msd_count_scan_kernel, dim3(1), dim3(1024), 0, s, counts, offs, plan);
+hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *part, uint32_t *offs, MsdPlan *plan,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(msd_count_part_kernel, dim3(kCountChunks), dim3(256), 0, s, counts, part, plan);
+    hipLaunchKernelGGL(msd_count_scan_kernel, dim3(kCountChunks), dim3(256), 0, s, counts, part, offs, plan);
     return hipGetLastError();
 }
 
