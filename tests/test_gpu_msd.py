@@ -64,6 +64,10 @@ FUSED_CASES = [
     (250_000, 250_000, 2, 2, 0, 0, "zipf", None, None),
     (33_333, 44_444, 5, 3, 4, 2, "wide", (0, 0), (1, 0)),
     (1_000_000, 1_000_000, 2, 2, 0, 0, "uniform", (0, 5000), (0, 5000)),
+    # WHERE keeps few rows: a handful of valid samples (repeated splitter
+    # positions), and none at all (every splitter INT64_MAX)
+    (200_000, 200_000, 2, 2, 0, 0, "uniform", (0, 599_000), (0, 590_000)),
+    (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 299_995), (0, 299_995)),
 ]
 
 
