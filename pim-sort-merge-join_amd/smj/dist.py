@@ -93,7 +93,8 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
     all_buf = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(all_cnt, cnt, group=group)
     dist.all_gather(all_buf, buf, group=group)
-    keys = torch.cat([b[: int(c.item())] for b, c in zip(all_buf, all_cnt)])
+    counts = torch.cat(all_cnt).tolist()  # one device -> host copy for all ranks' counts
+    keys = torch.cat([b[:c] for b, c in zip(all_buf, counts)])
     if keys.numel() == 0:
         return torch.zeros(parts - 1, dtype=torch.int64, device=home)
     keys = torch.sort(keys).values
