@@ -1888,6 +1888,7 @@ struct StSmem {
     };
     MsdGroup recs[2 * kStRecs];       // ring of this workgroup's group records
     uint32_t wsum[2][kStWaves];
+    uint32_t wlen[kStWaves];          // the next group's run-length scan (st_sort)
     uint32_t flag[2];
 };
 
@@ -1918,19 +1919,33 @@ __device__ unsigned long long g_st_sub[8];
         st_t = t_;                                                  \
     }
 
+__device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
+                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[2][kStIt],
+                                               StSmem &sm);
+
 // run lists from the offsB values (union region), then the row gathers of
 // group g into registers (row v = tid + k * kStThreads).  Row v's range is
 // found in O(1): the range holding the wave's first row (btab) and the last
 // non-empty range starting in (64b, v] (bitmap word + at[]).
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
     const uint32_t ex = block_excl_scan_nb<kStWaves>(len[0] | (len[1] << 16), sm.wsum[wsb], &tot);  // + barrier
     wsb ^= 1;
+    st_issue_lists(p, g, o0, o1, ex, rows, sm);
+}
+
+// st_issue after the run-length scan: ex = this thread's exclusive prefix of
+// (len R | len S << 16), the start bitmap zeroed and ordered by a barrier
+__device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
+                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[2][kStIt],
+                                               StSmem &sm) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         if (tid < g.kt[x] && x < p.ntab) {
@@ -1971,12 +1986,16 @@ __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key 
 // group is handed to the radix list)
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
-                                        uint32_t (&part)[kStIt]) {
-    const int tid = threadIdx.x;
+                                        uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
+                                        uint32_t &nex) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
     uint32_t w[2][kStIt], rank[2][kStIt];
     if (tid == 0) sm.flag[wsb] = 0;  // longest equal-key run (0: none)
+    // for the next group's st_issue_lists (the list region is idle until then;
+    // the barriers below order this before its atomicOr)
+    for (int i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -2008,8 +2027,23 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
         tot |= t << (16 * x);
     }
     if (mrun > 1u) atomicMax(&sm.flag[wsb], mrun);  // longest equal-key run
-    uint32_t all;
-    const uint32_t ex = block_excl_scan_nb<kStWaves>(tot, sm.wsum[wsb], &all);  // publishes flag[wsb]
+    // one barrier for two block scans: this group's bin totals and the next
+    // group's run lengths (len R | len S << 16); publishes flag[wsb]
+    const uint32_t lens = (no1[0] - no0[0]) | ((no1[1] - no0[1]) << 16);
+    const uint32_t i1 = wave_incl_scan(tot, lane), i2 = wave_incl_scan(lens, lane);
+    if (lane == 63) {
+        sm.wsum[wsb][wave] = i1;
+        sm.wlen[wave] = i2;
+    }
+    __syncthreads();
+    uint32_t b1 = 0, b2 = 0;
+#pragma unroll
+    for (int u = 0; u < kStWaves; u++) {
+        b1 += u < wave ? sm.wsum[wsb][u] : 0u;
+        b2 += u < wave ? sm.wlen[u] : 0u;
+    }
+    const uint32_t ex = b1 + i1 - tot;
+    nex = b2 + i2 - lens;
     const uint32_t fl = sm.flag[wsb];
     wsb ^= 1;
     ST_SUB(1);
@@ -2217,16 +2251,18 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
         }
         FIN_STAMP(1);
         uint32_t mmask = 0, part[kStIt];
-        const bool ok = st_sort(p, g, gi, cur, sm, wsb, mmask, part);  // cur is staged in LDS here
+        uint32_t nex;  // the next group's run-length prefix, scanned with this group's bins
+        const bool ok = st_sort(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex);  // cur is staged in LDS here
         FIN_STAMP(2);
-        // st_issue writes only the list region (unused by the sort) and the
-        // other wsum buffer, and its scan barrier orders the sort's last
-        // histogram reads before st_emit zeroes the histogram; st_emit writes
-        // `match` (aliasing the list) only after its own scan barrier, which
-        // every wave reaches after its st_issue reads.  Without st_issue one
-        // barrier does both.
+        // st_issue_lists writes only the list region (unused by the sort; its
+        // start bitmap was zeroed, and its run lengths scanned, inside
+        // st_sort), and its barrier orders the sort's last histogram reads
+        // before st_emit zeroes the histogram; st_emit writes `match`
+        // (aliasing the list) only after its own scan barrier, which every
+        // wave reaches after its st_issue_lists reads.  Without a next group
+        // one barrier does both.
         if (nfit)  // the next group's rows: in flight while this one is written out
-            st_issue(p, gn, o0, o1, cur, sm, wsb);
+            st_issue_lists(p, gn, o0, o1, nex, cur, sm);
         else
             __syncthreads();
         FIN_STAMP(3);
