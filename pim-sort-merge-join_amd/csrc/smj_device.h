@@ -27,6 +27,25 @@ __device__ __forceinline__ void load_row(const int64_t *__restrict__ p, int64_t 
     }
 }
 
+// store_row with nontemporal (streaming) stores: for tiles written once and
+// read back only by a later pass, after gigabytes of other traffic
+template <int COLS>
+__device__ __forceinline__ void store_row_nt(int64_t *__restrict__ p, const int64_t (&r)[COLS]) {
+    if constexpr (COLS % 2 == 0) {
+        i64x2 *q = reinterpret_cast<i64x2 *>(p);
+#pragma unroll
+        for (int c = 0; c < COLS / 2; c++) {
+            i64x2 t;
+            t.x = r[2 * c];
+            t.y = r[2 * c + 1];
+            __builtin_nontemporal_store(t, q + c);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < COLS; c++) __builtin_nontemporal_store(r[c], p + c);
+    }
+}
+
 template <int COLS>
 __device__ __forceinline__ void store_row(int64_t *__restrict__ p, const int64_t (&r)[COLS]) {
     if constexpr (COLS % 2 == 0) {

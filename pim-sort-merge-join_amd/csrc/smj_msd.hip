@@ -852,7 +852,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
                 const int s = min(tid + it * NT, nrows - 1);
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)s * COLS, r);
-                store_row<COLS>(dst + (size_t)s * COLS, r);
+                store_row_nt<COLS>(dst + (size_t)s * COLS, r);
             }
         }
         PB_STAMP(5);
@@ -2136,7 +2136,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 #pragma unroll
         for (int k = 0; k < kStIt; k++) {
             const int q = tid + k * kStThreads;
-            if (q < n[x]) dst[q] = sm.stage[x][sm.key[x][q] & IDX];
+            if (q < n[x]) __builtin_nontemporal_store(sm.stage[x][sm.key[x][q] & IDX], dst + q);  // final rows: streamed
         }
     }
     if (!p.join) return;
@@ -2169,7 +2169,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
                 const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
                 val = key2 ? r.x : r.y;
             }
-            dst[wd] = val;
+            __builtin_nontemporal_store(val, dst + wd);  // join slots: read back by msd_compact only
         }
     }
 }
