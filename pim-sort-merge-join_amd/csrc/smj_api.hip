@@ -31,7 +31,7 @@ extern "C" const char *smj_strerror(int code) {
     case SMJ_ERR_HIP: return "HIP runtime error";
     case SMJ_ERR_NOMEM: return "out of memory";
     case SMJ_ERR_NODEVICE: return "no usable gfx950 device";
-    case SMJ_ERR_TOO_LARGE: return "table too large (rows >= 2^30 or cols > 8)";
+    case SMJ_ERR_TOO_LARGE: return "table too large (rows >= 2^31 or cols > 8)";
     case SMJ_ERR_TIMEOUT: return "look-back wait timed out in a kernel";
     case SMJ_ERR_UNSUPPORTED: return "unsupported";
     default: return "unknown error";
@@ -194,15 +194,16 @@ int scratch(DevScratch **out) {
     HIP_TRY(hipGetDevice(&dev));
     DevScratch &s = g_scratch[dev];
     if (s.dev < 0) {
-        s.dev = dev;
         HIP_TRY(hipMalloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
         HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
         HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
+        HIP_TRY(hipMemset(s.ctr, 0, sizeof(Counters) * 8));
         HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 256));
         HIP_TRY(hipMalloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
         HIP_TRY(hipMalloc(&s.trash, sizeof(int64_t) * kSortThreads * 16));
         HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 256, hipHostMallocDefault));
+        s.dev = dev;  // only once every buffer exists
     }
     *out = &s;
     return SMJ_OK;
@@ -213,14 +214,6 @@ int check_table(int64_t n, int cols, int col_a, int col_b) {
         return SMJ_ERR_INVALID;
     if (cols > SMJ_MAX_COLS || n >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     return SMJ_OK;
-}
-
-// Look-back timeouts are reported by the kernels through Counters::err.
-int check_err(DevScratch *sc, int slot, hipStream_t s) {
-    uint32_t err = 0;
-    HIP_TRY(hipMemcpyAsync(&err, &sc->ctr[slot].err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return err ? SMJ_ERR_TIMEOUT : SMJ_OK;
 }
 }  // namespace
 
@@ -351,7 +344,6 @@ extern "C" int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int
     hipStream_t s = (hipStream_t)stream;
     SMJ_TRY(check_table(na, cols, key_col, key_col));
     SMJ_TRY(check_table(nb, cols, key_col, key_col));
-    if (na + nb >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     if (na + nb == 0) return SMJ_OK;
     if (!out || (na && !a) || (nb && !b)) return SMJ_ERR_INVALID;
     DevScratch *sc;
@@ -373,7 +365,6 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
     hipStream_t s = (hipStream_t)stream;
     SMJ_TRY(check_table(nr, c1, key1, key1));
     SMJ_TRY(check_table(ns, c2, key2, key2));
-    if (nr + ns >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     if (!d_out_rows) return SMJ_ERR_INVALID;
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
@@ -444,6 +435,8 @@ struct MsdScratch {
     void *work = nullptr;
     size_t c_work = 0;
     int64_t *d_tmp = nullptr;
+    int64_t *lspl = nullptr;    // partitioned mode: the part splitters (device)
+    int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
@@ -462,7 +455,6 @@ int msd_scratch(MsdScratch **out) {
     HIP_TRY(hipGetDevice(&dev));
     MsdScratch &m = g_msd[dev];
     if (m.dev < 0) {
-        m.dev = dev;
         HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
         HIP_TRY(hipMalloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
         HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
@@ -478,7 +470,10 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.radix_list, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
         HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
+        HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 64));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
+        m.dev = dev;  // only once every buffer exists (a failed call retries the allocation)
     }
     *out = &m;
     return SMJ_OK;
@@ -492,9 +487,11 @@ void msd_free_all() {
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
-                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp})
+                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp,
+                        (void *)m.lspl})
             hipFree(p);
         hipHostFree(m.h_plan);
+        hipHostFree(m.h_samp);
     }
     g_msd.clear();
 }
@@ -761,6 +758,122 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
     if (n > 0 && (!src || !out || src == out)) return SMJ_ERR_INVALID;
     return SMJ_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Partitioned mode (tables over kMsdSingleMax rows; BASELINE C4 / C5 on one
+// GPU).  One MSD pipeline call has 255 x 2048 sub-buckets of <= 1024 rows per
+// table, i.e. room for ~4e8 rows of well-spread keys; larger tables are first
+// range-partitioned on the key into P parts of <= kMsdPartRows rows per table
+// (smj_dev_partition: the WHERE clause + a stable bucket scatter, one read and
+// one write), and each part runs the pipeline in place.  Parts are disjoint,
+// ascending key ranges and sort + zip join are per-key operations, so part p's
+// sorted rows belong exactly where the partition put them (the exclusive
+// prefix of the part counts) and its joined rows follow part p - 1's: the
+// concatenation is cpu_app.c's result.  Splitters are weighted quantiles of a
+// key sample of both tables (a key never spans two parts).
+// ---------------------------------------------------------------------------
+constexpr int64_t kMsdSingleMax = (int64_t)1 << 28;  // rows per table of one pipeline call
+constexpr int64_t kMsdPartRows = 150000000;          // target rows per table and part
+
+int g_force_parts = 0;  // smj_debug_force_parts: the partitioned mode at any size (tests)
+
+int64_t msd_large_parts(const MsdIn *in, int ntab) {
+    if (g_force_parts > 0) return std::min(64, g_force_parts);
+    int64_t mx = 0;
+    for (int x = 0; x < ntab; x++) mx = std::max(mx, in[x].n);
+    return std::min<int64_t>(64, (mx + kMsdPartRows - 1) / kMsdPartRows);
+}
+
+int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s);
+
+int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+    MsdScratch *ms;
+    SMJ_TRY(msd_scratch(&ms));
+    const int64_t P = msd_large_parts(in, ntab);
+    // 1. a sample of the selected keys of every table (msd_sample_gather_kernel)
+    {
+        MsdSampleParams sp{};
+        for (int x = 0; x < ntab; x++)
+            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val};
+        sp.ntab = ntab;
+        sp.spl = ms->spl;
+        sp.samp = ms->samp;
+        ProfScope ps("msd_part_sample", 0, s);
+        HIP_TRY(launch_msd_sample_gather(sp, s));
+    }
+    HIP_TRY(hipMemcpyAsync(ms->h_samp, ms->samp, sizeof(int64_t) * (2 * kSampleMax + kSampleGatherBlocksH),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // 2. P - 1 splitters: weighted quantiles (a sample of table x stands for
+    // n_x / (its sample count) input rows; dropped rows are not samples)
+    std::vector<std::pair<int64_t, double>> kw;
+    double W = 0;
+    for (int x = 0; x < ntab; x++) {
+        const int64_t cnt = std::min<int64_t>(in[x].n, kSampleMax);
+        if (cnt == 0) continue;
+        const double w = (double)in[x].n / (double)cnt;
+        for (int64_t j = 0; j < cnt; j++) {
+            const int64_t k = ms->h_samp[x * kSampleMax + j];
+            if (k == INT64_MAX) continue;  // a row the select drops
+            kw.emplace_back(k, w);
+            W += w;
+        }
+    }
+    std::sort(kw.begin(), kw.end());
+    std::vector<int64_t> spl;
+    {
+        double acc = 0;
+        size_t i = 0;
+        for (int64_t p = 1; p < P && !kw.empty(); p++) {
+            const double target = W * (double)p / (double)P;
+            while (i + 1 < kw.size() && acc + kw[i].second < target) acc += kw[i++].second;
+            const int64_t k = kw[i].first;  // bucket(key) = #{splitters < key}: key k closes part p - 1
+            if (spl.empty() || spl.back() < k) spl.push_back(k);
+        }
+    }
+    const int nspl = (int)spl.size();
+    if (nspl) HIP_TRY(hipMemcpyAsync(ms->lspl, spl.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, s));
+    // 3. select + stable partition of every table straight into its output
+    // buffer (the parts are then sorted in place)
+    std::vector<int64_t> cnt[2], off[2];
+    for (int x = 0; x < ntab; x++) {
+        cnt[x].assign(nspl + 1, 0);
+        if (in[x].n)
+            SMJ_TRY(smj_dev_partition(in[x].src, in[x].n, in[x].cols, in[x].use_sel, in[x].sel_col, in[x].sel_val,
+                                      in[x].key, ms->lspl, nspl, in[x].out, cnt[x].data(), s));
+        off[x].assign(nspl + 2, 0);
+        for (int p = 0; p <= nspl; p++) off[x][p + 1] = off[x][p] + cnt[x][p];
+        h_rows[x] = off[x][nspl + 1];
+    }
+    // 4. the pipeline per part, in place
+    int64_t J = 0;
+    const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
+    for (int p = 0; p <= nspl; p++) {
+        MsdIn part[2];
+        int np = 0;
+        for (int x = 0; x < ntab; x++) {
+            if (cnt[x][p] == 0) continue;
+            T *base = in[x].out + off[x][p] * in[x].cols;
+            part[np++] = MsdIn{base, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
+        }
+        int64_t rows[3] = {0, 0, 0};
+        if (np == 2 && join) {
+            SMJ_TRY(msd_run(part, 2, 1, key2, out_j + J * tc, rows, s));
+            J += rows[2];
+        } else {
+            for (int i = 0; i < np; i++) SMJ_TRY(msd_run(&part[i], 1, 0, 0, nullptr, rows, s));
+        }
+    }
+    if (join) h_rows[2] = J;
+    return SMJ_OK;
+}
+
+// the pipeline, partitioned when a table exceeds one call's capacity
+int msd_any(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+    bool large = g_force_parts > 0;
+    for (int x = 0; x < ntab; x++) large |= in[x].n > kMsdSingleMax;
+    return large ? msd_large(in, ntab, join, key2, out_j, h_rows, s) : msd_run(in, ntab, join, key2, out_j, h_rows, s);
+}
 }  // namespace
 
 // Diagnostic only (not part of smj.h): re-run the last pipeline call's part_b
@@ -829,7 +942,7 @@ extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int
     if (n_rows == 0) return SMJ_OK;
     MsdIn t{in, n_rows, col_num, use_select, select_col, key_col, select_val, out};
     int64_t rows[3] = {0, 0, 0};
-    SMJ_TRY(msd_run(&t, 1, 0, 0, nullptr, rows, (hipStream_t)stream));
+    SMJ_TRY(msd_any(&t, 1, 0, 0, nullptr, rows, (hipStream_t)stream));
     *out_rows = rows[0];
     return SMJ_OK;
 }
@@ -842,7 +955,6 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
     h_rows[0] = h_rows[1] = h_rows[2] = 0;
     SMJ_TRY(msd_check(R, nr, c1, use_sel1, sel_col1, key1, R_sorted));
     SMJ_TRY(msd_check(S, ns, c2, use_sel2, sel_col2, key2, S_sorted));
-    if (nr + ns >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     if (nr > 0 && ns > 0 && !out) return SMJ_ERR_INVALID;
     hipStream_t s = (hipStream_t)stream;
     if (nr == 0 || ns == 0) {  // nothing to join: sort what there is
@@ -852,8 +964,12 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
     }
     const MsdIn t[2] = {{R, nr, c1, use_sel1, sel_col1, key1, sel_val1, R_sorted},
                         {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
-    return msd_run(t, 2, 1, key2, out, h_rows, s);
+    return msd_any(t, 2, 1, key2, out, h_rows, s);
 }
+
+// Diagnostic only (not part of smj.h): run every pipeline call in the
+// partitioned mode with `parts` parts (0 = automatic: tables over 2^28 rows).
+extern "C" void smj_debug_force_parts(int parts) { g_force_parts = parts > 0 ? parts : 0; }
 
 // ---------------------------------------------------------------------------
 // T = UINT64 / DOUBLE (common.h:3-9): the int64 pipeline
@@ -1149,7 +1265,7 @@ int need_init() {
 int check_block(const dpu_block_t *bl, const void *ptr) {
     if (!bl || bl->row_num < 0 || bl->col_num < 1) return SMJ_ERR_INVALID;
     if (bl->row_num > 0 && !ptr) return SMJ_ERR_INVALID;
-    if (bl->col_num > SMJ_MAX_COLS || bl->row_num >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
+    if (bl->col_num > SMJ_MAX_COLS) return SMJ_ERR_TOO_LARGE;  // row_num is an int: < SMJ_MAX_ROWS
     return SMJ_OK;
 }
 
@@ -1195,9 +1311,7 @@ extern "C" int smj_sort(const dpu_block_t *bl, T *rows, int key_col) {
     SMJ_TRY(smj_dev_select_sort((T *)din.p, bl->row_num, bl->col_num, 0, 0, 0, key_col, 0, (T *)dout.p, &m, s));
     HIP_TRY(hipMemcpyAsync(rows, dout.p, bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    DevScratch *sc;
-    SMJ_TRY(scratch(&sc));
-    return check_err(sc, 0, s);
+    return SMJ_OK;
 }
 
 extern "C" int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const T *b, int key_col,
@@ -1296,13 +1410,6 @@ extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, con
     if (j) HIP_TRY(hipMemcpyAsync(res, dout.p, (size_t)j * tc * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
-    DevScratch *sc;
-    SMJ_TRY(scratch(&sc));
-    int rc = check_err(sc, 0, st);
-    if (rc != SMJ_OK) {
-        free(res);
-        return rc;
-    }
     if (timing) {
         timing->cpu_gpu_ms = ev_ms(ev[0], ev[1]);
         timing->gpu_ms = ev_ms(ev[1], ev[2]);

@@ -281,6 +281,11 @@ struct MsdFinalParams {
 };
 
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
+// the sample gather alone: samp[x * kSampleMax + j] = sampled key j of table x
+// (INT64_MAX for a row the select drops or a missing row), samp[2 kSampleMax
+// + b] = valid samples of gather block b (blocks [0, 16) sample table 0)
+hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s);
+constexpr int kSampleGatherBlocksH = 2 * kSampleMax / 256;
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
 // per-bucket run sums and counts per segment; also the selected-key min / max
 // per (segment, wave): segmm[kMsdSegs * 4][2] (256 entries, INT64_MAX / MIN when empty)

@@ -2518,6 +2518,11 @@ hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(msd_sample_gather_kernel, dim3(kSampleGatherBlocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
     const unsigned grid = blocks_for(p.n, msd_tile(cols));

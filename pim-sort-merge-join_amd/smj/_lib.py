@@ -59,6 +59,7 @@ SIGNATURES = {
     "smj_zipf_zeta": (_D, [_L, _D]),
     "smj_debug_msd_stats": (None, [_PL]),
     "smj_debug_msd_groups": (None, [_PL]),
+    "smj_debug_force_parts": (None, [_I]),
     "smj_prof_enable": (None, [_I]),
     "smj_prof_report": (_I, [ctypes.c_char_p, ctypes.c_size_t]),
 }

@@ -59,12 +59,19 @@ class HipOps:
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
+def sample_index(n, samples, device=None):
+    """min(samples, n) row indices spread evenly over [0, n - 1], in exact
+    int64 arithmetic (a float32 linspace rounds n - 1 up to n above 2^24 rows
+    and would read past the table)."""
+    k = min(samples, n)
+    return torch.arange(k, dtype=torch.int64, device=device) * (n - 1) // max(k - 1, 1)
+
+
 def _sample_keys(table, key_col, samples):
     n = table.shape[0]
     if n == 0:
         return table.new_empty((0,))
-    idx = torch.linspace(0, n - 1, min(samples, n), device=table.device).round().long()
-    return table[idx, key_col].contiguous()
+    return table[sample_index(n, samples, table.device), key_col].contiguous()
 
 
 def _wire_device(t, group=None):

@@ -36,6 +36,18 @@ def _table(t, name):
     return t
 
 
+def _out(t, name, rows, cols, like, dtype=torch.int64):
+    """A caller-provided output buffer: the C layer trusts its capacity, so an
+    undersized, strided or foreign buffer is refused here."""
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == dtype and t.dim() == 2 and t.is_contiguous()):
+        raise ValueError(f"{name} must be a contiguous 2-D {dtype} CUDA tensor")
+    if t.device != like.device:
+        raise ValueError(f"{name} is on {t.device}, the inputs on {like.device}")
+    if t.shape[1] != cols or t.shape[0] < rows:
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, needs at least ({rows}, {cols})")
+    return t
+
+
 def select_sort(table, key_col=0, select_col=0, select_val=None, key_base=0, out=None, stream=None):
     """out[:m] <- stable sort on table[:, key_col] of the rows with
     table[:, select_col] > select_val (all rows when select_val is None).
@@ -43,8 +55,7 @@ def select_sort(table, key_col=0, select_col=0, select_val=None, key_base=0, out
     lib = _lib.load()
     _table(table, "table")
     n, cols = table.shape
-    if out is None:
-        out = torch.empty_like(table)
+    out = torch.empty_like(table) if out is None else _out(out, "out", n, cols, table)
     m = ctypes.c_int64(0)
     use = select_val is not None
     _lib.check(lib.smj_dev_select_sort(_ptr(table), n, cols, int(use), select_col,
@@ -58,8 +69,7 @@ def select_sort_lsd(table, key_col=0, select_col=0, select_val=None, key_base=0,
     lib = _lib.load()
     _table(table, "table")
     n, cols = table.shape
-    if out is None:
-        out = torch.empty_like(table)
+    out = torch.empty_like(table) if out is None else _out(out, "out", n, cols, table)
     m = ctypes.c_int64(0)
     use = select_val is not None
     _lib.check(lib.smj_dev_select_sort_lsd(_ptr(table), n, cols, int(use), select_col,
@@ -95,12 +105,14 @@ def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=N
     _table(S, "S")
     nr, c1 = R.shape
     ns, c2 = S.shape
-    if R_sorted is None:
-        R_sorted = torch.empty_like(R)
-    if S_sorted is None:
-        S_sorted = torch.empty_like(S)
+    if S.device != R.device:
+        raise ValueError("R and S must be on the same device")
+    R_sorted = torch.empty_like(R) if R_sorted is None else _out(R_sorted, "R_sorted", nr, c1, R)
+    S_sorted = torch.empty_like(S) if S_sorted is None else _out(S_sorted, "S_sorted", ns, c2, R)
     if out is None:
         out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=torch.int64, device=R.device)
+    else:
+        _out(out, "out", min(nr, ns), c1 + c2 - 1, R)
     rows = (ctypes.c_int64 * 3)()
     s1 = select1 or (0, 0)
     s2 = select2 or (0, 0)
@@ -117,10 +129,12 @@ def _sort_merge_join_typed(lib, R, S, key1, key2, select1, select2, R_sorted, S_
             raise ValueError(f"{name}: contiguous 2-D 8-byte CUDA tensor required")
     nr, c1 = R.shape
     ns, c2 = S.shape
-    R_sorted = torch.empty_like(R) if R_sorted is None else R_sorted
-    S_sorted = torch.empty_like(S) if S_sorted is None else S_sorted
+    R_sorted = torch.empty_like(R) if R_sorted is None else _out(R_sorted, "R_sorted", nr, c1, R, R.dtype)
+    S_sorted = torch.empty_like(S) if S_sorted is None else _out(S_sorted, "S_sorted", ns, c2, R, S.dtype)
     if out is None:
         out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=R.dtype, device=R.device)
+    else:
+        _out(out, "out", min(nr, ns), c1 + c2 - 1, R, R.dtype)
     rows = (ctypes.c_int64 * 3)()
     s1 = select1 or (0, 0)
     s2 = select2 or (0, 0)
@@ -146,6 +160,12 @@ def msd_groups():
     return tuple(int(v) for v in out)
 
 
+def force_parts(parts=0):
+    """Diagnostic: run every pipeline call in the partitioned mode with `parts`
+    key-range parts (0 = automatic: only tables over 2^28 rows are split)."""
+    _lib.load().smj_debug_force_parts(int(parts))
+
+
 def biased_base(key_base):
     return int(key_base) & ((1 << 64) - 1)
 
@@ -155,8 +175,7 @@ def select(table, select_col, select_val, out=None, stream=None):
     lib = _lib.load()
     _table(table, "table")
     n, cols = table.shape
-    if out is None:
-        out = torch.empty_like(table)
+    out = torch.empty_like(table) if out is None else _out(out, "out", n, cols, table)
     m = ctypes.c_int64(0)
     _lib.check(lib.smj_dev_select(_ptr(table), n, cols, select_col, int(select_val), _ptr(out),
                                   ctypes.byref(m), _stream(stream)), "smj_dev_select")
@@ -172,6 +191,8 @@ def merge(a, b, key_col=0, out=None, stream=None):
         raise ValueError("runs must have the same column count")
     if out is None:
         out = torch.empty((a.shape[0] + b.shape[0], a.shape[1]), dtype=torch.int64, device=a.device)
+    else:
+        _out(out, "out", a.shape[0] + b.shape[0], a.shape[1], a)
     _lib.check(lib.smj_dev_merge(_ptr(a), a.shape[0], _ptr(b), b.shape[0], a.shape[1], key_col, _ptr(out),
                                  _stream(stream)), "smj_dev_merge")
     return out
@@ -188,6 +209,8 @@ def join(R, S, key1=0, key2=0, out=None, count=None, sync=True, stream=None):
     tc = c1 + c2 - 1
     if out is None:
         out = torch.empty((max(min(nr, ns), 1), tc), dtype=torch.int64, device=R.device)
+    else:
+        _out(out, "out", min(nr, ns), tc, R)
     if count is None:
         count = torch.zeros(1, dtype=torch.int64, device=R.device)
     j = ctypes.c_int64(0)
@@ -224,6 +247,8 @@ def partition_scatter(table, splitters, counts, key_col=0, select_col=0, select_
     total = sum(counts)
     if out is None:
         out = torch.empty((max(total, 1), cols), dtype=torch.int64, device=table.device)
+    else:
+        _out(out, "out", total, cols, table)
     c = (ctypes.c_int64 * len(counts))(*counts)
     use = select_val is not None
     _lib.check(lib.smj_dev_partition_scatter(_ptr(table), n, cols, int(use), select_col,
@@ -242,6 +267,8 @@ def partition(table, splitters, key_col=0, select_col=0, select_val=None, out=No
     ns = int(splitters.numel())
     if out is None:
         out = torch.empty((max(n, 1), cols), dtype=torch.int64, device=table.device)
+    else:
+        _out(out, "out", n, cols, table)
     counts = (ctypes.c_int64 * (ns + 1))()
     use = select_val is not None
     _lib.check(lib.smj_dev_partition(_ptr(table), n, cols, int(use), select_col, int(select_val) if use else 0,

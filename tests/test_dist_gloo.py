@@ -170,6 +170,17 @@ def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):
     assert load < 1.10, load
 
 
+@pytest.mark.parametrize("n", [1, 2, 4095, 4096, 4097, 16_777_217, 50_000_000, 100_000_000, 2_000_000_000])
+def test_sample_index_stays_in_bounds(n):
+    """The splitter sample's row indices are exact int64 (a float32
+    linspace rounds n - 1 up to n above 2^24 rows)."""
+    from smj import dist as sdist
+    idx = sdist.sample_index(n, 4096)
+    assert idx.dtype == torch.int64 and idx.numel() == min(n, 4096)
+    assert int(idx.min()) == 0 and int(idx.max()) == n - 1
+    assert bool((idx[1:] > idx[:-1]).all()) if idx.numel() > 1 else True
+
+
 def test_stage_count():
     from smj import dist as sdist
     # 2 (W K - 1) boundaries must fit the 64-bucket partition kernel

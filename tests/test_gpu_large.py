@@ -1,0 +1,181 @@
+"""GPU parity of the partitioned mode (tables over 2^28 rows; BASELINE C4 and
+C5 on one MI355X) of smj_dev_sort_merge_join.
+
+* At small sizes the mode is forced (smj_debug_force_parts) and the outputs
+  are compared with the CPU oracle bit for bit.
+* At full size (C5: 1e8 x 1e9 Zipf(0.9); C4: 1e9 x 1e9 uniform) the outputs
+  are checked through size-independent properties:
+    - sorted tables: row count = the WHERE count, keys non-decreasing,
+      payloads (= input row ids) strictly increasing within equal keys, and
+      every output row equal to the input row its payload names -- together
+      exactly "the stable sort of the selected rows";
+    - joined rows: equal to a torch restatement of cpu_app.c's zip join
+      (:204-266) over the verified sorted tables: R position i with key k
+      pairs with S position lbS(k) + (i - lbR(k)) while that is < ubS(k);
+    - key windows (the heaviest key, and a ~1e6-row window) of the INPUT
+      tables, in input order, through the C oracle: sort and join are per-key
+      operations, so the window's oracle result must equal the output slices
+      holding its keys.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+from test_gpu_msd import dev, host, ref_pipeline, table  # noqa: E402
+
+SEL = 5000
+CHUNK = 100_000_000
+
+
+@pytest.fixture
+def parts():
+    from smj import ops
+    yield ops.force_parts
+    ops.force_parts(0)
+
+
+FORCED = [
+    # nr, ns, c1, c2, key1, key2, kind, select1, select2, parts
+    (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 5000), (0, 5000), 2),
+    (300_000, 200_000, 2, 2, 0, 0, "uniform", (0, 5000), (0, 5000), 7),
+    (250_000, 250_000, 2, 2, 0, 0, "zipf", None, None, 8),
+    (200_000, 150_000, 4, 5, 2, 4, "dom3", None, None, 5),
+    (70_000, 9_000, 3, 2, 1, 0, "dups", (2, -10), None, 3),
+    (120_000, 80_000, 2, 2, 0, 0, "extremes", None, None, 4),
+    (300_000, 300_000, 2, 2, 0, 0, "same", None, None, 6),
+    (40_000, 60_000, 8, 8, 7, 0, "wide", (0, 0), None, 16),
+    (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 299_995), (0, 299_995), 4),
+    (0, 50_000, 2, 2, 0, 0, "uniform", None, None, 3),
+]
+
+
+@pytest.mark.parametrize("nr,ns,c1,c2,k1,k2,kind,s1,s2,p", FORCED)
+def test_partitioned_mode_matches_oracle(gpu, oracle_built, parts, nr, ns, c1, c2, k1, k2, kind, s1, s2, p):
+    from smj import ops
+    parts(p)
+    rng = np.random.default_rng(nr * 3 + ns + p)
+    R = table(rng, nr, c1, kind, k1, 0)
+    S = table(rng, ns, c2, kind, k2, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R).reshape(nr, c1), dev(S).reshape(ns, c2), k1, k2, s1, s2)
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, s2)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, c1))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, c2))
+    if nr and ns:
+        np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
+
+
+def test_partitioned_select_sort_matches_oracle(gpu, oracle_built, parts):
+    from smj import ops
+    parts(5)
+    rng = np.random.default_rng(7)
+    t = table(rng, 400_000, 3, "dups", 1, 0)
+    got = ops.select_sort(dev(t), 1, 2, -20)
+    np.testing.assert_array_equal(host(got), oracle.select_sort(t, 1, 2, -20).reshape(-1, 3))
+
+
+# ---- full-size properties ----------------------------------------------------
+def check_sorted_selection(T, got, sel):
+    """got == the stable sort on column 0 of T's rows with column 0 > sel
+    (column 1 of T = the row id)."""
+    n = T.shape[0]
+    want = 0
+    for a in range(0, n, CHUNK):
+        want += int((T[a: a + CHUNK, 0] > sel).sum())
+    assert got.shape[0] == want
+    m = got.shape[0]
+    for a in range(0, m, CHUNK):
+        b = min(m, a + CHUNK + 1)
+        k, pay = got[a:b, 0], got[a:b, 1]
+        assert bool((k > sel).all())
+        dk = k[1:] - k[:-1]
+        assert bool((dk >= 0).all()), "keys out of order"
+        eq = dk == 0
+        assert bool((pay[1:][eq] > pay[:-1][eq]).all()), "equal keys out of input order"
+        assert torch.equal(T[got[a:b, 1]], got[a:b]), "an output row is not its input row"
+
+
+def check_join(gR, gS, gJ):
+    """gJ == the zip join of the (verified) sorted tables, restated in torch."""
+    kR = gR[:, 0].contiguous()
+    kS = gS[:, 0].contiguous()
+    off = 0
+    for a in range(0, kR.shape[0], CHUNK):
+        k = kR[a: a + CHUNK]
+        lbR = torch.searchsorted(kR, k, side="left")
+        occ = torch.arange(a, a + k.shape[0], device=k.device) - lbR
+        lbS = torch.searchsorted(kS, k, side="left")
+        ubS = torch.searchsorted(kS, k, side="right")
+        hit = occ < (ubS - lbS)
+        part = (lbS + occ)[hit]
+        want = torch.stack([gR[a: a + CHUNK, 0][hit], gR[a: a + CHUNK, 1][hit], gS[part, 1]], 1)
+        assert torch.equal(gJ[off: off + want.shape[0]], want), f"joined rows differ in R chunk at {a}"
+        off += want.shape[0]
+        del lbR, occ, lbS, ubS, hit, part, want
+    assert off == gJ.shape[0]
+
+
+def check_window(R, S, gR, gS, gJ, lo, hi):
+    """Input rows with lo <= key <= hi (input order) through the C oracle ==
+    the output slices holding those keys."""
+    def window_in(T):
+        m = (T[:, 0] >= lo) & (T[:, 0] <= hi)
+        return host(T[m])
+
+    def window_out(G):
+        k = G[:, 0].contiguous()
+        a = int(torch.searchsorted(k, torch.tensor([lo], device=k.device), side="left"))
+        b = int(torch.searchsorted(k, torch.tensor([hi], device=k.device), side="right"))
+        return host(G[a:b])
+
+    Rw, Sw = window_in(R), window_in(S)
+    Rs, Ss, J = ref_pipeline(Rw, Sw, 0, 0, (0, SEL), (0, SEL))
+    np.testing.assert_array_equal(window_out(gR), Rs)
+    np.testing.assert_array_equal(window_out(gS), Ss)
+    np.testing.assert_array_equal(window_out(gJ), J)
+    return len(Rs) + len(Ss), len(J)
+
+
+def run_full(R, S):
+    from smj import ops
+    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, SEL), (0, SEL))
+    torch.cuda.synchronize()
+    return gR, gS, gJ
+
+
+def test_c5_full_size_one_gpu(gpu, oracle_built):
+    """BASELINE C5 at full size on one MI355X: |R| = 1e8, |S| = 1e9,
+    Zipf(0.9) keys over 1e8 values (seeds 3 / 4), WHERE col0 > 5000."""
+    from smj import ops
+    R = ops.gen_zipf(100_000_000, seed=3, domain=100_000_000, theta=0.9)
+    S = ops.gen_zipf(1_000_000_000, seed=4, domain=100_000_000, theta=0.9)
+    gR, gS, gJ = run_full(R, S)
+    check_sorted_selection(R, gR, SEL)
+    check_sorted_selection(S, gS, SEL)
+    check_join(gR, gS, gJ)
+    # the heaviest key (single-key groups far over the LDS capacity) and a window
+    top = int(torch.mode(S[:1_000_000, 0]).values)
+    rows, j = check_window(R, S, gR, gS, gJ, top, top)
+    assert rows > 1_000_000 and j > 0
+    mid = gS.shape[0] // 2
+    check_window(R, S, gR, gS, gJ, int(gS[mid, 0]), int(gS[mid + 500_000, 0]))
+
+
+def test_c4_full_size_one_gpu(gpu, oracle_built):
+    """BASELINE C4's tables (1e9 x 1e9, keys iid uniform in [1, 3e9], seeds
+    1 / 2, WHERE col0 > 5000) on ONE MI355X through the partitioned mode."""
+    from smj import ops
+    n = 1_000_000_000
+    R = ops.gen_uniform(n, seed=1, key_range=3 * n)
+    S = ops.gen_uniform(n, seed=2, key_range=3 * n)
+    gR, gS, gJ = run_full(R, S)
+    check_sorted_selection(R, gR, SEL)
+    check_sorted_selection(S, gS, SEL)
+    check_join(gR, gS, gJ)
+    assert gJ.shape[0] > 0.2 * n
+    lo = int(gR[n // 3, 0])
+    rows, j = check_window(R, S, gR, gS, gJ, lo, lo + 1_500_000)
+    assert rows > 500_000 and j > 0
