@@ -20,8 +20,11 @@
  *     UINT64 / DOUBLE) reach the fused pipeline through the *_typed entry
  *     points; smj_sort_merge_join / smj_dev_sort_merge_join map to them;
  *   - row counts must be < 2^31 per table (dpu_block_t.row_num is an int,
- *     common.h:17) and col_num in [1, 8].  Tables over 2^28 rows are
- *     range-partitioned on the key inside the library.
+ *     common.h:17) and col_num in [1, 1024].  Tables over 1.6e8 rows are
+ *     range-partitioned on the key inside the library, tables over 8 columns
+ *     are sorted as (key, row id) pairs and gathered; the
+ *     LSD and partition entry points take 1..8 columns (else
+ *     SMJ_ERR_UNSUPPORTED).
  *
  * Two layers:
  *   smj_*      host pointers, exactly the reference's data flow (app.c);
@@ -50,11 +53,11 @@ extern "C" {
 #define SMJ_ERR_HIP (-2)          /* a HIP runtime call failed             */
 #define SMJ_ERR_NOMEM (-3)        /* device or host allocation failed      */
 #define SMJ_ERR_NODEVICE (-4)     /* no gfx950 device / smj_init missing   */
-#define SMJ_ERR_TOO_LARGE (-5)    /* row count >= 2^31 or too many columns */
+#define SMJ_ERR_TOO_LARGE (-5)    /* row count >= 2^31 or over 1024 columns */
 #define SMJ_ERR_TIMEOUT (-6)      /* an in-kernel look-back wait timed out */
 #define SMJ_ERR_UNSUPPORTED (-7)
 
-#define SMJ_MAX_COLS 8
+#define SMJ_MAX_COLS 1024  /* tables over 8 columns take the index-sort path */
 #define SMJ_MAX_ROWS ((int64_t)1 << 31)
 
 const char *smj_strerror(int code);

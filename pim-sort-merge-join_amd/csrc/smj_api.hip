@@ -31,7 +31,7 @@ extern "C" const char *smj_strerror(int code) {
     case SMJ_ERR_HIP: return "HIP runtime error";
     case SMJ_ERR_NOMEM: return "out of memory";
     case SMJ_ERR_NODEVICE: return "no usable gfx950 device";
-    case SMJ_ERR_TOO_LARGE: return "table too large (rows >= 2^31 or cols > 8)";
+    case SMJ_ERR_TOO_LARGE: return "table too large (rows >= 2^31 or cols > 1024)";
     case SMJ_ERR_TIMEOUT: return "look-back wait timed out in a kernel";
     case SMJ_ERR_UNSUPPORTED: return "unsupported";
     default: return "unknown error";
@@ -215,6 +215,18 @@ int check_table(int64_t n, int cols, int col_a, int col_b) {
     if (cols > SMJ_MAX_COLS || n >= SMJ_MAX_ROWS) return SMJ_ERR_TOO_LARGE;
     return SMJ_OK;
 }
+
+// Row kernels are instantiated for 1..8 columns; wider tables take the
+// index-sort path ((key, row id) pairs through the same kernels, then row
+// gathers) wherever an entry point offers it, else SMJ_ERR_UNSUPPORTED.
+constexpr int kDirectCols = 8;
+int direct_only(int cols) { return cols > kDirectCols ? SMJ_ERR_UNSUPPORTED : SMJ_OK; }
+
+// wide-row forms of the standalone select / merge / join (index-sort path, below)
+int idx_select(const T *in, int64_t n, int cols, int sel_col, T sel_val, T *out, int64_t *out_rows, hipStream_t s);
+int idx_merge(const T *a, int64_t na, const T *b, int64_t nb, int cols, int key_col, T *out, hipStream_t s);
+int idx_join(const T *R, int64_t nr, int c1, const T *S, int64_t ns, int c2, int key1, int key2, T *out,
+             int64_t *d_out_rows, int64_t *h_out_rows, hipStream_t s);
 }  // namespace
 
 // One scatter pass (chunk_hist -> chunk_scan -> chunk_scatter).  rows_out:
@@ -249,6 +261,7 @@ static int run_pass(DevScratch *sc, const PassSpec &ps, const uint32_t *base, Co
 static int lsd_select_sort(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
                            int key_col, uint64_t key_base, T *out, int64_t *out_rows, hipStream_t s) {
     SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    SMJ_TRY(direct_only(cols));
     if (!out_rows) return SMJ_ERR_INVALID;
     *out_rows = 0;
     if (n == 0) return SMJ_OK;
@@ -315,6 +328,7 @@ extern "C" int smj_dev_select(const T *in, int64_t n, int cols, int sel_col, T s
     *out_rows = 0;
     if (n == 0) return SMJ_OK;
     if (!in || !out || in == out) return SMJ_ERR_INVALID;
+    if (cols > kDirectCols) return idx_select(in, n, cols, sel_col, sel_val, out, out_rows, s);
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
     HIP_TRY(hipMemsetAsync(&sc->ctr[1], 0, sizeof(Counters), s));
@@ -346,6 +360,7 @@ extern "C" int smj_dev_merge(const T *a, int64_t na, const T *b, int64_t nb, int
     SMJ_TRY(check_table(nb, cols, key_col, key_col));
     if (na + nb == 0) return SMJ_OK;
     if (!out || (na && !a) || (nb && !b)) return SMJ_ERR_INVALID;
+    if (cols > kDirectCols) return idx_merge(a, na, b, nb, cols, key_col, out, s);
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
     const int64_t ntiles = (na + nb + kJoinTile - 1) / kJoinTile;
@@ -366,6 +381,10 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
     SMJ_TRY(check_table(nr, c1, key1, key1));
     SMJ_TRY(check_table(ns, c2, key2, key2));
     if (!d_out_rows) return SMJ_ERR_INVALID;
+    if ((c1 > kDirectCols || c2 > kDirectCols) && nr > 0 && ns > 0) {
+        if (!R || !S || !out) return SMJ_ERR_INVALID;
+        return idx_join(R, nr, c1, S, ns, c2, key1, key2, out, d_out_rows, h_out_rows, s);
+    }
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
     if (nr == 0 || ns == 0) {
@@ -772,7 +791,7 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
 // concatenation is cpu_app.c's result.  Splitters are weighted quantiles of a
 // key sample of both tables (a key never spans two parts).
 // ---------------------------------------------------------------------------
-constexpr int64_t kMsdSingleMax = (int64_t)1 << 28;  // rows per table of one pipeline call
+constexpr int64_t kMsdSingleMax = 160000000;  // rows per table of one pipeline call (<= 256 pass-B tiles per bucket)
 constexpr int64_t kMsdPartRows = 150000000;          // target rows per table and part
 
 int g_force_parts = 0;  // smj_debug_force_parts: the partitioned mode at any size (tests)
@@ -874,6 +893,118 @@ int msd_any(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     for (int x = 0; x < ntab; x++) large |= in[x].n > kMsdSingleMax;
     return large ? msd_large(in, ntab, join, key2, out_j, h_rows, s) : msd_run(in, ntab, join, key2, out_j, h_rows, s);
 }
+
+// ---------------------------------------------------------------------------
+// Index-sort path (col_num > 8 -- cpu_app.c's load_csv
+// takes any column count, :46-79, and join_in_cpu emits c1 + c2 - 1 of them,
+// :204-266).  The pipeline runs on 16-B (key, row id) pairs -- the 2-column
+// kernels whatever the width -- and whole rows are gathered once by id at
+// the end; joined rows are gathered from (key, R id, S id) triples.  Stable
+// order is preserved (ids ascend within a key).  For T = uint64 / double the
+// pair kernel compares keys and select values through the order-preserving
+// map, and the gathered rows are the input rows bit for bit.
+// ---------------------------------------------------------------------------
+struct IdxScratch {
+    void *pr[2] = {nullptr, nullptr}, *ps[2] = {nullptr, nullptr}, *jp = nullptr;
+    size_t cpr[2] = {0, 0}, cps[2] = {0, 0}, cjp = 0;
+};
+std::map<int, IdxScratch> g_idx;
+
+int idx_scratch(IdxScratch **out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    *out = &g_idx[dev];
+    return SMJ_OK;
+}
+
+void idx_free_all() {
+    for (auto &kv : g_idx) {
+        hipSetDevice(kv.first);
+        for (void *q : {kv.second.pr[0], kv.second.pr[1], kv.second.ps[0], kv.second.ps[1], kv.second.jp}) hipFree(q);
+    }
+    g_idx.clear();
+}
+
+// pairs of table x into ix->pr[x] (sel_val already mapped for ktype != 0)
+int idx_pairs(IdxScratch *ix, int x, const MsdIn &t, int ktype, int64_t row0, hipStream_t s) {
+    const size_t b = (size_t)std::max<int64_t>(1, t.n) * 16;
+    SMJ_TRY(grow(&ix->pr[x], &ix->cpr[x], b));
+    SMJ_TRY(grow(&ix->ps[x], &ix->cps[x], b));
+    ProfScope ps("idx_pairs", 8.0 * t.cols * t.n + 16.0 * t.n, s);
+    HIP_TRY(launch_row_pairs(t.src, t.n, t.cols, t.key, t.use_sel, t.sel_col, t.sel_val, ktype, row0,
+                             (int64_t *)ix->pr[x], s));
+    return SMJ_OK;
+}
+
+int msd_indexed(const MsdIn *in, int ntab, int join, int key2, int ktype, T *out_j, int64_t *h_rows, hipStream_t s) {
+    IdxScratch *ix;
+    SMJ_TRY(idx_scratch(&ix));
+    MsdIn pin[2];
+    for (int x = 0; x < ntab; x++) {
+        SMJ_TRY(idx_pairs(ix, x, in[x], ktype, 0, s));
+        pin[x] = MsdIn{(const T *)ix->pr[x], in[x].n, 2, 1, 1, (T)-1, 0, (T *)ix->ps[x]};  // keep id > -1
+    }
+    int64_t rows[3] = {0, 0, 0};
+    if (join) {
+        SMJ_TRY(grow(&ix->jp, &ix->cjp, (size_t)std::max<int64_t>(1, std::min(in[0].n, in[1].n)) * 24));
+        SMJ_TRY(msd_any(pin, 2, 1, 0, (T *)ix->jp, rows, s));
+    } else {
+        SMJ_TRY(msd_any(pin, ntab, 0, 0, nullptr, rows, s));
+    }
+    for (int x = 0; x < ntab; x++) {
+        h_rows[x] = rows[x];
+        ProfScope ps("idx_gather", 2.0 * 8.0 * in[x].cols * rows[x], s);
+        HIP_TRY(launch_gather_rows(in[x].src, in[x].n, nullptr, in[x].cols, (const int64_t *)ix->ps[x], 2, 1, rows[x],
+                                   in[x].out, s));
+    }
+    if (join) {
+        h_rows[2] = rows[2];
+        const int tc = in[0].cols + in[1].cols - 1;
+        ProfScope ps("idx_join_gather", 8.0 * (2 * tc + 3) * rows[2], s);
+        HIP_TRY(launch_join_gather(in[0].src, in[0].cols, in[1].src, in[1].cols, key2, (const int64_t *)ix->jp,
+                                   rows[2], out_j, s));
+    }
+    return SMJ_OK;
+}
+
+int idx_select(const T *in, int64_t n, int cols, int sel_col, T sel_val, T *out, int64_t *out_rows, hipStream_t s) {
+    IdxScratch *ix;
+    SMJ_TRY(idx_scratch(&ix));
+    SMJ_TRY(idx_pairs(ix, 0, MsdIn{in, n, cols, 1, sel_col, 0, sel_val, out}, SMJ_KEY_INT64, 0, s));
+    int64_t m = 0;
+    SMJ_TRY(smj_dev_select((const T *)ix->pr[0], n, 2, 1, (T)-1, (T *)ix->ps[0], &m, s));
+    HIP_TRY(launch_gather_rows(in, n, nullptr, cols, (const int64_t *)ix->ps[0], 2, 1, m, out, s));
+    *out_rows = m;
+    return SMJ_OK;
+}
+
+int idx_merge(const T *a, int64_t na, const T *b, int64_t nb, int cols, int key_col, T *out, hipStream_t s) {
+    IdxScratch *ix;
+    SMJ_TRY(idx_scratch(&ix));
+    SMJ_TRY(idx_pairs(ix, 0, MsdIn{a, na, cols, 0, 0, key_col, 0, out}, SMJ_KEY_INT64, 0, s));
+    SMJ_TRY(idx_pairs(ix, 1, MsdIn{b, nb, cols, 0, 0, key_col, 0, out}, SMJ_KEY_INT64, na, s));
+    SMJ_TRY(grow(&ix->jp, &ix->cjp, (size_t)(na + nb) * 16));
+    SMJ_TRY(smj_dev_merge((const T *)ix->pr[0], na, (const T *)ix->pr[1], nb, 2, 0, (T *)ix->jp, s));
+    HIP_TRY(launch_gather_rows(a, na, b, cols, (const int64_t *)ix->jp, 2, 1, na + nb, out, s));
+    return SMJ_OK;
+}
+
+int idx_join(const T *R, int64_t nr, int c1, const T *S, int64_t ns, int c2, int key1, int key2, T *out,
+             int64_t *d_out_rows, int64_t *h_out_rows, hipStream_t s) {
+    IdxScratch *ix;
+    SMJ_TRY(idx_scratch(&ix));
+    SMJ_TRY(idx_pairs(ix, 0, MsdIn{R, nr, c1, 0, 0, key1, 0, out}, SMJ_KEY_INT64, 0, s));
+    SMJ_TRY(idx_pairs(ix, 1, MsdIn{S, ns, c2, 0, 0, key2, 0, out}, SMJ_KEY_INT64, 0, s));
+    SMJ_TRY(grow(&ix->jp, &ix->cjp, (size_t)std::min(nr, ns) * 24));
+    int64_t J = 0;
+    SMJ_TRY(smj_dev_join((const T *)ix->pr[0], nr, 2, (const T *)ix->pr[1], ns, 2, 0, 0, (T *)ix->jp, d_out_rows, &J, s));
+    HIP_TRY(launch_join_gather(R, c1, S, c2, key2, (const int64_t *)ix->jp, J, out, s));
+    if (h_out_rows) {
+        HIP_TRY(hipStreamSynchronize(s));
+        *h_out_rows = J;
+    }
+    return SMJ_OK;
+}
 }  // namespace
 
 // Diagnostic only (not part of smj.h): re-run the last pipeline call's part_b
@@ -942,7 +1073,10 @@ extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int
     if (n_rows == 0) return SMJ_OK;
     MsdIn t{in, n_rows, col_num, use_select, select_col, key_col, select_val, out};
     int64_t rows[3] = {0, 0, 0};
-    SMJ_TRY(msd_any(&t, 1, 0, 0, nullptr, rows, (hipStream_t)stream));
+    if (col_num > kDirectCols)
+        SMJ_TRY(msd_indexed(&t, 1, 0, 0, SMJ_KEY_INT64, nullptr, rows, (hipStream_t)stream));
+    else
+        SMJ_TRY(msd_any(&t, 1, 0, 0, nullptr, rows, (hipStream_t)stream));
     *out_rows = rows[0];
     return SMJ_OK;
 }
@@ -964,11 +1098,12 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
     }
     const MsdIn t[2] = {{R, nr, c1, use_sel1, sel_col1, key1, sel_val1, R_sorted},
                         {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
+    if (c1 > kDirectCols || c2 > kDirectCols) return msd_indexed(t, 2, 1, key2, SMJ_KEY_INT64, out, h_rows, s);
     return msd_any(t, 2, 1, key2, out, h_rows, s);
 }
 
 // Diagnostic only (not part of smj.h): run every pipeline call in the
-// partitioned mode with `parts` parts (0 = automatic: tables over 2^28 rows).
+// partitioned mode with `parts` parts (0 = automatic: tables over 1.6e8 rows).
 extern "C" void smj_debug_force_parts(int parts) { g_force_parts = parts > 0 ? parts : 0; }
 
 // ---------------------------------------------------------------------------
@@ -1008,6 +1143,24 @@ extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_
     SMJ_TRY(msd_check((const T *)R, nr, c1, use_sel1, sel_col1, key1, (const T *)R_sorted));
     SMJ_TRY(msd_check((const T *)S, ns, c2, use_sel2, sel_col2, key2, (const T *)S_sorted));
     hipStream_t st = (hipStream_t)stream;
+    if (c1 > kDirectCols || c2 > kDirectCols) {  // index sort: the map is applied inside the pair kernel
+        if (nr > 0 && ns > 0 && !out) return SMJ_ERR_INVALID;
+        h_rows[0] = h_rows[1] = h_rows[2] = 0;
+        MsdIn t[2] = {{(const T *)R, nr, c1, use_sel1, sel_col1, key1, key_fwd_host(sel_bits1, key_type), (T *)R_sorted},
+                      {(const T *)S, ns, c2, use_sel2, sel_col2, key2, key_fwd_host(sel_bits2, key_type), (T *)S_sorted}};
+        if (nr > 0 && ns > 0) {
+            SMJ_TRY(msd_indexed(t, 2, 1, key2, key_type, (T *)out, h_rows, st));
+        } else {
+            int64_t rows[3] = {0, 0, 0};
+            for (int x = 0; x < 2; x++)
+                if (t[x].n) {
+                    SMJ_TRY(msd_indexed(&t[x], 1, 0, 0, key_type, nullptr, rows, st));
+                    h_rows[x] = rows[0];
+                }
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        return SMJ_OK;
+    }
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     TypedScratch &ts = g_typed[dev];
@@ -1039,6 +1192,7 @@ extern "C" int smj_dev_partition_count(const T *in, int64_t n, int cols, int use
                                        T *h_minmax, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    SMJ_TRY(direct_only(cols));
     if (n_split < 0 || n_split > kMaxSplitters || !h_counts || !h_minmax) return SMJ_ERR_INVALID;
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
@@ -1072,6 +1226,7 @@ extern "C" int smj_dev_partition_scatter(const T *in, int64_t n, int cols, int u
                                          const int64_t *h_counts, T *out, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    SMJ_TRY(direct_only(cols));
     if (n_split < 0 || n_split > kMaxSplitters || !h_counts || !out || in == out) return SMJ_ERR_INVALID;
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
@@ -1119,6 +1274,7 @@ extern "C" int smj_dev_partition(const T *in, int64_t n, int cols, int use_selec
                                  void *stream) {
     hipStream_t s = (hipStream_t)stream;
     SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    SMJ_TRY(direct_only(cols));
     if (n_split < 0 || n_split > kMaxSplitters || !h_counts) return SMJ_ERR_INVALID;
     for (int b = 0; b <= n_split; b++) h_counts[b] = 0;
     if (n == 0) return SMJ_OK;
@@ -1235,6 +1391,7 @@ extern "C" void smj_finalize(void) {
     }
     g_scratch.clear();
     msd_free_all();
+    idx_free_all();
     for (auto e : g_event_pool) hipEventDestroy(e);
     g_event_pool.clear();
     if (g_host_stream) {

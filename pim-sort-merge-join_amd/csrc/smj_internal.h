@@ -133,6 +133,14 @@ hipError_t read_phase_cycles(unsigned long long *out16);
 // columns onto int64 (inverse = 0) or back (inverse = 1); src may equal dst
 hipError_t launch_key_map(const int64_t *src, int64_t *dst, int64_t rows, int cols, uint32_t colmask, int ktype,
                           int inverse, hipStream_t s);
+// index-sort path for wide rows (smj_kernels.hip): (key, row id) pairs, row
+// gathers by id, joined rows from (key, R id, S id) triples
+hipError_t launch_row_pairs(const int64_t *src, int64_t n, int cols, int key, int use_sel, int sel_col,
+                            int64_t sel_val, int ktype, int64_t row0, int64_t *out, hipStream_t s);
+hipError_t launch_gather_rows(const int64_t *src0, int64_t n0, const int64_t *src1, int cols, const int64_t *ids,
+                              int id_stride, int id_col, int64_t m, int64_t *dst, hipStream_t s);
+hipError_t launch_join_gather(const int64_t *R, int c1, const int64_t *S, int c2, int key2, const int64_t *jp,
+                              int64_t J, int64_t *out, hipStream_t s);
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed,
                               uint64_t key_range, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
@@ -165,7 +173,10 @@ constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key or
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
-constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
+#ifndef SMJ_ST_GRID
+#define SMJ_ST_GRID 512
+#endif
+constexpr int kMsdStageGrid = SMJ_ST_GRID;  // persistent staged final kernel: 2 workgroups per CU
 constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = 256;              // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)

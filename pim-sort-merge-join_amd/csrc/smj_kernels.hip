@@ -1249,4 +1249,113 @@ hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t se
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// index-sort path for wide rows (col_num > 8, any T):
+// the pipeline runs on 16-B (key, row id) pairs and whole rows are gathered
+// once at the end, so a row of any width moves twice instead of six times
+// ---------------------------------------------------------------------------
+// pair r = (map(key), row0 + r), or (map(key), -1) when the WHERE predicate
+// (map(row[sel_col]) > sel_val, sel_val already mapped) drops the row: the
+// pipeline then selects on payload > -1.  ktype: 0 int64, 1 uint64, 2 double.
+__global__ __launch_bounds__(256) void row_pairs_kernel(const int64_t *__restrict__ src, int64_t n, int cols,
+                                                        int key, int use_sel, int sel_col, int64_t sel_val,
+                                                        int ktype, int64_t row0, i64x2 *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+        const int64_t *row = src + r * cols;
+        int64_t k = row[key];
+        bool keep = true;
+        if (use_sel) {
+            int64_t v = row[sel_col];
+            if (ktype) v = key_fwd(v, ktype);
+            keep = v > sel_val;
+        }
+        if (ktype) k = key_fwd(k, ktype);
+        i64x2 pr;
+        pr.x = k;
+        pr.y = keep ? row0 + r : -1;
+        out[r] = pr;
+    }
+}
+
+// dst row i = source row id(i) whole (id = ids[i * id_stride + id_col]); ids
+// below n0 name rows of src0, the others rows id - n0 of src1.  One thread
+// per output word: reads run along a source row, writes are coalesced.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restrict__ src0, int64_t n0,
+                                                          const int64_t *__restrict__ src1, int cols,
+                                                          const int64_t *__restrict__ ids, int id_stride, int id_col,
+                                                          int64_t m, uint32_t magic, int64_t *__restrict__ dst) {
+    constexpr int64_t kRowsPerBlock = 128;
+    for (int64_t b = blockIdx.x; b * kRowsPerBlock < m; b += gridDim.x) {
+        const int64_t r0 = b * kRowsPerBlock, rows = min(kRowsPerBlock, m - r0);
+        const uint32_t words = (uint32_t)(rows * cols);
+        for (uint32_t w = threadIdx.x; w < words; w += 256) {
+            const uint32_t i = cols > 1 ? __umulhi(w, magic) : w, c = w - i * (uint32_t)cols;
+            const int64_t id = ids[(r0 + i) * id_stride + id_col];
+            const int64_t *s = id < n0 ? src0 + id * cols : src1 + (id - n0) * cols;
+            dst[(r0 + i) * cols + c] = s[c];
+        }
+    }
+}
+
+// joined row j = R row jp[j].y (c1 words) then S row jp[j].z without key2;
+// jp rows are (key, R row id, S row id).  One thread per output word.
+__global__ __launch_bounds__(256) void join_gather_kernel(const int64_t *__restrict__ R, int c1,
+                                                          const int64_t *__restrict__ S, int c2, int key2,
+                                                          const int64_t *__restrict__ jp, int64_t J, uint32_t magic,
+                                                          int64_t *__restrict__ out) {
+    constexpr int64_t kRowsPerBlock = 128;
+    const int tc = c1 + c2 - 1;
+    for (int64_t b = blockIdx.x; b * kRowsPerBlock < J; b += gridDim.x) {
+        const int64_t r0 = b * kRowsPerBlock, rows = min(kRowsPerBlock, J - r0);
+        const uint32_t words = (uint32_t)(rows * tc);
+        for (uint32_t w = threadIdx.x; w < words; w += 256) {
+            const uint32_t i = tc > 1 ? __umulhi(w, magic) : w;
+            const int c = (int)(w - i * (uint32_t)tc);
+            const int64_t *t = jp + (r0 + i) * 3;
+            int64_t v;
+            if (c < c1) {
+                v = R[t[1] * c1 + c];
+            } else {
+                const int j = c - c1;
+                v = S[t[2] * c2 + j + (j >= key2 ? 1 : 0)];
+            }
+            out[(r0 + i) * tc + c] = v;
+        }
+    }
+}
+
+// floor(w / d) as __umulhi(w, magic): exact while w * (magic * d - 2^32) < 2^32,
+// i.e. for w < 128 * d with d <= 2^11 (one block's words)
+static uint32_t div_magic(int d) { return d > 1 ? (uint32_t)((0x100000000ull + d - 1) / d) : 0u; }
+
+hipError_t launch_row_pairs(const int64_t *src, int64_t n, int cols, int key, int use_sel, int sel_col,
+                            int64_t sel_val, int ktype, int64_t row0, int64_t *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, 256), 16384));
+    hipLaunchKernelGGL(row_pairs_kernel, dim3(grid), dim3(256), 0, s, src, n, cols, key, use_sel, sel_col, sel_val,
+                       ktype, row0, reinterpret_cast<i64x2 *>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const int64_t *src0, int64_t n0, const int64_t *src1, int cols, const int64_t *ids,
+                              int id_stride, int id_col, int64_t m, int64_t *dst, hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    if (cols > 1024) return hipErrorInvalidValue;  // 128 rows x cols words per block: div_magic stays exact
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(m, 128), 16384));
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid), dim3(256), 0, s, src0, n0, src1, cols, ids, id_stride, id_col,
+                       m, div_magic(cols), dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_join_gather(const int64_t *R, int c1, const int64_t *S, int c2, int key2, const int64_t *jp,
+                              int64_t J, int64_t *out, hipStream_t s) {
+    if (J <= 0) return hipSuccess;
+    if (c1 + c2 - 1 > 2047) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(J, 128), 16384));
+    hipLaunchKernelGGL(join_gather_kernel, dim3(grid), dim3(256), 0, s, R, c1, S, c2, key2, jp, J,
+                       div_magic(c1 + c2 - 1), out);
+    return hipGetLastError();
+}
+
 }  // namespace smj

@@ -166,6 +166,32 @@ def main():
     write("neg_s.csv", table(["k", "p"], ns))
     specs.append(("neg_wide", "neg_r.csv", "neg_s.csv", (0, -2**31 - 1, 0, -2**31 - 1, 0, 0)))
 
+    # rows wider than 8 columns (the index-sort path; cpu_app.c's load_csv
+    # takes any column count, :46-79): key and select columns not in column 0
+    rng2 = random.Random(20261016)
+    w12r = [[rng2.randint(-30, 30) for _ in range(12)] for _ in range(2500)]
+    w12s = [[rng2.randint(-30, 30) for _ in range(12)] for _ in range(2000)]
+    for i, r in enumerate(w12r):
+        r[0] = i  # row ids in a payload column: stability is visible
+    for i, r in enumerate(w12s):
+        r[1] = 10000 + i
+    write("w12_r.csv", table([f"r{c}" for c in range(12)], w12r))
+    write("w12_s.csv", table([f"s{c}" for c in range(12)], w12s, crlf=True))
+    w20r = [[rng2.randint(0, 999) for _ in range(20)] for _ in range(1500)]
+    w20s = [[rng2.randint(0, 999) for _ in range(9)] for _ in range(1800)]
+    for r in w20r:
+        r[19] = rng2.randint(100, 400)
+    for i, r in enumerate(w20s):
+        r[0] = rng2.randint(100, 400)
+        r[5] = i
+    write("w20_r.csv", table([f"c{c}" for c in range(20)], w20r))
+    write("w20_s.csv", table([f"d{c}" for c in range(9)], w20s))
+    specs += [
+        ("wide12", "w12_r.csv", "w12_s.csv", (3, -10, 11, -5, 5, 7)),
+        ("wide20_9", "w20_r.csv", "w20_s.csv", (0, 300, 4, 100, 19, 0)),
+        ("wide9_20", "w20_s.csv", "w20_r.csv", (4, 100, 0, 300, 0, 19)),
+    ]
+
     for name, i1, i2, cfg in specs:
         d1, d2 = unpack(i1, tmpdir), unpack(i2, tmpdir)
         out, rows = run_ref(d1, d2, cfg, tmpdir, name)

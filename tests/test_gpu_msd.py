@@ -68,6 +68,11 @@ FUSED_CASES = [
     # positions), and none at all (every splitter INT64_MAX)
     (200_000, 200_000, 2, 2, 0, 0, "uniform", (0, 599_000), (0, 590_000)),
     (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 299_995), (0, 299_995)),
+    # rows wider than 8 columns (index sort + row gathers)
+    (120_000, 90_000, 12, 9, 5, 8, "dups", (2, -10), (0, 0)),
+    (50_000, 70_000, 20, 2, 19, 0, "uniform", None, (0, 5000)),
+    (30_000, 30_000, 40, 17, 0, 16, "same", None, None),
+    (200_000, 200_000, 10, 10, 3, 3, "zipf", (1, 50), None),
 ]
 
 
@@ -184,6 +189,9 @@ TYPED_CASES = [
     (2, 200_000, 200_000, 2, 2, 0, 0, "double", (0, -1e6), (0, 0.0)),
     (2, 30_000, 40_000, 4, 3, 2, 1, "double_dups", (0, 0.5), None),
     (2, 25_000, 25_000, 3, 3, 1, 2, "double_dups", (1, -0.0), (0, -3.0)),
+    # wider than 8 columns: keys mapped inside the pair kernel, rows copied bit for bit (no -0.0 folding)
+    (1, 60_000, 40_000, 10, 9, 4, 8, "atoi", (0, 100), (2, 5)),
+    (2, 50_000, 50_000, 12, 12, 11, 0, "double_dups", (3, 0.5), None),
 ]
 
 
@@ -210,7 +218,7 @@ def test_typed_pipeline_matches_oracle(gpu, oracle_built, kt, nr, ns, c1, c2, k1
     Rs = oracle.select_sort_t(R, kt, k1, *(s1 or (0, None)))
     Ss = oracle.select_sort_t(S, kt, k2, *(s2 or (0, None)))
     J = oracle.join_t(Rs, Ss, kt, k1, k2)
-    if kt == 2:  # folded columns: keys and select columns
+    if kt == 2 and max(c1, c2) <= 8:  # folded columns: keys and select columns (direct path only)
         cR = {k1} | ({s1[0]} if s1 else set())
         cS = {k2} | ({s2[0]} if s2 else set())
         cJ = cR | {c1 + (c if c < k2 else c - 1) for c in cS if c != k2}

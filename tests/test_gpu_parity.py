@@ -53,6 +53,9 @@ SORT_CASES = [
     (70_000, 2, "extremes", 0, None), (50_000, 1, "wide", 0, None), (60_000, 3, "uniform", 2, (1, 1000)),
     (90_000, 4, "dups", 3, (2, -10)), (33_333, 5, "wide", 4, None), (40_000, 6, "uniform", 1, (5, 5000)),
     (20_000, 7, "dups", 6, None), (30_000, 8, "uniform", 5, (0, 90000)), (1_000_000, 2, "uniform", 0, (0, 5000)),
+    # wider than 8 columns: the index-sort path
+    (50_000, 9, "dups", 8, (3, 0)), (70_000, 12, "uniform", 4, None), (20_000, 33, "extremes", 31, (0, 0)),
+    (0, 16, "uniform", 0, None),
 ]
 
 
@@ -68,7 +71,7 @@ def test_select_sort_matches_oracle(gpu, oracle_built, n, cols, kind, key, sel):
 
 
 @pytest.mark.parametrize("n,cols,sel", [(0, 2, (0, 0)), (5000, 2, (0, 10)), (300_001, 3, (1, 0)),
-                                        (100_000, 4, (3, -10 ** 17))])
+                                        (100_000, 4, (3, -10 ** 17)), (80_000, 10, (9, 3)), (7_000, 25, (2, -40))])
 def test_select_matches_oracle(gpu, oracle_built, n, cols, sel):
     from smj import ops
     rng = np.random.default_rng(5)
@@ -81,7 +84,8 @@ def test_select_matches_oracle(gpu, oracle_built, n, cols, sel):
 
 @pytest.mark.parametrize("na,nb,cols,kmax", [(0, 10, 2, 5), (10, 0, 2, 5), (1, 1, 2, 1), (5000, 7000, 2, 20),
                                              (100_000, 33_333, 3, 1000), (4096, 4096, 1, 1 << 50),
-                                             (250_000, 250_000, 2, 7)])
+                                             (250_000, 250_000, 2, 7), (30_000, 50_000, 11, 100),
+                                             (0, 5_000, 9, 3)])
 def test_merge_matches_oracle(gpu, oracle_built, na, nb, cols, kmax):
     from smj import ops
     rng = np.random.default_rng(na + nb)
@@ -100,6 +104,8 @@ JOIN_CASES = [
     (100_000, 100_000, 2, 2, 0, 0, 300_000), (70_000, 9_000, 3, 2, 1, 0, 50), (9_000, 70_000, 2, 4, 0, 3, 50),
     (200_000, 150_000, 4, 5, 2, 4, 3), (40_000, 40_000, 1, 1, 0, 0, 1 << 60), (50_000, 60_000, 8, 8, 7, 0, 1000),
     (300_000, 300_000, 2, 2, 0, 0, 1),
+    # wider than 8 columns: joined through (key, row id) pairs
+    (60_000, 40_000, 9, 2, 3, 0, 500), (20_000, 30_000, 3, 14, 0, 13, 40), (10_000, 10_000, 20, 20, 19, 0, 5),
 ]
 
 
@@ -177,7 +183,7 @@ def sha(path):
 @pytest.mark.parametrize("case", ["bundled_100k", "test_10k", "test_10k_key1_sel2", "test_10k_key3_key2", "kat_all",
                                   "kat_sel100", "kat_default", "dup_heavy", "dup_heavy_sel", "empty_select",
                                   "all_same_key", "empty_table", "single_rows", "atoi_edge", "wide_mixed",
-                                  "neg_wide"])
+                                  "neg_wide", "wide12", "wide20_9", "wide9_20"])
 def test_smj_app_result_csv_bit_exact(gpu, manifest, golden_dir, tmp_path, case):
     """The C host (drop-in for app.c) on the reference's CSVs: result.csv
     byte-identical to the reference cpu_app.c output."""
@@ -285,7 +291,7 @@ def test_baseline_size_parity(gpu, oracle_built, n, kind):
 
 
 @pytest.mark.parametrize("binary,ktype", [("smj_app_u64", 1), ("smj_app_f64", 2)])
-@pytest.mark.parametrize("case", ["test_10k", "atoi_edge", "neg_wide", "dup_heavy_sel"])
+@pytest.mark.parametrize("case", ["test_10k", "atoi_edge", "neg_wide", "dup_heavy_sel", "wide12", "wide20_9"])
 def test_smj_app_typed_result_csv(gpu, oracle_built, manifest, golden_dir, tmp_path, binary, ktype, case):
     """The app.c drop-in built with common.h T = uint64_t / double: result.csv
     byte-identical to cpu_app.c's pipeline restated with the same T (atoi

@@ -1,0 +1,12 @@
+#!/bin/bash
+# tools/build_variant.sh NAME "-DFLAG=.. ..." -- build libsmj_hip.so with extra
+# compile flags into pim-sort-merge-join_amd/lib/variants/NAME/ (A/B runs load
+# it through SMJ_LIB=...).
+set -e
+NAME=$1; FLAGS=$2
+cd "$(dirname "$0")/../pim-sort-merge-join_amd"
+OUT=lib/variants/$NAME; mkdir -p $OUT build/v_$NAME
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value -I../include -Icsrc -Ihost $FLAGS"
+for f in smj_kernels smj_msd smj_api; do $H -c csrc/$f.hip -o build/v_$NAME/$f.o & done; wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libsmj_hip.so build/v_$NAME/*.o -Wl,-soname,libsmj_hip.so
+echo built $OUT/libsmj_hip.so

@@ -30,6 +30,8 @@ for s in $STEPS; do
     quick) run quick 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
     qfull) SMJ_PASSB_FULL=1 run qfull 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
     phases) run phases 300 python tools/msd_phases.py ;;
+    l3)    run l3 300 python tools/l3_probe.py ;;
+    large) run large 900 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     h2d)   run h2d 300 python tools/h2d_probe.py ;;
