@@ -83,11 +83,22 @@ typedef struct {
 
 /* ---- lifetime ----------------------------------------------------------- */
 /* Replaces dpu_alloc(NR_DPUS, profile, &set) (include/dpu/dpu.h:164; called
- * at app.c:175,315,422,638).  n_gpus <= 0 means "all visible".  Selects
- * device 0 for the host-pointer API.  Returns the number of GPUs in use
- * (>= 1) or a negative error. */
+ * at app.c:175,315,422,638): the device set of the host-pointer API is GPUs
+ * 0 .. n_gpus - 1 (n_gpus <= 0 or over the visible count: all visible).
+ * Returns the number of GPUs in the set (>= 1) or a negative error.  With
+ * more than one, smj_sort_merge_join and smj_sort shard their tables over
+ * every GPU of the set (range partition + one exchange over xGMI, one host
+ * worker thread per GPU); smj_select / smj_merge / smj_join run on the
+ * first. */
 int smj_init(int n_gpus);
-/* Replaces dpu_free(set) (include/dpu/dpu.h:189; app.c:307,402,503,761). */
+/* The device set as an explicit list of HIP device ids; an id may repeat
+ * (several shards on one GPU: tests the sharded path on one device).
+ * Returns n or a negative error. */
+int smj_init_devices(const int *device_ids, int n);
+/* Size of the current device set (0 before smj_init). */
+int smj_device_count(void);
+/* Replaces dpu_free(set) (include/dpu/dpu.h:189; app.c:307,402,503,761):
+ * releases the device set and every library-owned buffer. */
 void smj_finalize(void);
 /* Version string of the library build. */
 const char *smj_version(void);
@@ -284,6 +295,9 @@ void smj_debug_msd_stats(int64_t *out4);
 /* Final-stage group counts of the last MSD pipeline call: out3[0] = LDS
  * (dense) groups, out3[1] = radix-tier groups, out3[2] = 64-bit-tier groups. */
 void smj_debug_msd_groups(int64_t *out3);
+/* Run every pipeline call in the partitioned mode with `parts` key-range
+ * parts (tests); 0 = automatic (tables over 1.6e8 rows). */
+void smj_debug_force_parts(int parts);
 
 /* ---- profiling ---------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by hipEvents recorded on

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -68,6 +69,8 @@ struct ProfRec {
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
 std::vector<hipEvent_t> g_event_pool;
+std::mutex g_mu;  // scratch maps and profiler records (the host API drives devices from worker threads)
+thread_local int t_slot = -1;  // smj::set_scratch_slot
 
 hipEvent_t take_event() {
     if (!g_event_pool.empty()) {
@@ -88,13 +91,17 @@ struct ProfScope {
         if (!on) return;
         rec.name = name;
         rec.bytes = bytes;
-        rec.a = take_event();
-        rec.b = take_event();
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            rec.a = take_event();
+            rec.b = take_event();
+        }
         if (rec.a) hipEventRecord(rec.a, s);
     }
     ~ProfScope() {
         if (!on || !rec.a || !rec.b) return;
         hipEventRecord(rec.b, s);
+        std::lock_guard<std::mutex> lk(g_mu);
         g_prof.push_back(rec);
     }
 };
@@ -145,6 +152,7 @@ static std::string prof_json() {
 // Returns SMJ_OK after filling buf (and resetting the records), or the
 // buffer size needed (records kept) when buf is NULL / too small.
 extern "C" int smj_prof_report(char *buf, size_t buflen) {
+    std::lock_guard<std::mutex> lk(g_mu);
     const std::string out = prof_json();
     if (!buf || buflen < out.size() + 1) return (int)out.size() + 1;
     memcpy(buf, out.c_str(), out.size() + 1);
@@ -175,8 +183,14 @@ struct DevScratch {
     int64_t *h_small = nullptr;                      // pinned, 256 int64
 };
 std::map<int, DevScratch> g_scratch;
-int g_ngpus = 0;
-hipStream_t g_host_stream = nullptr;  // stream of the host-pointer API (device 0)
+
+// Scratch is per device, or per slot when a host worker thread set one: the
+// multi-device host API may run several pipelines on one physical device
+// (virtual devices, smj_init_devices) and they must not share buffers.
+int scratch_key(int *dev) {
+    if (hipGetDevice(dev) != hipSuccess) return -1;
+    return t_slot >= 0 ? (1 << 16) + t_slot : *dev;
+}
 
 int grow(void **p, size_t *cap, size_t need) {
     if (need <= *cap) return SMJ_OK;
@@ -191,8 +205,10 @@ int grow(void **p, size_t *cap, size_t need) {
 
 int scratch(DevScratch **out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    DevScratch &s = g_scratch[dev];
+    const int key = scratch_key(&dev);
+    if (key < 0) return SMJ_ERR_HIP;
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevScratch &s = g_scratch[key];
     if (s.dev < 0) {
         HIP_TRY(hipMalloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
         HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
@@ -471,8 +487,10 @@ MsdFinalParams g_fin_last{};  // last pipeline call's final launch (smj_debug_fi
 
 int msd_scratch(MsdScratch **out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    MsdScratch &m = g_msd[dev];
+    const int key = scratch_key(&dev);
+    if (key < 0) return SMJ_ERR_HIP;
+    std::lock_guard<std::mutex> lk(g_mu);
+    MsdScratch &m = g_msd[key];
     if (m.dev < 0) {
         HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
         HIP_TRY(hipMalloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
@@ -501,7 +519,8 @@ int msd_scratch(MsdScratch **out) {
 void msd_free_all() {
     for (auto &kv : g_msd) {
         MsdScratch &m = kv.second;
-        hipSetDevice(kv.first);
+        if (m.dev < 0) continue;
+        hipSetDevice(m.dev);
         for (auto &t : m.t)
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
                 hipFree(p);
@@ -525,8 +544,12 @@ struct MsdIn {            // one input table of the pipeline
 
 // Records the index of the last profiling record (to patch its byte count
 // once the row counts are known).
-size_t prof_last() { return g_prof.empty() ? (size_t)-1 : g_prof.size() - 1; }
+size_t prof_last() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_prof.empty() ? (size_t)-1 : g_prof.size() - 1;
+}
 void prof_set_bytes(size_t i, double bytes) {
+    std::lock_guard<std::mutex> lk(g_mu);
     if (g_prof_on && i < g_prof.size()) g_prof[i].bytes = bytes;
 }
 
@@ -588,6 +611,9 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
 // join, h_rows[2] the joined row count.  One stream synchronisation at the
 // end (plus one more round when oversized groups need the fallback).
 int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+    for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
+        SMJ_TRY(check_table(in[x].n, in[x].cols, in[x].use_sel ? in[x].sel_col : 0, in[x].key));
+    if (join && (ntab != 2 || key2 != in[1].key)) return SMJ_ERR_INVALID;
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
     int T_[2] = {1, 1}, TB_[2] = {1, 1};  // pass-A / pass-B tile rows
@@ -680,8 +706,10 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             ProfScope ps("msd_part_b", 0, s);
             HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s));
         }
-        g_pb_last[x] = PbLast{p, in[x].cols, maxB[x]};
-        g_pb_ntab = ntab;
+        if (t_slot < 0) {  // diagnostics of the calling thread's last pipeline (not the host API's workers)
+            g_pb_last[x] = PbLast{p, in[x].cols, maxB[x]};
+            g_pb_ntab = ntab;
+        }
         pb[x] = prof_last();
     }
     {
@@ -717,7 +745,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.ntab = ntab;
     fp.join = join;
     fp.key2 = key2;
-    g_fin_last = fp;
+    if (t_slot < 0) g_fin_last = fp;
     size_t pf;
     {
         ProfScope ps("msd_final", 0, s);
@@ -741,13 +769,15 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    g_msd_stats[0] = ms->h_plan->nsingle;
-    g_msd_stats[1] = ms->h_plan->nbig;
-    g_msd_stats[2] = ms->h_plan->m[0];
-    g_msd_stats[3] = ms->h_plan->m[1];
-    g_msd_groups[0] = ms->h_plan->ngroups;
-    g_msd_groups[1] = ms->h_plan->nradix;
-    g_msd_groups[2] = ms->h_plan->nwide;
+    if (t_slot < 0) {
+        g_msd_stats[0] = ms->h_plan->nsingle;
+        g_msd_stats[1] = ms->h_plan->nbig;
+        g_msd_stats[2] = ms->h_plan->m[0];
+        g_msd_stats[3] = ms->h_plan->m[1];
+        g_msd_groups[0] = ms->h_plan->ngroups;
+        g_msd_groups[1] = ms->h_plan->nradix;
+        g_msd_groups[2] = ms->h_plan->nwide;
+    }
     bool redo = false;
     SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
     if (redo) {
@@ -905,6 +935,7 @@ int msd_any(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
 // map, and the gathered rows are the input rows bit for bit.
 // ---------------------------------------------------------------------------
 struct IdxScratch {
+    int dev = -1;
     void *pr[2] = {nullptr, nullptr}, *ps[2] = {nullptr, nullptr}, *jp = nullptr;
     size_t cpr[2] = {0, 0}, cps[2] = {0, 0}, cjp = 0;
 };
@@ -912,14 +943,18 @@ std::map<int, IdxScratch> g_idx;
 
 int idx_scratch(IdxScratch **out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    *out = &g_idx[dev];
+    const int key = scratch_key(&dev);
+    if (key < 0) return SMJ_ERR_HIP;
+    std::lock_guard<std::mutex> lk(g_mu);
+    *out = &g_idx[key];
+    (*out)->dev = dev;
     return SMJ_OK;
 }
 
 void idx_free_all() {
     for (auto &kv : g_idx) {
-        hipSetDevice(kv.first);
+        if (kv.second.dev < 0) continue;
+        hipSetDevice(kv.second.dev);
         for (void *q : {kv.second.pr[0], kv.second.pr[1], kv.second.ps[0], kv.second.ps[1], kv.second.jp}) hipFree(q);
     }
     g_idx.clear();
@@ -942,7 +977,7 @@ int msd_indexed(const MsdIn *in, int ntab, int join, int key2, int ktype, T *out
     MsdIn pin[2];
     for (int x = 0; x < ntab; x++) {
         SMJ_TRY(idx_pairs(ix, x, in[x], ktype, 0, s));
-        pin[x] = MsdIn{(const T *)ix->pr[x], in[x].n, 2, 1, 1, (T)-1, 0, (T *)ix->ps[x]};  // keep id > -1
+        pin[x] = MsdIn{(const T *)ix->pr[x], in[x].n, 2, 1, 1, 0, (T)-1, (T *)ix->ps[x]};  // key 0, keep id > -1
     }
     int64_t rows[3] = {0, 0, 0};
     if (join) {
@@ -1116,10 +1151,21 @@ extern "C" void smj_debug_force_parts(int parts) { g_force_parts = parts > 0 ? p
 // ---------------------------------------------------------------------------
 namespace {
 struct TypedScratch {
+    int dev = -1;
     void *r = nullptr, *s = nullptr;
     size_t cr = 0, cs = 0;
 };
 std::map<int, TypedScratch> g_typed;
+
+void typed_free_all() {
+    for (auto &kv : g_typed) {
+        if (kv.second.dev < 0) continue;
+        hipSetDevice(kv.second.dev);
+        hipFree(kv.second.r);
+        hipFree(kv.second.s);
+    }
+    g_typed.clear();
+}
 
 int64_t key_fwd_host(uint64_t u, int ktype) {
     if (ktype == SMJ_KEY_UINT64) return (int64_t)(u ^ 0x8000000000000000ull);
@@ -1162,8 +1208,15 @@ extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_
         return SMJ_OK;
     }
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    TypedScratch &ts = g_typed[dev];
+    const int key = scratch_key(&dev);
+    if (key < 0) return SMJ_ERR_HIP;
+    TypedScratch *tsp;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        tsp = &g_typed[key];
+        tsp->dev = dev;
+    }
+    TypedScratch &ts = *tsp;
     SMJ_TRY(grow(&ts.r, &ts.cr, std::max<size_t>(1, (size_t)nr * c1 * 8)));
     SMJ_TRY(grow(&ts.s, &ts.cs, std::max<size_t>(1, (size_t)ns * c2 * 8)));
     const uint32_t mR = cols_mask(key1, use_sel1, sel_col1), mS = cols_mask(key2, use_sel2, sel_col2);
@@ -1356,223 +1409,26 @@ extern "C" int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t see
 }
 
 // ---------------------------------------------------------------------------
-// lifetime + host-pointer API (the app.c drop-in)
+// release of every library-owned buffer (smj_finalize, smj_host.hip)
 // ---------------------------------------------------------------------------
-extern "C" int smj_init(int n_gpus) {
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SMJ_ERR_NODEVICE;
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, 0));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        fprintf(stderr, "smj: device 0 is %s, this library is built for gfx950\n", prop.gcnArchName);
-        return SMJ_ERR_NODEVICE;
-    }
-    g_ngpus = (n_gpus <= 0 || n_gpus > count) ? count : n_gpus;
-    HIP_TRY(hipSetDevice(0));
-    if (!g_host_stream) HIP_TRY(hipStreamCreateWithFlags(&g_host_stream, hipStreamNonBlocking));
-    return g_ngpus;
-}
-
-extern "C" void smj_finalize(void) {
+void smj::api_free_all() {
+    std::lock_guard<std::mutex> lk(g_mu);
     for (auto &kv : g_scratch) {
         DevScratch &s = kv.second;
-        hipSetDevice(kv.first);
-        hipFree(s.tmp);
-        hipFree(s.status);
-        hipFree(s.apart);
-        hipFree(s.hist);
-        hipFree(s.plan);
-        hipFree(s.ctr);
-        hipFree(s.dcount);
-        hipFree(s.segsum);
-        hipFree(s.trash);
+        if (s.dev < 0) continue;
+        hipSetDevice(s.dev);
+        for (void *q : {s.tmp, s.status, s.apart, (void *)s.hist, (void *)s.plan, (void *)s.ctr, (void *)s.dcount,
+                        (void *)s.segsum, (void *)s.trash})
+            hipFree(q);
         hipHostFree(s.h_plan);
         hipHostFree(s.h_small);
     }
     g_scratch.clear();
     msd_free_all();
     idx_free_all();
+    typed_free_all();
     for (auto e : g_event_pool) hipEventDestroy(e);
     g_event_pool.clear();
-    if (g_host_stream) {
-        hipSetDevice(0);
-        hipStreamDestroy(g_host_stream);
-        g_host_stream = nullptr;
-    }
-    g_ngpus = 0;
 }
 
-namespace {
-// RAII device buffer for the host-pointer API
-struct DevBuf {
-    void *p = nullptr;
-    ~DevBuf() { if (p) hipFree(p); }
-    int alloc(size_t bytes) {
-        HIP_TRY(hipMalloc(&p, std::max<size_t>(bytes, 16)));
-        return SMJ_OK;
-    }
-};
-
-int need_init() {
-    if (g_ngpus <= 0) return SMJ_ERR_NODEVICE;
-    HIP_TRY(hipSetDevice(0));
-    return SMJ_OK;
-}
-
-int check_block(const dpu_block_t *bl, const void *ptr) {
-    if (!bl || bl->row_num < 0 || bl->col_num < 1) return SMJ_ERR_INVALID;
-    if (bl->row_num > 0 && !ptr) return SMJ_ERR_INVALID;
-    if (bl->col_num > SMJ_MAX_COLS) return SMJ_ERR_TOO_LARGE;  // row_num is an int: < SMJ_MAX_ROWS
-    return SMJ_OK;
-}
-
-double ev_ms(hipEvent_t a, hipEvent_t b) {
-    float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
-    return ms;
-}
-}  // namespace
-
-extern "C" int smj_select(const dpu_block_t *bl, const T *in, T *out, int select_col, T select_val,
-                          int *out_rows) {
-    SMJ_TRY(need_init());
-    SMJ_TRY(check_block(bl, in));
-    if (!out_rows || (bl->row_num > 0 && !out) || select_col < 0 || select_col >= bl->col_num)
-        return SMJ_ERR_INVALID;
-    const size_t bytes = (size_t)bl->row_num * bl->col_num * sizeof(T);
-    DevBuf din, dout;
-    SMJ_TRY(din.alloc(bytes));
-    SMJ_TRY(dout.alloc(bytes));
-    hipStream_t s = g_host_stream;
-    HIP_TRY(hipMemcpyAsync(din.p, in, bytes, hipMemcpyHostToDevice, s));
-    int64_t m = 0;
-    SMJ_TRY(smj_dev_select((T *)din.p, bl->row_num, bl->col_num, select_col, select_val, (T *)dout.p, &m, s));
-    HIP_TRY(hipMemcpyAsync(out, dout.p, (size_t)m * bl->col_num * sizeof(T), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    *out_rows = (int)m;
-    return SMJ_OK;
-}
-
-extern "C" int smj_sort(const dpu_block_t *bl, T *rows, int key_col) {
-    SMJ_TRY(need_init());
-    SMJ_TRY(check_block(bl, rows));
-    if (key_col < 0 || key_col >= bl->col_num) return SMJ_ERR_INVALID;
-    if (bl->row_num < 2) return SMJ_OK;
-    const size_t bytes = (size_t)bl->row_num * bl->col_num * sizeof(T);
-    DevBuf din, dout;
-    SMJ_TRY(din.alloc(bytes));
-    SMJ_TRY(dout.alloc(bytes));
-    hipStream_t s = g_host_stream;
-    HIP_TRY(hipMemcpyAsync(din.p, rows, bytes, hipMemcpyHostToDevice, s));
-    int64_t m = 0;
-    SMJ_TRY(smj_dev_select_sort((T *)din.p, bl->row_num, bl->col_num, 0, 0, 0, key_col, 0, (T *)dout.p, &m, s));
-    HIP_TRY(hipMemcpyAsync(rows, dout.p, bytes, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return SMJ_OK;
-}
-
-extern "C" int smj_merge(const dpu_block_t *bl1, const T *a, const dpu_block_t *bl2, const T *b, int key_col,
-                         T *out) {
-    SMJ_TRY(need_init());
-    SMJ_TRY(check_block(bl1, a));
-    SMJ_TRY(check_block(bl2, b));
-    if (bl1->col_num != bl2->col_num || key_col < 0 || key_col >= bl1->col_num) return SMJ_ERR_INVALID;
-    const int cols = bl1->col_num;
-    const int64_t na = bl1->row_num, nb = bl2->row_num;
-    if (na + nb == 0) return SMJ_OK;
-    if (!out) return SMJ_ERR_INVALID;
-    DevBuf da, db, dout;
-    SMJ_TRY(da.alloc((size_t)na * cols * 8));
-    SMJ_TRY(db.alloc((size_t)nb * cols * 8));
-    SMJ_TRY(dout.alloc((size_t)(na + nb) * cols * 8));
-    hipStream_t s = g_host_stream;
-    if (na) HIP_TRY(hipMemcpyAsync(da.p, a, (size_t)na * cols * 8, hipMemcpyHostToDevice, s));
-    if (nb) HIP_TRY(hipMemcpyAsync(db.p, b, (size_t)nb * cols * 8, hipMemcpyHostToDevice, s));
-    SMJ_TRY(smj_dev_merge((T *)da.p, na, (T *)db.p, nb, cols, key_col, (T *)dout.p, s));
-    HIP_TRY(hipMemcpyAsync(out, dout.p, (size_t)(na + nb) * cols * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return SMJ_OK;
-}
-
-extern "C" int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_, const T *S, int key1, int key2,
-                        T **out, int64_t *out_rows) {
-    SMJ_TRY(need_init());
-    SMJ_TRY(check_block(r, R));
-    SMJ_TRY(check_block(s_, S));
-    if (!out || !out_rows || key1 < 0 || key1 >= r->col_num || key2 < 0 || key2 >= s_->col_num)
-        return SMJ_ERR_INVALID;
-    const int c1 = r->col_num, c2 = s_->col_num, tc = c1 + c2 - 1;
-    const int64_t nr = r->row_num, ns = s_->row_num, cap = std::min(nr, ns);
-    DevBuf dr, ds, dout, dcnt;
-    SMJ_TRY(dr.alloc((size_t)nr * c1 * 8));
-    SMJ_TRY(ds.alloc((size_t)ns * c2 * 8));
-    SMJ_TRY(dout.alloc((size_t)cap * tc * 8));
-    SMJ_TRY(dcnt.alloc(sizeof(int64_t)));
-    hipStream_t st = g_host_stream;
-    if (nr) HIP_TRY(hipMemcpyAsync(dr.p, R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
-    if (ns) HIP_TRY(hipMemcpyAsync(ds.p, S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
-    int64_t j = 0;
-    SMJ_TRY(smj_dev_join((T *)dr.p, nr, c1, (T *)ds.p, ns, c2, key1, key2, (T *)dout.p, (int64_t *)dcnt.p, &j, st));
-    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
-    if (!res) return SMJ_ERR_NOMEM;
-    if (j) HIP_TRY(hipMemcpyAsync(res, dout.p, (size_t)j * tc * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    *out = res;
-    *out_rows = j;
-    return SMJ_OK;
-}
-
-extern "C" int smj_sort_merge_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_, const T *S,
-                                   int select_col1, T select_val1, int select_col2, T select_val2, int key1,
-                                   int key2, T **out, int64_t *out_rows, smj_timing_t *timing) {
-    return smj_sort_merge_join_typed(SMJ_KEY_INT64, r, R, s_, S, select_col1, (uint64_t)select_val1, select_col2,
-                                     (uint64_t)select_val2, key1, key2, (void **)out, out_rows, timing);
-}
-
-extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, const void *R, const dpu_block_t *s_,
-                                         const void *S, int select_col1, uint64_t sel_bits1, int select_col2,
-                                         uint64_t sel_bits2, int key1, int key2, void **out, int64_t *out_rows,
-                                         smj_timing_t *timing) {
-    SMJ_TRY(need_init());
-    SMJ_TRY(check_block(r, (const T *)R));
-    SMJ_TRY(check_block(s_, (const T *)S));
-    if (!out || !out_rows) return SMJ_ERR_INVALID;
-    const int c1 = r->col_num, c2 = s_->col_num, tc = c1 + c2 - 1;
-    if (key1 < 0 || key1 >= c1 || key2 < 0 || key2 >= c2 || select_col1 < 0 || select_col1 >= c1 ||
-        select_col2 < 0 || select_col2 >= c2)
-        return SMJ_ERR_INVALID;
-    const int64_t nr = r->row_num, ns = s_->row_num;
-    hipStream_t st = g_host_stream;
-    hipEvent_t ev[5];
-    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
-    struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 5; i++) hipEventDestroy(e[i]); } } evf{ev};
-    DevBuf dr, ds, drs, dss, dout, dcnt;
-    SMJ_TRY(dr.alloc((size_t)nr * c1 * 8));
-    SMJ_TRY(ds.alloc((size_t)ns * c2 * 8));
-    SMJ_TRY(drs.alloc((size_t)nr * c1 * 8));
-    SMJ_TRY(dss.alloc((size_t)ns * c2 * 8));
-    SMJ_TRY(dcnt.alloc(sizeof(int64_t)));
-    HIP_TRY(hipEventRecord(ev[0], st));
-    if (nr) HIP_TRY(hipMemcpyAsync(dr.p, R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
-    if (ns) HIP_TRY(hipMemcpyAsync(ds.p, S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipEventRecord(ev[1], st));
-    SMJ_TRY(dout.alloc((size_t)std::max<int64_t>(1, std::min(nr, ns)) * tc * 8));
-    int64_t rows[3] = {0, 0, 0};
-    SMJ_TRY(smj_dev_sort_merge_join_typed(key_type, dr.p, nr, c1, 1, select_col1, sel_bits1, key1, ds.p, ns, c2, 1,
-                                          select_col2, sel_bits2, key2, drs.p, dss.p, dout.p, rows, st));
-    const int64_t j = rows[2];
-    HIP_TRY(hipEventRecord(ev[2], st));
-    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
-    if (!res) return SMJ_ERR_NOMEM;
-    if (j) HIP_TRY(hipMemcpyAsync(res, dout.p, (size_t)j * tc * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipEventRecord(ev[3], st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (timing) {
-        timing->cpu_gpu_ms = ev_ms(ev[0], ev[1]);
-        timing->gpu_ms = ev_ms(ev[1], ev[2]);
-        timing->gpu_cpu_ms = ev_ms(ev[2], ev[3]);
-    }
-    *out = res;
-    *out_rows = j;
-    return SMJ_OK;
-}
+void smj::set_scratch_slot(int slot) { t_slot = slot; }

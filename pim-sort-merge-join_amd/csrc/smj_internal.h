@@ -173,10 +173,7 @@ constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key or
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
-#ifndef SMJ_ST_GRID
-#define SMJ_ST_GRID 512
-#endif
-constexpr int kMsdStageGrid = SMJ_ST_GRID;  // persistent staged final kernel: 2 workgroups per CU
+constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
 constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = 256;              // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
@@ -290,6 +287,13 @@ struct MsdFinalParams {
     uint32_t *radix_list;// groups for the radix tier (msd_final_kernel in list mode; nullptr = contiguous mode)
     int ntab, join, key2, dbg;
 };
+
+// ---- C-ABI internals shared by smj_api.hip and smj_host.hip -------------------
+// frees every library-owned device / pinned buffer (smj_finalize)
+void api_free_all();
+// worker threads of the multi-device host API give each device of the set its
+// own scratch (several may map to one physical device); -1 = per device
+void set_scratch_slot(int slot);
 
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 // the sample gather alone: samp[x * kSampleMax + j] = sampled key j of table x

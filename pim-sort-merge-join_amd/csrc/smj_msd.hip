@@ -1866,25 +1866,15 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
 // are gathered into registers while this one is sorted and written.  Groups
 // outside its limits (key span > kStageRange, an equal-key run >
 // kMaxDupRun, > kStList pass-B tiles) go to the radix list.
-constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 3 per CU (1024-thread workgroups: slower, r01z)
-#ifndef SMJ_ST_LIST
-#define SMJ_ST_LIST 512
-#endif
-#ifndef SMJ_ST_RECS
-#define SMJ_ST_RECS 64
-#endif
-constexpr int kStList = SMJ_ST_LIST;           // pass-B tiles per bucket and table a staged group may span
+constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 2 per CU (1024-thread workgroups: slower, r01z)
+constexpr int kStList = 512;                   // pass-B tiles per bucket and table a staged group may span
 constexpr int kStIt = kGroupCap / kStThreads;  // rows per table per thread
 constexpr int kStRange = kStageRange;
-constexpr int kStRecs = SMJ_ST_RECS;           // group records per LDS chunk (two chunks in flight)
+constexpr int kStRecs = 64;                    // group records per LDS chunk (two chunks in flight)
 static_assert(kFinIdxBits == 10, "sort word = residual << 10 | group row");
 
-// LDS: 50.6 KiB, three workgroups per CU (24 waves; the kernel is latency-
-// bound: one workgroup per CU instead of two cost +62 %, tools/final_ablate.py).
-// Only the payload column is staged: a row's key is the group base plus the
-// residual in its sort word.
 struct StSmem {
-    int64_t pay[2][kGroupCap];        // payload (non-key) column, gather order
+    i64x2 stage[2][kGroupCap];        // rows in gather order
     uint32_t key[2][kGroupCap];       // sort words, sorted
     uint32_t hist[2][kStRange / 2];   // packed u16 bins (zeroed for the next group during the emit)
     union {
@@ -2014,7 +2004,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             w[x][k] = ~0u;
             rank[x][k] = 0;
             if (v < n[x]) {
-                sm.pay[x][v] = p.tab[x].key ? rows[x][k].x : rows[x][k].y;
+                sm.stage[x][v] = rows[x][k];
                 const uint32_t res = (uint32_t)((uint64_t)st_key(rows[x][k], p.tab[x].key) - (uint64_t)g.base);
                 w[x][k] = (res << kFinIdxBits) | (uint32_t)v;
                 const uint32_t sh = 16u * (res & 1u);
@@ -2143,18 +2133,10 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         i64x2 *dst = reinterpret_cast<i64x2 *>(p.tab[x].out) + (x ? g.outS : g.outR);
-        const int kc = p.tab[x].key;
 #pragma unroll
         for (int k = 0; k < kStIt; k++) {
             const int q = tid + k * kStThreads;
-            if (q < n[x]) {
-                const uint32_t w = sm.key[x][q];
-                const int64_t key = g.base + (int64_t)(w >> kFinIdxBits), pay = sm.pay[x][w & IDX];
-                i64x2 r;
-                r.x = kc ? pay : key;
-                r.y = kc ? key : pay;
-                __builtin_nontemporal_store(r, dst + q);  // final rows: streamed
-            }
+            if (q < n[x]) __builtin_nontemporal_store(sm.stage[x][sm.key[x][q] & IDX], dst + q);  // final rows: streamed
         }
     }
     if (!p.join) return;
@@ -2170,7 +2152,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     __syncthreads();
     // output word wd = row * 3 + column: R key, R payload, S payload
     int64_t *dst = p.slots + (int64_t)g.outR * 3;
-    const int kc0 = p.tab[0].key;
+    const int key2 = p.key2;
     // fixed trip count (total <= kGroupCap), see st_load_recs
     constexpr int EMIT_IT = (3 * kGroupCap + kStThreads - 1) / kStThreads;
 #pragma unroll
@@ -2180,11 +2162,12 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
             const uint32_t row = wd / 3u, c = wd - row * 3u;
             const uint32_t m = sm.match[row];
             int64_t val;
-            if (c < 2) {  // R's columns: the key from the sort word, the payload staged
-                const uint32_t w = kR[m >> kFinIdxBits];
-                val = c == kc0 ? g.base + (int64_t)(w >> kFinIdxBits) : sm.pay[0][w & IDX];
-            } else {      // S's column other than key2: its payload
-                val = sm.pay[1][kS[m & IDX] & IDX];
+            if (c < 2) {
+                const i64x2 r = sm.stage[0][kR[m >> kFinIdxBits] & IDX];
+                val = c ? r.y : r.x;
+            } else {
+                const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
+                val = key2 ? r.x : r.y;
             }
             __builtin_nontemporal_store(val, dst + wd);  // join slots: read back by msd_compact only
         }
@@ -2214,10 +2197,7 @@ __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0
 // neighbours in key order: the pass-B tile lines and offsB lines two
 // neighbouring groups share are fetched into that XCD's L2 once.
 constexpr int kXcdSlots = 8;
-#ifndef SMJ_ST_MINW
-#define SMJ_ST_MINW 4
-#endif
-__global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
+__global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
@@ -2244,7 +2224,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
             if (li + kStRecs < cnt) st_load_recs(p, g0, gs, li + kStRecs, cnt, sm, (int)((c + 1) & 1));
             __syncthreads();
         }
-        const MsdGroup &g = sm.recs[li % (2 * kStRecs)];  // fields read from LDS where used (register pressure)
+        const MsdGroup g = sm.recs[li % (2 * kStRecs)];
         if (g.flags) {
             have = false;
             continue;
@@ -2262,9 +2242,10 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         }
         FIN_STAMP(0);
         bool nfit = false;
-        const MsdGroup &gn = sm.recs[(li + 1) % (2 * kStRecs)];
+        MsdGroup gn{};
         uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
         if (li + 1 < cnt) {
+            gn = sm.recs[(li + 1) % (2 * kStRecs)];
             nfit = st_ok(p, gn);
             if (nfit) st_load_offs(p, gn, o0, o1);
         }

@@ -3,6 +3,11 @@
  * (sort-merge-join/app.c).  Same command line (app.c:130-131):
  *
  *   smj_app data1.csv data2.csv [-o result.csv] [--select c1 v1 c2 v2] [--keys k1 k2]
+ *           [--gpus N | --devices i,j,...]
+ *
+ * --gpus N (default NR_GPUS, user.h) is the device set smj_init gets, the
+ * way NR_DPUS sizes dpu_alloc; --devices lists HIP device ids explicitly and
+ * may repeat one (the sharded path on a single GPU).
  *
  * Loads both CSVs with the reference's ingest semantics (app.c:153-159),
  * runs select -> sort -> merge -> join on the GPU through the C-ABI in
@@ -35,6 +40,7 @@ int main(int argc, char **argv)
     const char *in1 = NULL, *in2 = NULL, *out_path = "./data/result.csv";
     int sc1 = SELECT_COL1, sc2 = SELECT_COL2, k1 = JOIN_KEY1, k2 = JOIN_KEY2;
     long long sv1 = SELECT_VAL1, sv2 = SELECT_VAL2;
+    int ngpus = NR_GPUS, ndev = 0, devs[64];
     for (int i = 1; i < argc; i++) {
         if (!strcmp(argv[i], "-o") && i + 1 < argc) {
             out_path = argv[++i];
@@ -46,6 +52,10 @@ int main(int argc, char **argv)
         } else if (!strcmp(argv[i], "--keys") && i + 2 < argc) {
             k1 = atoi(argv[++i]);
             k2 = atoi(argv[++i]);
+        } else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) {
+            ngpus = atoi(argv[++i]);
+        } else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
+            for (char *t = strtok(argv[++i], ","); t && ndev < 64; t = strtok(NULL, ",")) devs[ndev++] = atoi(t);
         } else if (!in1) {
             in1 = argv[i];
         } else if (!in2) {
@@ -57,7 +67,7 @@ int main(int argc, char **argv)
     }
     if (!in1 || !in2) {
         fprintf(stderr, "usage: %s data1.csv data2.csv [-o result.csv] [--select c1 v1 c2 v2] "
-                        "[--keys k1 k2]\n", argv[0]);
+                        "[--keys k1 k2] [--gpus N | --devices i,j,...]\n", argv[0]);
         return 2;
     }
 
@@ -76,8 +86,9 @@ int main(int argc, char **argv)
     }
 
     /* dpu_alloc -> smj_init */
-    if (smj_init(NR_GPUS) < 1) {
-        fprintf(stderr, "smj_init: %s\n", smj_strerror(SMJ_ERR_NODEVICE));
+    const int got = ndev ? smj_init_devices(devs, ndev) : smj_init(ngpus);
+    if (got < 1) {
+        fprintf(stderr, "smj_init: %s\n", smj_strerror(got < 0 ? got : SMJ_ERR_NODEVICE));
         return EXIT_FAILURE;
     }
     dpu_block_t bl1 = {0, c1, r1}, bl2 = {1, c2, r2};
@@ -104,7 +115,7 @@ int main(int argc, char **argv)
     printf("-----------------------\n");
     printf("TOTAL %f\n", tm.cpu_gpu_ms + tm.gpu_ms + tm.gpu_cpu_ms);
     printf("#######################\n");
-    printf("rows %lld (csv load %.3f ms, save %.3f ms)\n\n", (long long)j, t_load, t_save);
+    printf("rows %lld on %d GPU(s) (csv load %.3f ms, save %.3f ms)\n\n", (long long)j, got, t_load, t_save);
 
     free(res);
     free(a);

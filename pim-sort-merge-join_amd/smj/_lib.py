@@ -35,6 +35,8 @@ SIGNATURES = {
     "smj_strerror": (ctypes.c_char_p, [_I]),
     "smj_version": (ctypes.c_char_p, []),
     "smj_init": (_I, [_I]),
+    "smj_init_devices": (_I, [_PI, _I]),
+    "smj_device_count": (_I, []),
     "smj_finalize": (None, []),
     "smj_select": (_I, [_P, _P, _P, _I, _L, _PI]),
     "smj_sort": (_I, [_P, _P, _I]),
