@@ -16,6 +16,10 @@ exchange runs in stages (key sub-ranges) overlapping the local sort + join
 of the previous stage (smj/dist.py).
 
 value = (|R| + |S| over all ranks) / max-over-ranks seconds per step.
+
+--workload c4 / c5 (single GPU, not the driver's default line) times the
+other BASELINE tables on ONE MI355X through the library's partitioned mode:
+C4's 1e9 x 1e9 uniform tables, C5's 1e8 x 1e9 Zipf(0.9) tables.
 """
 import argparse
 import json
@@ -48,6 +52,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per table per GPU")
+    p.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
+                   help="c3 (default, the metric's config); c4 / c5: BASELINE's 1e9-row tables on one GPU")
     p.add_argument("--cpu-sample", type=int, default=196608,
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
     p.add_argument("--cpu-mt", type=int, default=1,
@@ -78,14 +84,24 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     n = a.rows
+    if a.workload != "c3" and world > 1:
+        raise SystemExit("--workload c4 / c5 are single-GPU measurements")
+    if a.workload in ("c4", "c5"):
+        n = 1_000_000_000  # (C5: |S|)
     total = n * world
     key_range = 3 * total
-    R = ops.gen_uniform(n, row0=rank * n, seed=1, key_range=key_range, device=dev)
-    S = ops.gen_uniform(n, row0=rank * n, seed=2, key_range=key_range, device=dev)
+    if a.workload == "c5":
+        nr, ns = 100_000_000, 1_000_000_000
+        R = ops.gen_zipf(nr, seed=3, domain=100_000_000, theta=0.9, device=dev)
+        S = ops.gen_zipf(ns, seed=4, domain=100_000_000, theta=0.9, device=dev)
+    else:
+        nr = ns = n
+        R = ops.gen_uniform(n, row0=rank * n, seed=1, key_range=key_range, device=dev)
+        S = ops.gen_uniform(n, row0=rank * n, seed=2, key_range=key_range, device=dev)
     bufs = None
     if world == 1:
         bufs = {"R": torch.empty_like(R), "S": torch.empty_like(S),
-                "J": torch.empty((n, 3), dtype=torch.int64, device=dev)}
+                "J": torch.empty((min(nr, ns), 3), dtype=torch.int64, device=dev)}
     torch.cuda.synchronize()
 
     lb = {}
@@ -129,7 +145,7 @@ def main():
         joined = int(tt[1].item())
         dt = float(t[0].item())
     ms_step = dt / a.steps * 1e3
-    rows_step = 2 * total
+    rows_step = 2 * total if a.workload != "c5" else nr + ns
     value = rows_step / (dt / a.steps)
 
     # roofline of the dominant kernel: algorithmic bytes / its event time
@@ -171,7 +187,7 @@ def main():
     pipe_gbs = b_alg / (dt / a.steps) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
+    if rank == 0 and world == 1 and a.cpu_sample > 0 and a.workload == "c3":
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline leg only
         m = min(a.cpu_sample, n)
@@ -184,15 +200,19 @@ def main():
                          f"{secs:.2f} s, {jrows} joined rows"}
 
     cpu_mt = None
-    if rank == 0 and world == 1 and a.cpu_mt:
+    if rank == 0 and world == 1 and a.cpu_mt and a.workload == "c3":
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline leg only
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+        # the host cores this process may use: the CPU share granted to this GPU's job
+        # (OMP_NUM_THREADS on the GPU box), else every core the process is affine to
+        usable = len(os.sched_getaffinity(0))
+        threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or usable, usable)
         secs, rows = oracle.mt_pipeline(R.cpu().numpy(), S.cpu().numpy(), SELECT, KEYS, threads)
         assert rows[2] == joined, "CPU port disagrees with the GPU join count"
         cpu_mt = {"value": round(2 * n / secs, 1), "unit": "rows/s", "cores": threads, "kind": "port",
                   "sample": f"the full workload ({n} x {n} rows): oracle/cpu_mt.cpp, cpu_app.c's select + "
-                            f"stable sort + zip join on {threads} threads (chunk sort + merge rounds), g++ -O3; "
+                            f"stable sort + zip join on {threads} threads (the host cores granted to this GPU's "
+                            f"job; {usable} usable, {os.cpu_count()} in the node) (chunk sort + merge rounds), g++ -O3; "
                             f"{secs:.2f} s, {rows[2]} joined rows (equal to the GPU's)"}
 
     if rank == 0:
@@ -201,9 +221,13 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int64",
             "data": "synthetic: splitmix64 keys iid uniform in [1,3n], payload = global row index (generated on device)",
-            "config": {"workload": "C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, "
-                                   "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
-                       "rows_per_table_per_gpu": n, "rows_per_table_total": total, "key_range": key_range,
+            "config": {"workload": {"c3": "C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, "
+                                          "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
+                                    "c4": "C4's tables (|R|=|S|=1e9, uniform keys in [1,3e9]) on ONE GPU "
+                                          "(partitioned mode), WHERE col0 > 5000",
+                                    "c5": "C5's tables (|R|=1e8, |S|=1e9, Zipf 0.9 over 1e8 keys) on ONE GPU "
+                                          "(partitioned mode), WHERE col0 > 5000"}[a.workload],
+                       "rows_per_table_per_gpu": n if a.workload != "c5" else [nr, ns], "rows_per_table_total": total, "key_range": key_range,
                        "joined_rows": joined, "parallelism": f"range-partition x{world}",
                        "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
                        "exchange_stages": lb.get("stages", 0)},

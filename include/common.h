@@ -3,8 +3,10 @@
  *
  * A table is a row-major array T[row_num * col_num]; T is the element type
  * selected by one of INT64 (default) / UINT64 / DOUBLE exactly as in the
- * reference (common.h:1-9).  The MI355X library is built for INT64 (the
- * reference default); smj.h rejects the other element types at compile time.
+ * reference (common.h:1-9).  The library's cells are 8 bytes whatever T is:
+ * a C host compiled with -DUINT64 or -DDOUBLE reaches the same pipeline
+ * through smj.h's *_typed entry points (smj_sort_merge_join maps to them),
+ * which compare keys and select values as T.
  *
  * dpu_block_t is the 12-byte block descriptor the reference host pushes to
  * every DPU kernel (common.h:13-18, e.g. app.c:226, :447).  The C-ABI in

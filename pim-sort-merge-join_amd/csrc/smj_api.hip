@@ -610,7 +610,39 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
 // The pipeline.  h_rows[x] gets the selected row count of table x and, with
 // join, h_rows[2] the joined row count.  One stream synchronisation at the
 // end (plus one more round when oversized groups need the fallback).
-int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+// Staged host input (the host-pointer path): table x's
+// rows are copied from host[x] into in[x].src in chunks on the copy stream,
+// and part_a runs on each chunk's tiles as soon as it has landed, while the
+// next chunk is in flight.  The splitter sample is gathered on the host.
+struct MsdStage {
+    const int64_t *host[2];
+    hipStream_t copy;
+    int64_t chunk_rows;  // a multiple of every pass-A tile
+    hipEvent_t landed;   // recorded on the copy stream after the last chunk
+};
+
+// the samples msd_sample_gather_kernel would take, read from the host tables
+void host_sample(const MsdIn *in, const MsdStage &stg, int ntab, int64_t *samp) {
+    constexpr int kRun = 16, kClusters = kSampleMax / kRun;
+    for (int b = 0; b < kSampleGatherBlocksH; b++) samp[2 * kSampleMax + b] = 0;
+    for (int x = 0; x < 2; x++)
+        for (int64_t j = 0; j < kSampleMax; j++) {
+            int64_t k = INT64_MAX;
+            if (x < ntab && in[x].n > 0 && j < std::min<int64_t>(in[x].n, kSampleMax)) {
+                const int64_t n = in[x].n;
+                const int64_t r = n <= kSampleMax ? j : std::min(n - 1, ((2 * (j / kRun) + 1) * n) / (2 * kClusters) + j % kRun);
+                const int64_t *row = stg.host[x] + r * in[x].cols;
+                if (!in[x].use_sel || row[in[x].sel_col] > in[x].sel_val) {
+                    k = row[in[x].key];
+                    samp[2 * kSampleMax + (x * kSampleMax + j) / 256]++;
+                }
+            }
+            samp[x * kSampleMax + j] = k;
+        }
+}
+
+int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s,
+            const MsdStage *stg = nullptr) {
     for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
         SMJ_TRY(check_table(in[x].n, in[x].cols, in[x].use_sel ? in[x].sel_col : 0, in[x].key));
     if (join && (ntab != 2 || key2 != in[1].key)) return SMJ_ERR_INVALID;
@@ -653,13 +685,42 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         sp.spl = ms->spl;
         sp.samp = ms->samp;
         ProfScope ps("msd_sample", 0, s);
-        HIP_TRY(launch_msd_sample(sp, s));
+        if (stg) {
+            host_sample(in, *stg, ntab, ms->h_samp);
+            HIP_TRY(hipMemcpyAsync(ms->samp, ms->h_samp, sizeof(int64_t) * (2 * kSampleMax + kSampleGatherBlocksH),
+                                   hipMemcpyHostToDevice, s));
+            HIP_TRY(launch_msd_sample_select(sp, s));
+        } else {
+            HIP_TRY(launch_msd_sample(sp, s));
+        }
     }
     size_t pa[2] = {(size_t)-1, (size_t)-1};
+    std::vector<hipEvent_t> chunk_ev;  // staged input: one event per landed chunk
+    struct EvRelease {
+        std::vector<hipEvent_t> &v;
+        ~EvRelease() {
+            for (auto e : v) hipEventDestroy(e);
+        }
+    } ev_release{chunk_ev};
     for (int x = 0; x < ntab; x++) {
         MsdPartAParams p{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
                          (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
-        {
+        if (stg) {  // copy chunk c on the copy stream; part_a of chunk c once it has landed
+            const int64_t W = (int64_t)in[x].cols * 8, ch = stg->chunk_rows;
+            for (int64_t r0 = 0; r0 < in[x].n; r0 += ch) {
+                const int64_t r1 = std::min(in[x].n, r0 + ch);
+                HIP_TRY(hipMemcpyAsync((char *)in[x].src + r0 * W, (const char *)stg->host[x] + r0 * W, (r1 - r0) * W,
+                                       hipMemcpyHostToDevice, stg->copy));
+                hipEvent_t e;
+                HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                chunk_ev.push_back(e);
+                HIP_TRY(hipEventRecord(e, stg->copy));
+                if (x == ntab - 1 && r1 == in[x].n && stg->landed) HIP_TRY(hipEventRecord(stg->landed, stg->copy));
+                HIP_TRY(hipStreamWaitEvent(s, e, 0));
+                ProfScope ps("msd_part_a", 0, s);
+                HIP_TRY(launch_msd_part_a_tiles(p, in[x].cols, r0 / T_[x], (r1 + T_[x] - 1) / T_[x], s));
+            }
+        } else {
             ProfScope ps("msd_part_a", 0, s);
             HIP_TRY(launch_msd_part_a(p, in[x].cols, s));
         }
@@ -832,8 +893,6 @@ int64_t msd_large_parts(const MsdIn *in, int ntab) {
     for (int x = 0; x < ntab; x++) mx = std::max(mx, in[x].n);
     return std::min<int64_t>(64, (mx + kMsdPartRows - 1) / kMsdPartRows);
 }
-
-int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s);
 
 int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
     MsdScratch *ms;
@@ -1135,6 +1194,25 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
                         {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
     if (c1 > kDirectCols || c2 > kDirectCols) return msd_indexed(t, 2, 1, key2, SMJ_KEY_INT64, out, h_rows, s);
     return msd_any(t, 2, 1, key2, out, h_rows, s);
+}
+
+// The host-pointer path with staged input (smj_host.hip): R and S are
+// copied from the host in chunks overlapping part_a.  SMJ_ERR_UNSUPPORTED
+// where the plain path must be used instead (wide rows, partitioned sizes,
+// an empty table).
+int smj::msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int sc1, int64_t sv1, int key1,
+                                    const int64_t *hS, int64_t ns, int c2, int sc2, int64_t sv2, int key2, int64_t *dR,
+                                    int64_t *dS, int64_t *dRs, int64_t *dSs, int64_t *dJ, int64_t *h_rows,
+                                    hipStream_t s, hipStream_t copy, hipEvent_t landed) {
+    if (c1 > kDirectCols || c2 > kDirectCols || nr == 0 || ns == 0 || nr > kMsdSingleMax || ns > kMsdSingleMax ||
+        g_force_parts > 0)
+        return SMJ_ERR_UNSUPPORTED;
+    SMJ_TRY(check_table(nr, c1, sc1, key1));
+    SMJ_TRY(check_table(ns, c2, sc2, key2));
+    const MsdIn t[2] = {{dR, nr, c1, 1, sc1, key1, sv1, dRs}, {dS, ns, c2, 1, sc2, key2, sv2, dSs}};
+    const int64_t lcm = 4 * 5 * 3 * 7 * 8192;  // every pass-A tile (msd_tile: 512 x {16, 8, 5, 4, 3, 2} rows) divides it
+    const MsdStage stg{{hR, hS}, copy, lcm * std::max<int64_t>(1, (int64_t)(1 << 22) / lcm), landed};
+    return msd_run(t, 2, 1, key2, dJ, h_rows, s, &stg);
 }
 
 // Diagnostic only (not part of smj.h): run every pipeline call in the

@@ -68,6 +68,7 @@ enum { B_IN0, B_IN1, B_PART0, B_PART1, B_RECV0, B_RECV1, B_OUT0, B_OUT1, B_J, B_
 struct HostDev {
     int phys = -1;            // HIP device
     hipStream_t st = nullptr;
+    hipStream_t cp = nullptr;  // staged H2D copies (overlapping the first pass)
     void *b[B_N] = {};
     size_t c[B_N] = {};
 };
@@ -183,6 +184,7 @@ extern "C" int smj_init_devices(const int *device_ids, int n) {
         g_devs[d].phys = device_ids[d];
         HIP_TRY(hipSetDevice(device_ids[d]));
         HIP_TRY(hipStreamCreateWithFlags(&g_devs[d].st, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&g_devs[d].cp, hipStreamNonBlocking));
     }
     HIP_TRY(hipSetDevice(device_ids[0]));
     return n;
@@ -204,6 +206,7 @@ extern "C" void smj_finalize(void) {
         hipSetDevice(d.phys);
         for (int i = 0; i < B_N; i++) hipFree(d.b[i]);
         hipStreamDestroy(d.st);
+        hipStreamDestroy(d.cp);
     }
     g_devs.clear();
     api_free_all();
@@ -536,13 +539,27 @@ extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, con
     SMJ_TRY(hgrow(hd, B_OUT1, (size_t)ns * c2 * 8));
     SMJ_TRY(hgrow(hd, B_J, (size_t)std::max<int64_t>(1, std::min(nr, ns)) * tc * 8));
     HIP_TRY(hipEventRecord(ev[0], st));
-    if (nr) HIP_TRY(hipMemcpyAsync(hd.b[B_IN0], R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
-    if (ns) HIP_TRY(hipMemcpyAsync(hd.b[B_IN1], S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipEventRecord(ev[1], st));
     int64_t rows[3] = {0, 0, 0};
-    SMJ_TRY(smj_dev_sort_merge_join_typed(key_type, hd.b[B_IN0], nr, c1, 1, select_col1, sel_bits1, key1, hd.b[B_IN1],
-                                          ns, c2, 1, select_col2, sel_bits2, key2, hd.b[B_OUT0], hd.b[B_OUT1],
-                                          hd.b[B_J], rows, st));
+    // staged: the tables cross PCIe in chunks while part_a already runs on the
+    // landed ones (SMJ_STAGED=0: one copy per table, then the pipeline)
+    static const bool staged_on = !getenv("SMJ_STAGED") || atoi(getenv("SMJ_STAGED")) != 0;
+    int rc = SMJ_ERR_UNSUPPORTED;
+    if (staged_on && key_type == SMJ_KEY_INT64) {
+        HIP_TRY(hipStreamWaitEvent(hd.cp, ev[0], 0));
+        rc = msd_staged_sort_merge_join((const int64_t *)R, nr, c1, select_col1, (int64_t)sel_bits1, key1,
+                                        (const int64_t *)S, ns, c2, select_col2, (int64_t)sel_bits2, key2,
+                                        (int64_t *)hd.b[B_IN0], (int64_t *)hd.b[B_IN1], (int64_t *)hd.b[B_OUT0],
+                                        (int64_t *)hd.b[B_OUT1], (int64_t *)hd.b[B_J], rows, st, hd.cp, ev[1]);
+        if (rc != SMJ_OK && rc != SMJ_ERR_UNSUPPORTED) return rc;
+    }
+    if (rc == SMJ_ERR_UNSUPPORTED) {
+        if (nr) HIP_TRY(hipMemcpyAsync(hd.b[B_IN0], R, (size_t)nr * c1 * 8, hipMemcpyHostToDevice, st));
+        if (ns) HIP_TRY(hipMemcpyAsync(hd.b[B_IN1], S, (size_t)ns * c2 * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(ev[1], st));
+        SMJ_TRY(smj_dev_sort_merge_join_typed(key_type, hd.b[B_IN0], nr, c1, 1, select_col1, sel_bits1, key1,
+                                              hd.b[B_IN1], ns, c2, 1, select_col2, sel_bits2, key2, hd.b[B_OUT0],
+                                              hd.b[B_OUT1], hd.b[B_J], rows, st));
+    }
     const int64_t j = rows[2];
     HIP_TRY(hipEventRecord(ev[2], st));
     T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));

@@ -173,7 +173,6 @@ constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key or
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
-constexpr int kMsdStageGrid = 512;         // persistent staged final kernel: 2 workgroups per CU
 constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = 256;              // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
@@ -195,7 +194,7 @@ struct MsdSampleParams {
 struct MsdPartAParams {
     const int64_t *src;
     int64_t n;
-    int use_sel, sel_col, key_col, pad;
+    int use_sel, sel_col, key_col, tile0;  // tile0: first tile of this launch (staged H2D: one launch per chunk)
     int64_t sel_val;
     const int64_t *spl;
     int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
@@ -294,6 +293,12 @@ void api_free_all();
 // worker threads of the multi-device host API give each device of the set its
 // own scratch (several may map to one physical device); -1 = per device
 void set_scratch_slot(int slot);
+// the fused pipeline on host tables copied in chunks that overlap part_a
+// (smj_api.hip); SMJ_ERR_UNSUPPORTED where the plain path must run instead
+int msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int sc1, int64_t sv1, int key1,
+                               const int64_t *hS, int64_t ns, int c2, int sc2, int64_t sv2, int key2, int64_t *dR,
+                               int64_t *dS, int64_t *dRs, int64_t *dSs, int64_t *dJ, int64_t *h_rows, hipStream_t s,
+                               hipStream_t copy, hipEvent_t landed);
 
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 // the sample gather alone: samp[x * kSampleMax + j] = sampled key j of table x
@@ -302,6 +307,10 @@ hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s);
 constexpr int kSampleGatherBlocksH = 2 * kSampleMax / 256;
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
+// tiles [t0, t1) only (their rows must be resident: the staged host path)
+hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p, int cols, int64_t t0, int64_t t1, hipStream_t s);
+// the splitter selection alone, over samples already in p.samp (host-side gather)
+hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s);
 // per-bucket run sums and counts per segment; also the selected-key min / max
 // per (segment, wave): segmm[kMsdSegs * 4][2] (256 entries, INT64_MAX / MIN when empty)
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,

@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t t = blockIdx.x, row0 = t * T;
+    const int64_t t = (int64_t)p.tile0 + blockIdx.x, row0 = t * T;
     const int nrows = (int)min((int64_t)T, p.n - row0);
     uint32_t *wc = s_wcnt + wave * RADIX;
     if (tid < kSplA) s_spl[tid] = p.spl[tid];
@@ -1858,23 +1858,39 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
 
 // ---- 2-column staged path --------------------------------------------------------
 // The common case, (key, payload) tables: every row of a group is gathered
-// ONCE (16 B, lanes on consecutive rows of a pass-B tile range) into an LDS
-// stage; the 32-bit sort words (key - base) << 10 | row are counting-sorted
+// ONCE (16 B, lanes on consecutive rows of a pass-B tile range); its payload
+// column is staged in LDS; the 32-bit sort words (key - base) << 10 | row are counting-sorted
 // (base and key span come from the group record, no reduction); the zip
 // join reads its run starts straight from the histogram; sorted rows and
 // join rows leave through LDS as coalesced stores.  The next group's rows
 // are gathered into registers while this one is sorted and written.  Groups
 // outside its limits (key span > kStageRange, an equal-key run >
 // kMaxDupRun, > kStList pass-B tiles) go to the radix list.
-constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 2 per CU (1024-thread workgroups: slower, r01z)
-constexpr int kStList = 512;                   // pass-B tiles per bucket and table a staged group may span
+constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 3 per CU (1024-thread workgroups: slower, r01z)
+#ifndef SMJ_ST_GRID
+#define SMJ_ST_GRID 768
+#endif
+#ifndef SMJ_ST_LIST
+#define SMJ_ST_LIST 256
+#endif
+#ifndef SMJ_ST_RECS
+#define SMJ_ST_RECS 16
+#endif
+constexpr int kStList = SMJ_ST_LIST;           // pass-B tiles per bucket and table a staged group may span
 constexpr int kStIt = kGroupCap / kStThreads;  // rows per table per thread
 constexpr int kStRange = kStageRange;
-constexpr int kStRecs = 64;                    // group records per LDS chunk (two chunks in flight)
+constexpr int kStRecs = SMJ_ST_RECS;           // group records per LDS chunk (two chunks in flight)
 static_assert(kFinIdxBits == 10, "sort word = residual << 10 | group row");
 
+// LDS: 50.4 KiB and 80 VGPRs (launch bounds: 6 waves per SIMD), so three
+// workgroups share a CU (24 waves).  Only the payload column is staged: a
+// row's key is the group base plus the residual in its sort word.  Same-box
+// A/B against the full-row, two-per-CU kernel (profiles/r02_final_occupancy_ab.txt):
+// 1.84 vs 1.91 ms and 2.00 vs 2.02 ms on two boxes; the same kernel at two
+// per CU is slower (2.03 ms), and without opaque_tid (below) it spills 100 B
+// per lane at 80 VGPRs and runs at 2.74 ms.
 struct StSmem {
-    i64x2 stage[2][kGroupCap];        // rows in gather order
+    int64_t pay[2][kGroupCap];        // payload (non-key) column, gather order
     uint32_t key[2][kGroupCap];       // sort words, sorted
     uint32_t hist[2][kStRange / 2];   // packed u16 bins (zeroed for the next group during the emit)
     union {
@@ -1892,6 +1908,15 @@ struct StSmem {
     uint32_t flag[2];
 };
 
+// threadIdx.x as a value the compiler may not hoist out of the group loop:
+// per-lane addresses are recomputed where used instead of living (spilled)
+// across the whole loop
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g) {
     return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStList &&
            (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList);
@@ -1899,7 +1924,7 @@ __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g
 
 __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
                                              uint32_t (&o1)[2]) {
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = opaque_tid();
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         o0[x] = o1[x] = 0;
@@ -1929,7 +1954,7 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
 // non-empty range starting in (64b, v] (bitmap word + at[]).
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = opaque_tid();
     for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
@@ -1943,7 +1968,7 @@ __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                                const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[2][kStIt],
                                                StSmem &sm) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t tid = opaque_tid(), lane = tid & 63;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
 #pragma unroll
@@ -1988,7 +2013,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
                                         const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
                                         uint32_t &nex) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
     uint32_t w[2][kStIt], rank[2][kStIt];
@@ -2004,7 +2029,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             w[x][k] = ~0u;
             rank[x][k] = 0;
             if (v < n[x]) {
-                sm.stage[x][v] = rows[x][k];
+                sm.pay[x][v] = p.tab[x].key ? rows[x][k].x : rows[x][k].y;
                 const uint32_t res = (uint32_t)((uint64_t)st_key(rows[x][k], p.tab[x].key) - (uint64_t)g.base);
                 w[x][k] = (res << kFinIdxBits) | (uint32_t)v;
                 const uint32_t sh = 16u * (res & 1u);
@@ -2124,7 +2149,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
 __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, StSmem &sm,
                                         int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt]) {
     constexpr uint32_t IDX = (1u << kFinIdxBits) - 1u;
-    const int tid = threadIdx.x;
+    const int tid = opaque_tid();
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
@@ -2133,10 +2158,18 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         i64x2 *dst = reinterpret_cast<i64x2 *>(p.tab[x].out) + (x ? g.outS : g.outR);
+        const int kc = p.tab[x].key;
 #pragma unroll
         for (int k = 0; k < kStIt; k++) {
             const int q = tid + k * kStThreads;
-            if (q < n[x]) __builtin_nontemporal_store(sm.stage[x][sm.key[x][q] & IDX], dst + q);  // final rows: streamed
+            if (q < n[x]) {
+                const uint32_t w = sm.key[x][q];
+                const int64_t key = g.base + (int64_t)(w >> kFinIdxBits), pay = sm.pay[x][w & IDX];
+                i64x2 r;
+                r.x = kc ? pay : key;
+                r.y = kc ? key : pay;
+                __builtin_nontemporal_store(r, dst + q);  // final rows: streamed
+            }
         }
     }
     if (!p.join) return;
@@ -2152,7 +2185,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     __syncthreads();
     // output word wd = row * 3 + column: R key, R payload, S payload
     int64_t *dst = p.slots + (int64_t)g.outR * 3;
-    const int key2 = p.key2;
+    const int kc0 = p.tab[0].key;
     // fixed trip count (total <= kGroupCap), see st_load_recs
     constexpr int EMIT_IT = (3 * kGroupCap + kStThreads - 1) / kStThreads;
 #pragma unroll
@@ -2162,12 +2195,11 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
             const uint32_t row = wd / 3u, c = wd - row * 3u;
             const uint32_t m = sm.match[row];
             int64_t val;
-            if (c < 2) {
-                const i64x2 r = sm.stage[0][kR[m >> kFinIdxBits] & IDX];
-                val = c ? r.y : r.x;
-            } else {
-                const i64x2 r = sm.stage[1][kS[m & IDX] & IDX];
-                val = key2 ? r.x : r.y;
+            if (c < 2) {  // R's columns: the key from the sort word, the payload staged
+                const uint32_t w = kR[m >> kFinIdxBits];
+                val = c == kc0 ? g.base + (int64_t)(w >> kFinIdxBits) : sm.pay[0][w & IDX];
+            } else {      // S's column other than key2: its payload
+                val = sm.pay[1][kS[m & IDX] & IDX];
             }
             __builtin_nontemporal_store(val, dst + wd);  // join slots: read back by msd_compact only
         }
@@ -2184,7 +2216,7 @@ __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0
     constexpr int WORDS = sizeof(MsdGroup) / 8;
     static_assert(kStRecs * WORDS <= kStThreads, "at most one record word per thread");
     int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
-    const int i = threadIdx.x;
+    const int i = opaque_tid();
     const int64_t t = t0 + i / WORDS;
     if (i < kStRecs * WORDS && t < cnt) dst[i] = reinterpret_cast<const int64_t *>(p.groups + g0 + t * gs)[i % WORDS];
 }
@@ -2197,7 +2229,10 @@ __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0
 // neighbours in key order: the pass-B tile lines and offsB lines two
 // neighbouring groups share are fetched into that XCD's L2 once.
 constexpr int kXcdSlots = 8;
-__global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const MsdFinalParams p) {
+#ifndef SMJ_ST_MINW
+#define SMJ_ST_MINW 6
+#endif
+__global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
@@ -2208,7 +2243,7 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
     unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
-        for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
     }
     if (0 < cnt) st_load_recs(p, g0, gs, 0, cnt, sm, 0);
     if (kStRecs < cnt) st_load_recs(p, g0, gs, kStRecs, cnt, sm, 1);
@@ -2224,13 +2259,13 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
             if (li + kStRecs < cnt) st_load_recs(p, g0, gs, li + kStRecs, cnt, sm, (int)((c + 1) & 1));
             __syncthreads();
         }
-        const MsdGroup g = sm.recs[li % (2 * kStRecs)];
+        const MsdGroup &g = sm.recs[li % (2 * kStRecs)];  // fields read from LDS where used (register pressure)
         if (g.flags) {
             have = false;
             continue;
         }
         if (!st_ok(p, g)) {
-            if (threadIdx.x == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            if (opaque_tid() == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
             have = false;
             continue;
         }
@@ -2242,10 +2277,9 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
         }
         FIN_STAMP(0);
         bool nfit = false;
-        MsdGroup gn{};
+        const MsdGroup &gn = sm.recs[(li + 1) % (2 * kStRecs)];
         uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
         if (li + 1 < cnt) {
-            gn = sm.recs[(li + 1) % (2 * kStRecs)];
             nfit = st_ok(p, gn);
             if (nfit) st_load_offs(p, gn, o0, o1);
         }
@@ -2270,7 +2304,7 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
             st_emit(p, g, gi, sm, wsb, mmask, part);
         } else {  // hand-over: the histogram still needs zeroing
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
-            for (int i = threadIdx.x; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+            for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
         }
         FIN_STAMP(4);
         have = nfit;
@@ -2278,7 +2312,7 @@ __global__ __launch_bounds__(kStThreads, 4) void msd_final_stage_kernel(const Ms
         FIN_STAMP(5);
         if (SMJ_STAMPS && (p.dbg & 1)) ph[9]++;
     }
-    if (SMJ_STAMPS && (p.dbg & 1) && threadIdx.x == 0)
+    if (SMJ_STAMPS && (p.dbg & 1) && opaque_tid() == 0)
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
 
@@ -2525,8 +2559,20 @@ hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
 
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
-    const unsigned grid = blocks_for(p.n, msd_tile(cols));
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(grid), dim3(kMsdThreads), 0, s, p));
+    return launch_msd_part_a_tiles(p, cols, 0, blocks_for(p.n, msd_tile(cols)), s);
+}
+
+hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t t0, int64_t t1, hipStream_t s) {
+    if (p_in.n <= 0 || t1 <= t0) return hipSuccess;
+    MsdPartAParams p = p_in;
+    p.tile0 = (int)t0;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3((unsigned)(t1 - t0)), dim3(kMsdThreads), 0,
+                                             s, p));
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(msd_sample_select_kernel, dim3(kSampleN / kSelSamples), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2607,8 +2653,9 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     const size_t pad = (p.dbg & 64) ? 40960 : 0;  // ablation: dynamic LDS pad -> 1 workgroup per CU
     const bool two = p.tab[0].cols == 2 && (p.ntab == 1 || p.tab[1].cols == 2);
     if (two) {
-        static_assert(kMsdStageGrid % kXcdSlots == 0, "whole XCD sets");
-        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(pad ? kMsdStageGrid / 2 : kMsdStageGrid), dim3(kStThreads),
+        constexpr int kStGrid = SMJ_ST_GRID;
+        static_assert(kStGrid % kXcdSlots == 0, "whole XCD sets");
+        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads),
                            pad, s, p);
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
