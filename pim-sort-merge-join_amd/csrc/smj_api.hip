@@ -451,9 +451,9 @@ extern "C" int smj_dev_join(const T *R, int64_t nr, int c1, const T *S, int64_t 
 namespace {
 struct MsdTabScratch {
     void *tempA = nullptr, *tempB = nullptr, *offsA = nullptr, *tmm = nullptr, *list = nullptr,
-         *tinfo = nullptr, *offsB = nullptr, *seg = nullptr, *bk = nullptr, *fb = nullptr;
+         *tinfo = nullptr, *offsB = nullptr, *seg = nullptr, *bk = nullptr, *fb = nullptr, *fb2 = nullptr;
     size_t c_tempA = 0, c_tempB = 0, c_offsA = 0, c_tmm = 0, c_list = 0, c_tinfo = 0, c_offsB = 0, c_seg = 0,
-           c_bk = 0, c_fb = 0;
+           c_bk = 0, c_fb = 0, c_fb2 = 0;
 };
 struct MsdScratch {
     int dev = -1;
@@ -469,6 +469,11 @@ struct MsdScratch {
     size_t c_slots = 0;
     void *work = nullptr;
     size_t c_work = 0;
+    void *jb = nullptr;  // batched fallback: join rows of the oversized groups
+    size_t c_jb = 0;
+    void *cwork = nullptr;  // msd_compact_big work list ({dense group, chunk})
+    size_t c_cwork = 0;
+    int64_t n_cwork = 0;
     int64_t *d_tmp = nullptr;
     int64_t *lspl = nullptr;    // partitioned mode: the part splitters (device)
     int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
@@ -522,10 +527,10 @@ void msd_free_all() {
         if (m.dev < 0) continue;
         hipSetDevice(m.dev);
         for (auto &t : m.t)
-            for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb})
+            for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb, t.fb2})
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
-                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, (void *)m.d_tmp,
+                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                         (void *)m.lspl})
             hipFree(p);
         hipHostFree(m.h_plan);
@@ -555,7 +560,9 @@ void prof_set_bytes(size_t i, double bytes) {
 
 // Oversized groups after the main pass: single-key ones stream through
 // msd_single_kernel; multi-key ones (and groups whose key range does not fit
-// the LDS sort word) are gathered and sorted / joined by the LSD path.
+// the LDS sort word) are gathered into one buffer per table, sorted by one
+// LSD sort and joined by one zip join (a fixed number of launches however
+// many such groups there are: Zipf tables have thousands).
 int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdFinalParams &fp, int64_t *out_j,
                  hipStream_t s, bool *redo_compact) {
     const MsdPlan &pl = *ms->h_plan;
@@ -581,25 +588,80 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
         HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
     }
-    for (uint32_t slot : bigs) {
-        const MsdGroup &g = groups[slot];
-        const uint32_t nx[2] = {g.nR, ntab > 1 ? g.nS : 0u};
-        const uint32_t ox[2] = {g.outR, g.outS};
-        for (int x = 0; x < ntab; x++) {
-            if (nx[x] == 0) continue;
-            MsdTabScratch &ts = ms->t[x];
-            SMJ_TRY(grow(&ts.fb, &ts.c_fb, (size_t)nx[x] * in[x].cols * 8));
-            HIP_TRY(launch_msd_gather(fp.tab[x], ms->groups, slot, nx[x], (int64_t *)ts.fb, s));
-            int64_t m = 0;
-            SMJ_TRY(lsd_select_sort((const T *)ts.fb, nx[x], in[x].cols, 0, 0, 0, in[x].key, 0,
-                                    in[x].out + (int64_t)ox[x] * in[x].cols, &m, s));
+    if (pl.nbig) {
+        // all oversized multi-key groups at once: gather (in key order) ->
+        // one stable sort per table -> copy back to each group's output rows;
+        // with join, one zip join of the two sorted buffers split per group
+        constexpr uint32_t kSeg = 4096;  // rows per copy-back work item
+        std::sort(bigs.begin(), bigs.end());  // dense group index = key order (the list is filled by atomics)
+        std::vector<uint4> gw[2], cw[2], bw;
+        int64_t tot[2] = {0, 0};
+        for (uint32_t slot : bigs) {
+            const MsdGroup &g = groups[slot];
+            const uint32_t nx[2] = {g.nR, ntab > 1 ? g.nS : 0u};
+            const uint32_t ox[2] = {g.outR, g.outS};
+            bw.push_back(make_uint4(slot, (uint32_t)tot[0], nx[0], nx[1]));
+            for (int x = 0; x < ntab; x++) {
+                for (uint32_t v = 0; v < nx[x]; v += kGroupCap)
+                    gw[x].push_back(make_uint4(slot, v, (uint32_t)(tot[x] + v), 0));
+                for (uint32_t v = 0; v < nx[x]; v += kSeg)
+                    cw[x].push_back(make_uint4((uint32_t)(tot[x] + v), ox[x] + v, std::min(kSeg, nx[x] - v), 0));
+                tot[x] += nx[x];
+            }
         }
-        if (join && nx[0] && nx[1]) {
+        if (tot[0] >= (int64_t)UINT32_MAX || tot[1] >= (int64_t)UINT32_MAX) return SMJ_ERR_TOO_LARGE;
+        std::vector<uint4> all;
+        size_t at[5];
+        for (int i = 0; i < 5; i++) {
+            const std::vector<uint4> &v = i < 2 ? gw[i] : i < 4 ? cw[i - 2] : bw;
+            at[i] = all.size();
+            all.insert(all.end(), v.begin(), v.end());
+        }
+        SMJ_TRY(grow(&ms->work, &ms->c_work, all.size() * sizeof(uint4)));
+        const uint4 *dw = (const uint4 *)ms->work;
+        HIP_TRY(hipMemcpyAsync(ms->work, all.data(), all.size() * sizeof(uint4), hipMemcpyHostToDevice, s));
+        for (int x = 0; x < ntab; x++) {
+            if (tot[x] == 0) continue;
+            MsdTabScratch &ts = ms->t[x];
+            SMJ_TRY(grow(&ts.fb, &ts.c_fb, (size_t)tot[x] * in[x].cols * 8));
+            SMJ_TRY(grow(&ts.fb2, &ts.c_fb2, (size_t)tot[x] * in[x].cols * 8));
+            {
+                ProfScope ps("msd_big", 16.0 * in[x].cols * tot[x], s);
+                HIP_TRY(launch_msd_gather_list(fp.tab[x], ms->groups, dw + at[x], (int64_t)gw[x].size(),
+                                               (int64_t *)ts.fb, s));
+            }
+            int64_t m = 0;
+            SMJ_TRY(lsd_select_sort((const T *)ts.fb, tot[x], in[x].cols, 0, 0, 0, in[x].key, 0, (T *)ts.fb2, &m, s));
+            if (m != tot[x]) return SMJ_ERR_HIP;
+            ProfScope ps("msd_big", 16.0 * in[x].cols * tot[x], s);
+            HIP_TRY(launch_msd_seg_copy((const int64_t *)ts.fb2, in[x].out, dw + at[2 + x], (int64_t)cw[x].size(),
+                                        in[x].cols, s));
+        }
+        if (join) {
             const int tc = in[0].cols + in[1].cols - 1;
-            SMJ_TRY(smj_dev_join(in[0].out + (int64_t)g.outR * in[0].cols, nx[0], in[0].cols,
-                                 in[1].out + (int64_t)g.outS * in[1].cols, nx[1], in[1].cols, in[0].key, in[1].key,
-                                 (T *)ms->slots + (int64_t)g.outR * tc, ms->d_tmp, nullptr, s));
-            HIP_TRY(hipMemcpyAsync(ms->counts + slot, ms->d_tmp, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+            SMJ_TRY(grow(&ms->jb, &ms->c_jb, (size_t)std::max<int64_t>(1, std::min(tot[0], tot[1])) * tc * 8));
+            SMJ_TRY(smj_dev_join((const T *)ms->t[0].fb2, tot[0], in[0].cols, (const T *)ms->t[1].fb2, tot[1],
+                                 in[1].cols, in[0].key, in[1].key, (T *)ms->jb, ms->d_tmp, nullptr, s));
+            ProfScope ps("msd_big", 0, s);
+            HIP_TRY(launch_msd_big_split((const int64_t *)ms->jb, ms->d_tmp, tc, (const int64_t *)ms->t[0].fb2,
+                                         in[0].cols, in[0].key, dw + at[4], (int64_t)bw.size(), ms->groups,
+                                         (int64_t *)ms->slots, ms->counts, s));
+        }
+        HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
+    }
+    if (join) {  // the oversized groups' join rows are packed in chunks (msd_compact_big_kernel)
+        std::vector<uint2> cw;
+        for (const std::vector<uint32_t> *l : {&singles, &bigs})
+            for (uint32_t slot : *l) {
+                const uint32_t m = std::min(groups[slot].nR, groups[slot].nS);
+                if (m > (uint32_t)kGroupCap)
+                    for (uint32_t c = 0; c * kCompactChunk < m; c++) cw.push_back(make_uint2(slot, c));
+            }
+        ms->n_cwork = (int64_t)cw.size();
+        if (!cw.empty()) {
+            SMJ_TRY(grow(&ms->cwork, &ms->c_cwork, cw.size() * sizeof(uint2)));
+            HIP_TRY(hipMemcpyAsync(ms->cwork, cw.data(), cw.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));  // host-owned
         }
     }
     (void)out_j;
@@ -702,9 +764,18 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             for (auto e : v) hipEventDestroy(e);
         }
     } ev_release{chunk_ev};
-    for (int x = 0; x < ntab; x++) {
-        MsdPartAParams p{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
-                         (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
+    MsdPartAParams pp[2];
+    for (int x = 0; x < ntab; x++)
+        pp[x] = MsdPartAParams{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
+                               (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
+    // both tables in one launch when nothing is staged and the widths agree (no tail between them)
+    const bool pa_fused = !stg && ntab == 2 && in[0].cols == in[1].cols;
+    if (pa_fused) {
+        ProfScope ps("msd_part_a", 0, s);
+        HIP_TRY(launch_msd_part_a2(pp[0], pp[1], in[0].cols, s));
+    }
+    for (int x = 0; x < ntab && !pa_fused; x++) {
+        const MsdPartAParams &p = pp[x];
         if (stg) {  // copy chunk c on the copy stream; part_a of chunk c once it has landed
             const int64_t W = (int64_t)in[x].cols * 8, ch = stg->chunk_rows;
             for (int64_t r0 = 0; r0 < in[x].n; r0 += ch) {
@@ -726,6 +797,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         }
         pa[x] = prof_last();
     }
+    if (pa_fused) pa[0] = prof_last();
     {
         ProfScope ps("msd_runs", 0, s);
         for (int x = 0; x < ntab; x++)
@@ -813,19 +885,22 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         HIP_TRY(launch_msd_final(fp, s));
     }
     pf = prof_last();
-    auto compact = [&]() -> int {
+    auto compact = [&](int after_fallback) -> int {
         {
             ProfScope ps("msd_count_scan", 0, s);
             HIP_TRY(launch_msd_count_scan(ms->counts, ms->cpart, ms->offs, ms->plan, s));
         }
         ProfScope ps("msd_compact", 0, s);
         HIP_TRY(launch_msd_compact((const int64_t *)ms->slots, ms->groups, ms->counts, ms->offs, ms->plan, tc, out_j,
-                                   s));
+                                   after_fallback, s));
+        if (after_fallback)
+            HIP_TRY(launch_msd_compact_big((const int64_t *)ms->slots, ms->groups, ms->counts, ms->offs,
+                                           (const uint2 *)ms->cwork, ms->n_cwork, tc, out_j, s));
         return SMJ_OK;
     };
     size_t pc = (size_t)-1;
-    if (join) {
-        SMJ_TRY(compact());
+    if (join) {  // speculative: a no-op when the plan turns out to have oversized groups
+        SMJ_TRY(compact(0));
         pc = prof_last();
     }
     HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
@@ -842,18 +917,21 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     bool redo = false;
     SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
     if (redo) {
-        SMJ_TRY(compact());
+        SMJ_TRY(compact(1));
         pc = prof_last();
         HIP_TRY(hipMemcpyAsync(&ms->h_plan->joined, &ms->plan->joined, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     const MsdPlan &pl = *ms->h_plan;
+    double pa_bytes = 0.0;
     for (int x = 0; x < ntab; x++) {
         const double W = 8.0 * in[x].cols;
-        prof_set_bytes(pa[x], W * ((double)in[x].n + pl.m[x]));
+        pa_bytes += W * ((double)in[x].n + pl.m[x]);
+        if (!pa_fused) prof_set_bytes(pa[x], W * ((double)in[x].n + pl.m[x]));
         prof_set_bytes(pb[x], W * 2.0 * pl.m[x]);
         h_rows[x] = pl.m[x];
     }
+    if (pa_fused) prof_set_bytes(pa[0], pa_bytes);
     const double Jb = join ? 8.0 * tc * (double)pl.joined : 0.0;
     double fb = Jb;
     for (int x = 0; x < ntab; x++) fb += 2.0 * 8.0 * in[x].cols * pl.m[x];

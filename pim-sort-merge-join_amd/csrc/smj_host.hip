@@ -33,6 +33,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
@@ -146,6 +147,18 @@ int64_t key_map_host(int64_t v, int ktype) {
 }
 
 uint32_t map_mask(int key, int sel_col) { return (1u << key) | (1u << sel_col); }
+
+// The caller free()s the result (app.c:759).  A large result is 2 MiB aligned
+// and advised onto huge pages: its first touch -- the D2H copy -- then takes a
+// few hundred page faults per GB instead of ~260 000 (a pageable D2H into a
+// fresh 4 KiB-page buffer ran at 13-17 GB/s, tools/h2d_overlap.py).
+void *result_alloc(size_t bytes) {
+    if (bytes < ((size_t)64 << 20)) return malloc(std::max<size_t>(bytes, 1));
+    void *p = nullptr;
+    if (posix_memalign(&p, (size_t)2 << 20, bytes) != 0) return nullptr;
+    madvise(p, bytes, MADV_HUGEPAGE);
+    return p;
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -279,7 +292,7 @@ extern "C" int smj_join(const dpu_block_t *r, const T *R, const dpu_block_t *s_,
     int64_t j = 0;
     SMJ_TRY(smj_dev_join((T *)hd.b[B_IN0], nr, c1, (T *)hd.b[B_IN1], ns, c2, key1, key2, (T *)hd.b[B_J],
                          (int64_t *)hd.b[B_SPL], &j, st));
-    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
+    T *res = (T *)result_alloc((size_t)j * tc * sizeof(T));
     if (!res) return SMJ_ERR_NOMEM;
     if (j && hipMemcpyAsync(res, hd.b[B_J], (size_t)j * tc * 8, hipMemcpyDeviceToHost, st) != hipSuccess) {
         free(res);
@@ -442,7 +455,7 @@ int sharded_run(int ktype, const HTab *tab, int ntab, int key2, T **out, int64_t
     T *res = nullptr;
     if (ntab > 1) {
         for (int d = 0; d < D; d++) at[d + 1] = at[d] + J[d];
-        res = (T *)malloc(std::max<size_t>((size_t)at[D] * tc * sizeof(T), 1));
+        res = (T *)result_alloc((size_t)at[D] * tc * sizeof(T));
         if (!res) return SMJ_ERR_NOMEM;
     } else {
         for (int d = 0; d < D; d++) at[d + 1] = at[d] + M[d];
@@ -562,7 +575,7 @@ extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, con
     }
     const int64_t j = rows[2];
     HIP_TRY(hipEventRecord(ev[2], st));
-    T *res = (T *)malloc(std::max<size_t>((size_t)j * tc * sizeof(T), 1));
+    T *res = (T *)result_alloc((size_t)j * tc * sizeof(T));
     if (!res) return SMJ_ERR_NOMEM;
     if ((j && hipMemcpyAsync(res, hd.b[B_J], (size_t)j * tc * 8, hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipEventRecord(ev[3], st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {

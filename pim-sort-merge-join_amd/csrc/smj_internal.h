@@ -175,7 +175,10 @@ constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kMsdFinalGrid = 1024;        // persistent final kernel: 4 workgroups per CU
 constexpr int kMsdPartBGrid = 512;         // persistent part_b: 2 workgroups per CU
 constexpr int kSampleMax = 4096;           // sampled keys per table
-constexpr int kMsdSegs = 256;              // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
+#ifndef SMJ_MSD_SEGS
+#define SMJ_MSD_SEGS 256
+#endif
+constexpr int kMsdSegs = SMJ_MSD_SEGS;     // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
 constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
 
@@ -200,6 +203,10 @@ struct MsdPartAParams {
     int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
     uint32_t *offs;      // [tiles][kOffsA]
     int64_t *tmm;        // [tiles][2] min / max selected key
+};
+struct MsdPartA2 {       // one part_a launch over up to two tables
+    MsdPartAParams t[2];
+    unsigned tiles0;     // blocks [0, tiles0) take table 0's tiles, the rest table 1's
 };
 struct MsdBucket {       // per pass-A bucket and table
     int64_t lo;          // pass-B digit (common to R and S): with r = key - lo,
@@ -307,6 +314,8 @@ hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s);
 constexpr int kSampleGatherBlocksH = 2 * kSampleMax / 256;
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
+// both tables (the same column count) in one launch: no tail between them
+hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, int cols, hipStream_t s);
 // tiles [t0, t1) only (their rows must be resident: the staged host path)
 hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p, int cols, int64_t t0, int64_t t1, hipStream_t s);
 // the splitter selection alone, over samples already in p.samp (host-side gather)
@@ -324,10 +333,23 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tile
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
-hipError_t launch_msd_gather(const MsdTab &tb, const MsdGroup *groups, uint32_t slot, int64_t rows,
-                             int64_t *dst, hipStream_t s);
+// batched fallback (oversized multi-key groups): see smj_msd.hip
+hipError_t launch_msd_gather_list(const MsdTab &tb, const MsdGroup *groups, const uint4 *work, int64_t nwork,
+                                  int64_t *dst, hipStream_t s);
+hipError_t launch_msd_seg_copy(const int64_t *src, int64_t *dst, const uint4 *work, int64_t nwork, int cols,
+                               hipStream_t s);
+hipError_t launch_msd_big_split(const int64_t *J, const int64_t *nJ, int tc, const int64_t *Rs, int c1, int key1,
+                                const uint4 *work, int64_t nwork, const MsdGroup *groups, int64_t *slots,
+                                uint32_t *counts, hipStream_t s);
+// groups with at most kGroupCap join rows; after_fallback == 0: nothing when the plan has oversized groups
 hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
-                              const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, hipStream_t s);
+                              const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, int after_fallback,
+                              hipStream_t s);
+// groups over kGroupCap join rows: work = {dense group, chunk of kCompactChunk rows}
+constexpr uint32_t kCompactChunk = 4096;
+hipError_t launch_msd_compact_big(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
+                                  const uint32_t *offs, const uint2 *work, int64_t nwork, int tc, int64_t *out,
+                                  hipStream_t s);
 hipError_t read_msd_phases(unsigned long long *out16);  // diagnostic (SMJ_DEBUG_MSD=1)
 // exclusive scan of the plan->ngroups dense group counts -> offs, total -> plan->joined
 hipError_t launch_msd_count_scan(const uint32_t *counts, uint32_t *part, uint32_t *offs, MsdPlan *plan,

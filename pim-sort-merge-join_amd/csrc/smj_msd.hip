@@ -282,7 +282,12 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 // part_a: select + stable tile-local partition by pass-A bucket
 // ---------------------------------------------------------------------------
 template <int COLS>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPartAParams p) {
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPartA2 q) {
+    // one launch may cover both tables (the same column count): blocks past
+    // q.tiles0 take table 1's tiles
+    const bool second = blockIdx.x >= q.tiles0;
+    const MsdPartAParams &p = second ? q.t[1] : q.t[0];
+    const unsigned bx = blockIdx.x - (second ? q.tiles0 : 0u);
     constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kOffsA;
     constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
     constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t t = (int64_t)p.tile0 + blockIdx.x, row0 = t * T;
+    const int64_t t = (int64_t)p.tile0 + bx, row0 = t * T;
     const int nrows = (int)min((int64_t)T, p.n - row0);
     uint32_t *wc = s_wcnt + wave * RADIX;
     if (tid < kSplA) s_spl[tid] = p.spl[tid];
@@ -2394,42 +2399,99 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
                               p.key2);
 }
 
-// gather a group's rows of table x into a contiguous buffer (LSD fallback)
-__global__ __launch_bounds__(kMsdThreads) void msd_gather_kernel(const MsdTab tb, const MsdGroup *groups,
-                                                                 uint32_t slot, int64_t *dst) {
+// Batched fallback for oversized multi-key groups (smj_api.hip msd_fallback):
+// the groups are disjoint key ranges in key order, so gathering all of them
+// (in group order) into one buffer, one stable sort of that buffer and one
+// zip join of the two sorted buffers give every group's sort and join at once.
+// work item = {dense group, first group row V0 of the chunk, buffer row of V0, -}
+__global__ __launch_bounds__(kMsdThreads) void msd_gather_list_kernel(const MsdTab tb, const MsdGroup *groups,
+                                                                      const uint4 *work, int64_t *dst) {
     __shared__ uint64_t s_tmp[kGroupCap];
     __shared__ uint32_t s_wsum[kMsdWaves];
-    const MsdGroup g = groups[slot];
+    const uint4 w = work[blockIdx.x];
+    const MsdGroup g = groups[w.x];
     const uint32_t nx = tb.x ? g.nS : g.nR;
-    const uint32_t V0 = blockIdx.x * (uint32_t)kGroupCap;
-    if (V0 >= nx) return;
-    const uint32_t V1 = min(V0 + (uint32_t)kGroupCap, nx);
+    const uint32_t V0 = w.y, V1 = min(V0 + (uint32_t)kGroupCap, nx);
+    const int64_t d0 = w.z;
     group_gather(tb, g, V0, V1, reinterpret_cast<uint2 *>(s_tmp), s_wsum, [&](uint32_t v, uint32_t src) {
-        copy_row<0>(tb.tempB + (int64_t)src * tb.cols, dst + (int64_t)v * tb.cols, tb.cols);
+        copy_row<0>(tb.tempB + (int64_t)src * tb.cols, dst + (d0 + (v - V0)) * tb.cols, tb.cols);
     });
+}
+
+// work item = {source row, destination row, rows, -}: contiguous row runs
+__global__ __launch_bounds__(256) void msd_seg_copy_kernel(const int64_t *__restrict__ src, int64_t *__restrict__ dst,
+                                                           const uint4 *work, int cols) {
+    const uint4 w = work[blockIdx.x];
+    const int64_t *a = src + (int64_t)w.x * cols;
+    int64_t *b = dst + (int64_t)w.y * cols;
+    const int64_t words = (int64_t)w.z * cols;
+    for (int64_t i = threadIdx.x; i < words; i += 256) b[i] = a[i];
+}
+
+// first index in [0, n) whose key is >= k (upper: > k)
+__device__ __forceinline__ int64_t key_bound(const int64_t *J, int64_t n, int tc, int kc, int64_t k, bool upper) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int64_t v = J[mid * tc + kc];
+        if (upper ? v <= k : v < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one workgroup per oversized group: its join rows are the rows of the
+// batched join J whose key lies in [first, last] of the group's sorted R rows;
+// copied to the group's slot rows, their number to counts.
+// work item = {dense group, first row of the group in the sorted R buffer, nR, nS}
+__global__ __launch_bounds__(256) void msd_big_split_kernel(const int64_t *__restrict__ J, const int64_t *nJp, int tc,
+                                                            const int64_t *__restrict__ Rs, int c1, int key1,
+                                                            const uint4 *work, const MsdGroup *groups,
+                                                            int64_t *__restrict__ slots, uint32_t *counts) {
+    const uint4 w = work[blockIdx.x];
+    if (w.z == 0 || w.w == 0) {
+        if (threadIdx.x == 0) counts[w.x] = 0;
+        return;
+    }
+    const int64_t nJ = *nJp;
+    const int64_t kmin = Rs[(int64_t)w.y * c1 + key1], kmax = Rs[((int64_t)w.y + w.z - 1) * c1 + key1];
+    const int64_t lo = key_bound(J, nJ, tc, key1, kmin, false), hi = key_bound(J, nJ, tc, key1, kmax, true);
+    if (threadIdx.x == 0) counts[w.x] = (uint32_t)(hi - lo);
+    const int64_t *a = J + lo * tc;
+    int64_t *b = slots + (int64_t)groups[w.x].outR * tc;
+    const int64_t words = (hi - lo) * tc;
+    for (int64_t i = threadIdx.x; i < words; i += 256) b[i] = a[i];
 }
 
 // pack the join slots: dense group g has counts[g] rows at slot row outR.
 // One wave per group (persistent over the groups), 8 words per lane in
 // flight per round; the next group's count / slot / offset are loaded while
-// this one is copied.
+// this one is copied.  Groups over kGroupCap join rows (only oversized ones
+// have them) are left to msd_compact_big_kernel; the speculative launch
+// before the fallback (after_fallback == 0) does nothing when the plan has
+// oversized groups, as the launch after it packs everything.
 __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restrict__ slots,
                                                           const MsdGroup *__restrict__ groups,
                                                           const uint32_t *__restrict__ counts,
                                                           const uint32_t *__restrict__ offs,
                                                           const MsdPlan *__restrict__ plan, int tc,
-                                                          int64_t *__restrict__ out) {
+                                                          int64_t *__restrict__ out, int after_fallback) {
     constexpr int U = 8;
     const int lane = threadIdx.x & 63;
+    if (!after_fallback && plan->nsingle + plan->nbig > 0) return;
     const int64_t ng = plan->ngroups, step = (int64_t)gridDim.x * 4;
     int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= ng) return;
-    uint32_t c = counts[g], o = offs[g], r = groups[g].outR;
+    auto cnt = [&](int64_t i) {
+        const uint32_t c = counts[i];
+        return c > (uint32_t)kGroupCap ? 0u : c;
+    };
+    uint32_t c = cnt(g), o = offs[g], r = groups[g].outR;
     for (; g < ng; g += step) {
         const int64_t gn = g + step;
         uint32_t cn = 0, on = 0, rn = 0;
         if (gn < ng) {
-            cn = counts[gn];
+            cn = cnt(gn);
             on = offs[gn];
             rn = groups[gn].outR;
         }
@@ -2453,6 +2515,24 @@ __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restr
         o = on;
         r = rn;
     }
+}
+
+// the groups with more than kGroupCap join rows, in chunks: work item =
+// {dense group, chunk}; chunks past the group's count (the host sizes the
+// list by min(nR, nS)) and groups at or under kGroupCap do nothing
+__global__ __launch_bounds__(256) void msd_compact_big_kernel(const int64_t *__restrict__ slots,
+                                                              const MsdGroup *__restrict__ groups,
+                                                              const uint32_t *__restrict__ counts,
+                                                              const uint32_t *__restrict__ offs, const uint2 *work,
+                                                              int tc, int64_t *__restrict__ out) {
+    const uint2 w = work[blockIdx.x];
+    const uint32_t c = counts[w.x], v0 = w.y * kCompactChunk;
+    if (c <= (uint32_t)kGroupCap || v0 >= c) return;
+    const uint32_t v1 = min(c, v0 + kCompactChunk);
+    const int64_t *src = slots + ((int64_t)groups[w.x].outR + v0) * tc;
+    int64_t *dst = out + ((int64_t)offs[w.x] + v0) * tc;
+    const int64_t nw = (int64_t)(v1 - v0) * tc;
+    for (int64_t i = threadIdx.x; i < nw; i += 256) dst[i] = src[i];
 }
 
 // exclusive scan of the dense group counts in two launches over chunks of
@@ -2564,10 +2644,25 @@ hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
 
 hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t t0, int64_t t1, hipStream_t s) {
     if (p_in.n <= 0 || t1 <= t0) return hipSuccess;
-    MsdPartAParams p = p_in;
-    p.tile0 = (int)t0;
+    MsdPartA2 q{};
+    q.t[0] = p_in;
+    q.t[0].tile0 = (int)t0;
+    q.tiles0 = (unsigned)(t1 - t0);
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3((unsigned)(t1 - t0)), dim3(kMsdThreads), 0,
-                                             s, p));
+                                             s, q));
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, int cols, hipStream_t s) {
+    MsdPartA2 q{};
+    q.t[0] = a;
+    q.t[1] = b;
+    q.t[0].tile0 = q.t[1].tile0 = 0;
+    q.tiles0 = a.n > 0 ? blocks_for(a.n, msd_tile(cols)) : 0u;
+    const unsigned tiles1 = b.n > 0 ? blocks_for(b.n, msd_tile(cols)) : 0u;
+    if (q.tiles0 + tiles1 == 0) return hipSuccess;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(q.tiles0 + tiles1), dim3(kMsdThreads), 0, s,
+                                             q));
     return hipGetLastError();
 }
 
@@ -2679,17 +2774,43 @@ hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_msd_gather(const MsdTab &tb, const MsdGroup *groups, uint32_t slot, int64_t rows, int64_t *dst,
-                             hipStream_t s) {
-    if (rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(msd_gather_kernel, dim3(blocks_for(rows, kGroupCap)), dim3(kMsdThreads), 0, s, tb, groups,
-                       slot, dst);
+hipError_t launch_msd_gather_list(const MsdTab &tb, const MsdGroup *groups, const uint4 *work, int64_t nwork,
+                                  int64_t *dst, hipStream_t s) {
+    if (nwork <= 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_gather_list_kernel, dim3((unsigned)nwork), dim3(kMsdThreads), 0, s, tb, groups, work, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_seg_copy(const int64_t *src, int64_t *dst, const uint4 *work, int64_t nwork, int cols,
+                               hipStream_t s) {
+    if (nwork <= 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_seg_copy_kernel, dim3((unsigned)nwork), dim3(256), 0, s, src, dst, work, cols);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_big_split(const int64_t *J, const int64_t *nJ, int tc, const int64_t *Rs, int c1, int key1,
+                                const uint4 *work, int64_t nwork, const MsdGroup *groups, int64_t *slots,
+                                uint32_t *counts, hipStream_t s) {
+    if (nwork <= 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_big_split_kernel, dim3((unsigned)nwork), dim3(256), 0, s, J, nJ, tc, Rs, c1, key1, work,
+                       groups, slots, counts);
     return hipGetLastError();
 }
 
 hipError_t launch_msd_compact(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
-                              const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(msd_compact_kernel, dim3(2048), dim3(256), 0, s, slots, groups, counts, offs, plan, tc, out);
+                              const uint32_t *offs, const MsdPlan *plan, int tc, int64_t *out, int after_fallback,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(msd_compact_kernel, dim3(2048), dim3(256), 0, s, slots, groups, counts, offs, plan, tc, out,
+                       after_fallback);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_compact_big(const int64_t *slots, const MsdGroup *groups, const uint32_t *counts,
+                                  const uint32_t *offs, const uint2 *work, int64_t nwork, int tc, int64_t *out,
+                                  hipStream_t s) {
+    if (nwork <= 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_compact_big_kernel, dim3((unsigned)nwork), dim3(256), 0, s, slots, groups, counts, offs,
+                       work, tc, out);
     return hipGetLastError();
 }
 

@@ -133,6 +133,37 @@ def test_multi_key_oversized_group_falls_back(gpu, oracle_built):
     np.testing.assert_array_equal(host(gJ), J)
 
 
+@pytest.mark.parametrize("c1,c2,sel", [(2, 2, None), (3, 4, (2, -(1 << 62) + (1 << 58)))])
+def test_many_oversized_groups_batched(gpu, oracle_built, c1, c2, sel):
+    """Hundreds of oversized multi-key groups (the shape Zipf tables produce
+    at C5's size: two neighbouring keys with ~600 rows each share one
+    sub-bucket of a wide bucket), some present in one table only: all of them
+    go through the one batched gather / sort / join of the fallback."""
+    from smj import ops
+    rng = np.random.default_rng(c1 + c2)
+    heavy = rng.choice(1 << 40, 600, replace=False) * 4
+
+    def make(n, cols, pay0, drop):
+        keys = [rng.integers(0, 1 << 42, n)]
+        for i, v in enumerate(heavy):
+            if i % 7 == drop:  # this pair only in the other table
+                continue
+            keys += [np.full(700 + i % 90, v), np.full(650 + i % 130, v + 1 + i % 3)]
+        k = rng.permutation(np.concatenate(keys))
+        t = rng.integers(-(1 << 62), 1 << 62, size=(len(k), cols))
+        t[:, 0] = k
+        t[:, 1] = pay0 + np.arange(len(k))
+        return np.ascontiguousarray(t, dtype=np.int64)
+
+    R, S = make(1_500_000, c1, 0, 3), make(1_200_000, c2, 10 ** 9, 5)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, sel, None)
+    assert ops.msd_stats()[1] > 100
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, sel, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, c1))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, c2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
+
+
 @pytest.mark.parametrize("n,cols,kind", [(100_000, 2, "uniform"), (70_000, 3, "dups"), (4097, 2, "wide")])
 def test_lsd_select_sort_matches_oracle(gpu, oracle_built, n, cols, kind):
     from smj import ops
