@@ -502,7 +502,7 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
-        HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * 256));
+        HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * kOffsA));
         HIP_TRY(hipMalloc(&m.cpart, sizeof(uint32_t) * 256));
         HIP_TRY(hipMalloc(&m.counts, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
@@ -728,7 +728,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
         SMJ_TRY(grow(&ts.offsB, &ts.c_offsB, (size_t)maxB[x] * kOffsB * sizeof(uint16_t)));
         SMJ_TRY(grow(&ts.seg, &ts.c_seg, 2 * kMsdSegs * kOffsA * 4 + kMsdSegs * 4 * 16 + 2 * kOffsA * 4));
-        SMJ_TRY(grow(&ts.bk, &ts.c_bk, 256 * sizeof(MsdBucket)));
+        SMJ_TRY(grow(&ts.bk, &ts.c_bk, kOffsA * sizeof(MsdBucket)));
     }
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
     if (join) SMJ_TRY(grow(&ms->slots, &ms->c_slots, std::max<size_t>(1, in[0].n) * tc * 8));
@@ -949,7 +949,7 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
 
 // ---------------------------------------------------------------------------
 // Partitioned mode (tables over kMsdSingleMax rows; BASELINE C4 / C5 on one
-// GPU).  One MSD pipeline call has 255 x 2048 sub-buckets of <= 1024 rows per
+// GPU).  One MSD pipeline call has 511 x 2048 sub-buckets of <= 1024 rows per
 // table, i.e. room for ~4e8 rows of well-spread keys; larger tables are first
 // range-partitioned on the key into P parts of <= kMsdPartRows rows per table
 // (smj_dev_partition: the WHERE clause + a stable bucket scatter, one read and

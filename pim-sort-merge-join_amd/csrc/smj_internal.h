@@ -161,9 +161,19 @@ __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_
 // (64 VGPRs, 2 x 16 waves per CU: part_b is latency-bound)
 __host__ __device__ constexpr int msd_tile_b(int cols) { return msd_tile(cols); }
 __host__ __device__ constexpr int pb_threads(int cols) { return cols == 2 ? 1024 : kMsdThreads; }
-constexpr int kSplA = 127;                 // pass-A splitters
-constexpr int kBucketsA = 2 * kSplA + 1;   // 255 pass-A buckets (odd = one key value)
-constexpr int kOffsA = 256;                // offsA row: 255 bucket starts + the tile's row count
+// pass-A splitters: 2^SMJ_SPLA_BITS - 1.  255 splitters give 256 open key
+// intervals (+ 255 single-key buckets): at C3 a bucket holds ~3.9e5 rows per
+// table, i.e. ~96 pass-B tiles whose runs a final group gathers (127
+// splitters: ~191 tiles of half the run length, and buckets over the final
+// stage's 256-tile list from ~1.3e8 rows per table on)
+#ifndef SMJ_SPLA_BITS
+#define SMJ_SPLA_BITS 8
+#endif
+constexpr int kSplABits = SMJ_SPLA_BITS;
+constexpr int kSplA = (1 << kSplABits) - 1;  // pass-A splitters
+constexpr int kBucketsA = 2 * kSplA + 1;     // 511 pass-A buckets (odd = one key value)
+constexpr int kOffsA = 2 << kSplABits;       // offsA row: 511 bucket starts + the tile's row count
+constexpr int kBitsA = kSplABits + 1;        // pass-A digit bits
 constexpr int kBitsB = 11;
 constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
 constexpr int kOffsB = kRadB + 8;          // offsB row (u16): 2048 starts + the tile's row count, padded to 16 B

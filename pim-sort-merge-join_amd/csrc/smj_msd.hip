@@ -181,8 +181,8 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
 __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
     int pos = 0;
 #pragma unroll
-    for (int step = 64; step >= 1; step >>= 1)
-        pos += (s_spl[pos + step - 1] < k) ? step : 0;  // index <= 126: 127 = 2^7 - 1 splitters
+    for (int step = 1 << (kSplABits - 1); step >= 1; step >>= 1)
+        pos += (s_spl[pos + step - 1] < k) ? step : 0;  // index <= kSplA - 1: kSplA = 2^kSplABits - 1 splitters
     const bool eq = pos < kSplA && s_spl[pos < kSplA ? pos : kSplA - 1] == k;
     return 2u * (uint32_t)pos + (eq ? 1u : 0u);
 }
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
         mn = v ? min(mn, k) : mn;
         mx = v ? max(mx, k) : mx;
     }
-    wave_rank<ITEMS, 8>(dig, vmask, wc, lane);
+    wave_rank<ITEMS, kBitsA>(dig, vmask, wc, lane);
     __syncthreads();
     const uint32_t total = tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
 #pragma unroll
@@ -338,7 +338,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    if (tid < RADIX) p.offs[t * kOffsA + tid] = s_bin[tid];  // s_bin[255] = total (bucket 255 is never used)
+    static_assert(RADIX <= kMsdThreads, "one offsA entry per thread");
+    if (tid < RADIX) p.offs[t * kOffsA + tid] = s_bin[tid];  // s_bin[kBucketsA] = total (that bucket is never used)
     if (tid == 0) {
         p.tmm[2 * t] = mn;
         p.tmm[2 * t + 1] = mx;
@@ -454,16 +455,17 @@ __global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanPara
     if (w == 0) p.tot[blockIdx.y][a] = tot;
 }
 
-// one workgroup of 256: thread = bucket.  Bucket sizes / bases of both
-// tables, the global key range, and the pass-B digit of every bucket.
-__global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) {
-    __shared__ uint32_t s_wsum[4];
-    __shared__ int64_t s_mm[8];
+// one workgroup of kOffsA threads: thread = bucket.  Bucket sizes / bases of
+// both tables, the global key range, and the pass-B digit of every bucket.
+constexpr int kBasesWaves = kOffsA / 64;
+__global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams p) {
+    __shared__ uint32_t s_wsum[kBasesWaves];
+    __shared__ int64_t s_mm[2 * kBasesWaves];
     const int a = threadIdx.x, lane = a & 63, wave = a >> 6;
     // global min / max of the selected keys over both tables
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (int x = 0; x < p.ntab; x++)  // per (segment, wave) partials of msd_runs_seg_kernel
-        for (int i = a; i < kMsdSegs * 4; i += 256) {
+        for (int i = a; i < kMsdSegs * 4; i += kOffsA) {
             mn = min(mn, p.segmm[x][2 * i]);
             mx = max(mx, p.segmm[x][2 * i + 1]);
         }
@@ -474,12 +476,12 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
     }
     if (lane == 0) {
         s_mm[wave] = mn;
-        s_mm[4 + wave] = mx;
+        s_mm[kBasesWaves + wave] = mx;
     }
     __syncthreads();
-    for (int w = 0; w < 4; w++) {
+    for (int w = 0; w < kBasesWaves; w++) {
         mn = min(mn, s_mm[w]);
-        mx = max(mx, s_mm[4 + w]);
+        mx = max(mx, s_mm[kBasesWaves + w]);
     }
     // rows of bucket a per table
     uint32_t Lt[2] = {0u, 0u};
@@ -530,9 +532,9 @@ __global__ __launch_bounds__(256) void msd_bases_kernel(const MsdBasesParams p) 
         const uint32_t L = a < kBucketsA ? p.totL[x][a] : 0u, C = a < kBucketsA ? p.totC[x][a] : 0u;
         const uint32_t K = (L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x];
         uint32_t totL, totC, totK;
-        const uint32_t rs = block_excl_scan<4>(L, s_wsum, &totL);
-        const uint32_t lb = block_excl_scan<4>(C, s_wsum, &totC);
-        const uint32_t tb = block_excl_scan<4>(K, s_wsum, &totK);
+        const uint32_t rs = block_excl_scan<kBasesWaves>(L, s_wsum, &totL);
+        const uint32_t lb = block_excl_scan<kBasesWaves>(C, s_wsum, &totC);
+        const uint32_t tb = block_excl_scan<kBasesWaves>(K, s_wsum, &totK);
         if (a < kBucketsA) {
             MsdBucket b;
             b.lo = lo;
@@ -2542,7 +2544,7 @@ __global__ __launch_bounds__(256) void msd_compact_big_kernel(const int64_t *__r
 // plan->joined = total.  grid kCountChunks x 256 (chunks past ngroups exit).
 constexpr int kCountPer = 16, kCountChunk = 256 * kCountPer;
 constexpr int kCountChunks = (kSlots + kCountChunk - 1) / kCountChunk;
-static_assert(kCountChunks <= 128, "one wave (2 sums per lane) adds the earlier chunks");
+static_assert(kCountChunks <= 256, "one wave (<= 4 sums per lane) adds the earlier chunks");
 __device__ __forceinline__ void count_load(const uint32_t *counts, int64_t ng, int64_t i0, uint32_t (&v)[kCountPer]) {
     if (i0 + kCountPer <= ng) {
         const uint4 *c4 = reinterpret_cast<const uint4 *>(counts + i0);
@@ -2593,7 +2595,9 @@ __global__ __launch_bounds__(256) void msd_count_scan_kernel(const uint32_t *__r
     count_load(counts, ng, i0, v);
     if (wave == 0) {
         const int b = (int)blockIdx.x;
-        uint32_t e = (lane < b ? part[lane] : 0u) + (lane + 64 < b ? part[lane + 64] : 0u);
+        uint32_t e = 0;
+#pragma unroll
+        for (int q = 0; q < (kCountChunks + 63) / 64; q++) e += lane + 64 * q < b ? part[lane + 64 * q] : 0u;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
         if (lane == 0) s_base = e;
@@ -2690,7 +2694,7 @@ hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int n
 }
 
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(msd_bases_kernel, dim3(1), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(msd_bases_kernel, dim3(1), dim3(kOffsA), 0, s, p);
     return hipGetLastError();
 }
 
