@@ -722,7 +722,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         const size_t W = (size_t)t.cols * 8;
         SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, std::max<size_t>(1, t.n) * W));
         SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * TB_[x] * W));
-        SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsA * 4));
+        SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsARow * 4));
         SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
         SMJ_TRY(grow(&ts.list, &ts.c_list, std::max<int64_t>(1, std::min<int64_t>(tilesA[x] * kBucketsA, t.n)) * 8));
         SMJ_TRY(grow(&ts.tinfo, &ts.c_tinfo, (size_t)maxB[x] * 8));
@@ -949,7 +949,7 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
 
 // ---------------------------------------------------------------------------
 // Partitioned mode (tables over kMsdSingleMax rows; BASELINE C4 / C5 on one
-// GPU).  One MSD pipeline call has 511 x 2048 sub-buckets of <= 1024 rows per
+// GPU).  One MSD pipeline call has 256 x 2048 sub-buckets of <= 1024 rows per
 // table, i.e. room for ~4e8 rows of well-spread keys; larger tables are first
 // range-partitioned on the key into P parts of <= kMsdPartRows rows per table
 // (smj_dev_partition: the WHERE clause + a stable bucket scatter, one read and

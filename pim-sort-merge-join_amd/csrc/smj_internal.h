@@ -161,19 +161,19 @@ __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_
 // (64 VGPRs, 2 x 16 waves per CU: part_b is latency-bound)
 __host__ __device__ constexpr int msd_tile_b(int cols) { return msd_tile(cols); }
 __host__ __device__ constexpr int pb_threads(int cols) { return cols == 2 ? 1024 : kMsdThreads; }
-// pass-A splitters: 2^SMJ_SPLA_BITS - 1.  255 splitters give 256 open key
-// intervals (+ 255 single-key buckets): at C3 a bucket holds ~3.9e5 rows per
-// table, i.e. ~96 pass-B tiles whose runs a final group gathers (127
-// splitters: ~191 tiles of half the run length, and buckets over the final
-// stage's 256-tile list from ~1.3e8 rows per table on)
-#ifndef SMJ_SPLA_BITS
-#define SMJ_SPLA_BITS 8
-#endif
-constexpr int kSplABits = SMJ_SPLA_BITS;
-constexpr int kSplA = (1 << kSplABits) - 1;  // pass-A splitters
-constexpr int kBucketsA = 2 * kSplA + 1;     // 511 pass-A buckets (odd = one key value)
-constexpr int kOffsA = 2 << kSplABits;       // offsA row: 511 bucket starts + the tile's row count
-constexpr int kBitsA = kSplABits + 1;        // pass-A digit bits
+// Pass A: 255 sampled splitters, 256 buckets (an 8-bit digit).  Bucket a
+// holds the keys in (spl[a-1], spl[a]]; a key value the sample saw more than
+// once (spl[i] == spl[i+1]: a heavy key) gets bucket i + 1 to itself, and the
+// buckets between its repeated splitters stay empty (bucket_a, msd_bases).
+// At C3 a bucket holds ~3.9e5 rows per table, i.e. ~96 pass-B tiles whose
+// runs a final group gathers (127 splitters and an odd single-key bucket per
+// splitter -- the round-1 layout -- gave ~191 tiles of half the run length,
+// and buckets over the final stage's 256-tile list from ~1.3e8 rows on).
+constexpr int kBitsA = 8;                    // pass-A digit bits
+constexpr int kBucketsA = 1 << kBitsA;       // 256 pass-A buckets
+constexpr int kSplA = kBucketsA - 1;         // 255 pass-A splitters
+constexpr int kOffsA = kBucketsA;            // per-bucket arrays (segment partials, bucket records)
+constexpr int kOffsARow = kBucketsA + 8;     // offsA row (u32): 256 bucket starts + the tile's row count, 16-B padded
 constexpr int kBitsB = 11;
 constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
 constexpr int kOffsB = kRadB + 8;          // offsB row (u16): 2048 starts + the tile's row count, padded to 16 B
@@ -211,7 +211,7 @@ struct MsdPartAParams {
     int64_t sel_val;
     const int64_t *spl;
     int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
-    uint32_t *offs;      // [tiles][kOffsA]
+    uint32_t *offs;      // [tiles][kOffsARow]
     int64_t *tmm;        // [tiles][2] min / max selected key
 };
 struct MsdPartA2 {       // one part_a launch over up to two tables
@@ -228,6 +228,8 @@ struct MsdBucket {       // per pass-A bucket and table
     uint32_t list_base;  // first run-list entry
     uint32_t nruns;      // run-list entries
     uint32_t tile_base;  // first pass-B tile
+    uint32_t one_key;    // the bucket's interval is a single key value (a heavy key's bucket)
+    uint32_t pad_;
 };
 struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t m[2];       // selected rows per table

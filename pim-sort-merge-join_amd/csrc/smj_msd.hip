@@ -10,9 +10,9 @@
 //
 // Data flow per table:
 //   sample    one workgroup sorts <= 16 Ki sampled keys of R and S (bitonic,
-//             LDS) and keeps 127 splitters; pass-A bucket of a key =
-//             2 * #{splitters < key} + (key == that splitter): 255 buckets,
-//             the odd ones hold exactly one key value (heavy keys).
+//             LDS) and keeps 255 splitters; pass-A bucket of a key =
+//             #{splitters < key} (+ 1 for a key the sample repeats: a heavy
+//             key gets a bucket to itself): 256 buckets.
 //   part_a    every tile of T rows (64 KiB) is select-filtered and stably
 //             partitioned by bucket IN ITS OWN REGION of tempA: one read, one
 //             fully coalesced write.  offsA[tile][bucket] = tile-local starts.
@@ -177,14 +177,17 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
     return all;
 }
 
-// pass-A bucket of a key: 2 * #{splitters < key} + (key == that splitter)
+// pass-A bucket of a key: pos = #{splitters < key}, or pos + 1 when the key
+// equals spl[pos] == spl[pos + 1] (a repeated splitter: a heavy key gets
+// bucket pos + 1 to itself; no other key maps there)
 __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
     int pos = 0;
 #pragma unroll
-    for (int step = 1 << (kSplABits - 1); step >= 1; step >>= 1)
-        pos += (s_spl[pos + step - 1] < k) ? step : 0;  // index <= kSplA - 1: kSplA = 2^kSplABits - 1 splitters
-    const bool eq = pos < kSplA && s_spl[pos < kSplA ? pos : kSplA - 1] == k;
-    return 2u * (uint32_t)pos + (eq ? 1u : 0u);
+    for (int step = kBucketsA / 2; step >= 1; step >>= 1)
+        pos += (s_spl[pos + step - 1] < k) ? step : 0;  // index <= kSplA - 1
+    const int q = pos + 1 < kSplA ? pos : kSplA - 2;
+    const bool rep = pos + 1 < kSplA && s_spl[q] == k && s_spl[q + 1] == k;
+    return (uint32_t)pos + (rep ? 1u : 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     const bool second = blockIdx.x >= q.tiles0;
     const MsdPartAParams &p = second ? q.t[1] : q.t[0];
     const unsigned bx = blockIdx.x - (second ? q.tiles0 : 0u);
-    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kOffsA;
+    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kBucketsA;
     constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
     constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
@@ -338,8 +341,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    static_assert(RADIX <= kMsdThreads, "one offsA entry per thread");
-    if (tid < RADIX) p.offs[t * kOffsA + tid] = s_bin[tid];  // s_bin[kBucketsA] = total (that bucket is never used)
+    static_assert(RADIX < kMsdThreads && RADIX < kOffsARow, "one offsA entry per thread");
+    if (tid <= RADIX) p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
     if (tid == 0) {
         p.tmm[2 * t] = mn;
         p.tmm[2 * t + 1] = mx;
@@ -495,15 +498,21 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     int64_t lo = 0;
     uint64_t scale = 0;
     uint32_t maxspan = kRadB;
+    bool one_key = false;
     if (a < kBucketsA) {
-        const int i = a >> 1;
+        // bucket a = (spl[a-1], spl[a]] (open ends: the global min / max),
+        // less a repeated splitter value, which is bucket i + 1 of its first
+        // occurrence i (bucket_a); buckets inside a run of repeats are empty
+        const int64_t *spl = p.spl;
         int64_t hi;
-        if (a & 1) {
-            lo = hi = p.spl[i];
+        if (a >= 1 && a < kSplA && spl[a] == spl[a - 1] && (a == 1 || spl[a - 2] != spl[a - 1])) {
+            lo = hi = spl[a - 1];  // a heavy key's own bucket
         } else {
-            lo = i == 0 ? mn : (int64_t)((uint64_t)p.spl[i - 1] + 1u);
-            hi = i == kSplA ? mx : (int64_t)((uint64_t)p.spl[i] - 1u);
+            lo = a == 0 ? mn : (int64_t)((uint64_t)spl[a - 1] + 1u);
+            hi = a == kSplA ? mx : spl[a];
+            if (a + 1 < kSplA && spl[a + 1] == spl[a]) hi = (int64_t)((uint64_t)spl[a] - 1u);  // repeated: not here
         }
+        one_key = lo == hi;
         const uint64_t range = hi > lo ? (uint64_t)hi - (uint64_t)lo : 0u;  // interval = range + 1 keys
         if (range >= (uint64_t)kRadB) {
             // k sub-buckets of ~kFill / k rows fill a group; a bucket too big for
@@ -545,6 +554,8 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             b.list_base = lb;
             b.nruns = C;
             b.tile_base = tb;
+            b.one_key = one_key ? 1u : 0u;
+            b.pad_ = 0;
             p.bk[x][a] = b;
         }
         if (a == 0) {
@@ -575,7 +586,7 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
     if (ok)
 #pragma unroll 8
         for (int64_t t = c0; t < c1; t++) {
-            const uint32_t len = offs[t * kOffsA + a + 1] - offs[t * kOffsA + a];
+            const uint32_t len = offs[t * kOffsARow + a + 1] - offs[t * kOffsARow + a];
             L += len;
             C += len ? 1u : 0u;
         }
@@ -591,8 +602,8 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
     const MsdBucket b = bk[a];
     const uint32_t uT = (uint32_t)TB;  // pass-B tile rows (T: pass-A tile rows)
     for (int64_t t = c0; t < c1; t++) {
-        const uint32_t o = offs[t * kOffsA + a];
-        const uint32_t len = offs[t * kOffsA + a + 1] - o;
+        const uint32_t o = offs[t * kOffsARow + a];
+        const uint32_t len = offs[t * kOffsARow + a + 1] - o;
         if (len) {
             list[b.list_base + Q] = make_uint2((uint32_t)(t * T) + o, P);
             for (uint32_t k = (P + uT - 1) / uT; k * uT < P + len; k++)  // pass-B tiles starting inside this run
@@ -966,7 +977,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         }
     }
     __syncthreads();
-    const bool single_sub = (a & 1) || p.bk[0][a].scale == 0;  // every sub-bucket holds one key value
+    const bool single_sub = p.bk[0][a].scale == 0;  // every sub-bucket holds one key value
     // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
@@ -1107,7 +1118,7 @@ __device__ __forceinline__ void group_gather(const MsdTab &tb, const MsdGroup &g
     const int tid = threadIdx.x;
     const MsdBucket bk = tb.bk[g.a];
     const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
-    if ((g.a & 1) && g.b0 == 0) {  // single-key bucket: its tiles are full and hold only sub-bucket 0
+    if (bk.one_key && g.b0 == 0) {  // single-key bucket: its tiles are full and hold only sub-bucket 0
         const uint32_t base = bk.tile_base * (uint32_t)tb.tile;
         for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads) fn(v, base + v);
         return;
@@ -2678,7 +2689,7 @@ hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s) {
 hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
                                const int64_t *tmm, int64_t *segmm, hipStream_t s) {
     const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
-    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsA, kBucketsA, segL, segC, tmm,
+    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsARow, kBucketsA, segL, segC, tmm,
                        segmm);
     return hipGetLastError();
 }
