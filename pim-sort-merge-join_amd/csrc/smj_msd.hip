@@ -177,6 +177,9 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
     return all;
 }
 
+// wave-uniform copy (SGPR) of a value loaded through a vector load
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 // pass-A bucket of a key: pos = #{splitters < key}, or pos + 1 when the key
 // equals spl[pos] == spl[pos + 1] (a repeated splitter: a heavy key gets
 // bucket pos + 1 to itself; no other key maps there)
@@ -569,48 +572,42 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     }
 }
 
-// grid (ceil(nb / 64), kMsdSegs) x 256: emit the run list entries of every
-// bucket (lane) for this segment, and the first run of every pass-B tile
+// grid (kBucketsA / 4, kMsdSegs) x 256: emit the run list entries of every
+// bucket for this segment, and the first run of every pass-B tile.  Wave =
+// bucket, lane = tile: the segment's runs of one bucket are 64 at a time
+// prefixed by two wave scans (rows, non-empty runs) and leave as consecutive
+// list entries (coalesced; a lane-per-bucket loop wrote 64 scattered 8-B
+// entries per store, 90 us per table at C3).  The offsA loads are strided,
+// but a 128-B line of a tile's row serves 32 buckets' waves from L2.
 __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__restrict__ offs, int64_t ntiles,
                                                              int T, int TB, const uint32_t *__restrict__ segL,
                                                              const uint32_t *__restrict__ segC,
                                                              const MsdBucket *__restrict__ bk,
                                                              uint2 *__restrict__ list, uint2 *__restrict__ tinfo) {
-    __shared__ uint32_t partL[4][64], partC[4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int a = blockIdx.x * 64 + lane;
-    const bool ok = a < kBucketsA;
-    int64_t c0, c1;
-    msd_seg_range(ntiles, c0, c1);
-    uint32_t L = 0, C = 0;
-    if (ok)
-#pragma unroll 8
-        for (int64_t t = c0; t < c1; t++) {
-            const uint32_t len = offs[t * kOffsARow + a + 1] - offs[t * kOffsARow + a];
-            L += len;
-            C += len ? 1u : 0u;
-        }
-    partL[w][lane] = L;
-    partC[w][lane] = C;
-    __syncthreads();
-    if (!ok) return;
+    const int lane = threadIdx.x & 63;
+    const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t Ls = (ntiles + kMsdSegs - 1) / kMsdSegs;
+    const int64_t c0 = min((int64_t)blockIdx.y * Ls, ntiles), c1 = min(c0 + Ls, ntiles);
     uint32_t P = segL[blockIdx.y * kOffsA + a], Q = segC[blockIdx.y * kOffsA + a];  // exclusive prefixes
-    for (int v = 0; v < w; v++) {
-        P += partL[v][lane];
-        Q += partC[v][lane];
-    }
-    const MsdBucket b = bk[a];
+    const uint32_t lbase = uni32(bk[a].list_base), tbase = uni32(bk[a].tile_base);
     const uint32_t uT = (uint32_t)TB;  // pass-B tile rows (T: pass-A tile rows)
-    for (int64_t t = c0; t < c1; t++) {
-        const uint32_t o = offs[t * kOffsARow + a];
-        const uint32_t len = offs[t * kOffsARow + a + 1] - o;
-        if (len) {
-            list[b.list_base + Q] = make_uint2((uint32_t)(t * T) + o, P);
-            for (uint32_t k = (P + uT - 1) / uT; k * uT < P + len; k++)  // pass-B tiles starting inside this run
-                tinfo[b.tile_base + k] = make_uint2((uint32_t)a, b.list_base + Q);
-            Q++;
-            P += len;
+    for (int64_t t0 = c0; t0 < c1; t0 += 64) {
+        const int64_t t = t0 + lane;
+        uint32_t o = 0, len = 0;
+        if (t < c1) {
+            o = offs[t * kOffsARow + a];
+            len = offs[t * kOffsARow + a + 1] - o;
         }
+        const uint32_t nz = len ? 1u : 0u;
+        const uint32_t il = wave_incl_scan(len, lane), iq = wave_incl_scan(nz, lane);
+        if (len) {
+            const uint32_t v = P + il - len, e = lbase + Q + iq - 1u;
+            list[e] = make_uint2((uint32_t)(t * T) + o, v);
+            for (uint32_t k = (v + uT - 1) / uT; k * uT < v + len; k++)  // pass-B tiles starting inside this run
+                tinfo[tbase + k] = make_uint2((uint32_t)a, e);
+        }
+        P += (uint32_t)__shfl((int)il, 63, 64);
+        Q += (uint32_t)__shfl((int)iq, 63, 64);
     }
 }
 
@@ -620,7 +617,6 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
 // ---------------------------------------------------------------------------
 // wave-uniform copies (SGPRs) of per-tile metadata loaded through vector loads
 // (kernel arguments may alias the outputs, so hipcc cannot use scalar loads)
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
 }
@@ -1935,6 +1931,15 @@ __device__ __forceinline__ int opaque_tid() {
     return t;
 }
 
+// Ablation bits of the staged kernel (timing only, output invalid), compiled
+// in with -DSMJ_ABLATE=1 (tools/final_ablate.py through smj_debug_final_time):
+// 2 = no sorted-row stores, 4 = synthetic rows instead of the gathers,
+// 8 = no join rows, 16 = no equal-key fix-up rounds
+#ifndef SMJ_ABLATE
+#define SMJ_ABLATE 0
+#endif
+#define ST_ABL(bit) (SMJ_ABLATE && (p.dbg & (bit)))
+
 __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g) {
     return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStList &&
            (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList);
@@ -2015,7 +2020,12 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
                                    ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
                 const uint32_t j = m ? sm.L.at[x][(b << 6) + 63 - __clzll((long long)m)] : sm.L.btab[x][b];
                 const uint2 e = sm.L.list[x][j];
-                r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[e.x + (v - e.y)];
+                if (ST_ABL(4)) {
+                    const int64_t k = g.base + (int64_t)((v * 3u) % max(g.span, 1u));
+                    r = {p.tab[x].key ? (int64_t)v : k, p.tab[x].key ? k : (int64_t)v};
+                } else {
+                    r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[e.x + (v - e.y)];
+                }
             }
             rows[x][k] = r;
         }
@@ -2120,7 +2130,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // (Measured slower: ranking each run member by a scan of its run, r01k;
     // the run's first thread insertion-sorting the run, r01ah: 2.81 vs 2.32 ms.)
     static_assert(kGroupCap / 2 <= kStThreads, "one compare-exchange per thread per table and round");
-    for (uint32_t rd = 0; rd < fl; rd++) {
+    for (uint32_t rd = 0; rd < (ST_ABL(16) ? 0u : fl); rd++) {
 #pragma unroll
         for (int x = 0; x < 2; x++) {
             const int q = 2 * tid + (int)(rd & 1u);
@@ -2180,7 +2190,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 #pragma unroll
         for (int k = 0; k < kStIt; k++) {
             const int q = tid + k * kStThreads;
-            if (q < n[x]) {
+            if (q < n[x] && !ST_ABL(2)) {
                 const uint32_t w = sm.key[x][q];
                 const int64_t key = g.base + (int64_t)(w >> kFinIdxBits), pay = sm.pay[x][w & IDX];
                 i64x2 r;
@@ -2190,7 +2200,7 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
             }
         }
     }
-    if (!p.join) return;
+    if (!p.join || ST_ABL(8)) return;
     const uint32_t *kR = sm.key[0], *kS = sm.key[1];
     uint32_t total;
     uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
@@ -2712,7 +2722,8 @@ hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
 hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
                                  const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
                                  hipStream_t s) {
-    const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
+    static_assert(kBucketsA % 4 == 0, "four buckets (waves) per workgroup");
+    const dim3 grid(kBucketsA / 4, kMsdSegs);
     hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, offs, ntiles, T, TB, segL, segC, bk, list, tinfo);
     return hipGetLastError();
 }

@@ -20,6 +20,11 @@ S = ops.gen_uniform(n, seed=2, key_range=3 * n)
 ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000))
 torch.cuda.synchronize()
 ms = ctypes.c_float()
-for dbg, name in [(0, "baseline"), (64, "1 workgroup per CU"), (0, "baseline"), (64, "1 workgroup per CU")]:
+CASES = [(0, "baseline"), (64, "1 workgroup per CU"), (2, "no sorted-row stores"), (8, "no join rows"),
+         (10, "no stores at all"), (4, "synthetic rows (no gathers)"), (14, "no gathers, no stores"),
+         (16, "no equal-key rounds"), (30, "no gathers/stores/rounds"), (0, "baseline")]
+if os.environ.get("DBG"):  # e.g. DBG=0,2,8
+    CASES = [(int(b), f"bits {b}") for b in os.environ["DBG"].split(",")]
+for dbg, name in CASES:
     assert lib.smj_debug_final_time(dbg, 5, ctypes.byref(ms)) == 0
-    print(f"dbg {dbg:2d} {name:24s} {ms.value:.3f} ms", flush=True)
+    print(f"dbg {dbg:2d} {name:28s} {ms.value:.3f} ms", flush=True)
