@@ -652,6 +652,15 @@ __device__ unsigned long long g_pb_phase[8];
         pb_t = t_;                                                  \
     }
 
+// threadIdx.x as a value the compiler may not hoist out of the group loop:
+// per-lane addresses are recomputed where used instead of living (spilled)
+// across the whole loop
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 constexpr int kPbFastMax = 16;  // longest sub-bucket run of a tile the atomic-rank path orders
 
 template <int COLS>
@@ -660,27 +669,32 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
     constexpr int NT = pb_threads(COLS), NW = NT / 64, T = msd_tile_b(COLS), ITEMS = T / NT, RADIX = kRadB;
     constexpr int DPT = RADIX / NT;  // histogram digits per thread (even)
     static_assert(T % NT == 0 && RADIX % (2 * NT) == 0, "tile / histogram split");
-    // One LDS region, reused per phase: (1) the run list + lookup aids
-    // (at[r] = entry of the run starting at tile row r, a bitmap of run
-    // starts, btab[b] = entry holding tile row 64 * b); (2) the atomic path's
-    // tile-row permutation + the ballot path's counters; (3) the staging tile.
-    // ~36 KiB for 2 columns: 3-4 workgroups per CU (part_b is latency-bound:
-    // one workgroup per CU instead of two costs +54 %, tools/pb_ablate.py).
-    constexpr int LISTB = (T + 1) * 8, ATB = T * 2, BMB = T / 8, BTB = T / 64 * 2;
+    // One LDS region, reused per phase: (1) the run list + lookup aids (a
+    // bitmap of run starts, btab[b] = entry holding tile row 64 * b: row r's
+    // entry is btab[r / 64] + the run starts in (64 (r / 64), r], a popcount);
+    // (2) the atomic path's tile-row permutation + the ballot path's
+    // counters; (3) the staging tile.  Part_b is latency-bound: one workgroup
+    // per CU instead of two costs +54 % (tools/pb_ablate.py).
+    constexpr int LISTB = (T + 1) * 8, ATB = 0, BMB = T / 8, BTB = T / 64 * 2;
     constexpr int ROWB = T * COLS * 8, PERMB = T * 2, CNTB = RADIX * 4, LKB = LISTB + ATB + BMB + BTB;
-    constexpr int UB0 = ROWB > PERMB + CNTB ? ROWB : PERMB + CNTB;
-    constexpr int UB = UB0 > LKB ? UB0 : LKB;
+    // the per-quad sub-bucket counts (below) sit past the lists, perm and
+    // counters: zeroed while the list is live, dead before the tile is staged
+    static_assert(NW % 4 == 0, "quads of waves");
+    constexpr int QN = NW / 4, QW = (QN + 1) / 2, QB = QW * RADIX * 4;
+    constexpr int QOFF0 = LKB > PERMB + CNTB ? LKB : PERMB + CNTB, QOFF = (QOFF0 + 15) / 16 * 16;
+    constexpr int UB = ROWB > QOFF + QB ? ROWB : QOFF + QB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
-    __shared__ uint32_t s_hist[RADIX / 2];  // packed u16 sub-bucket counts, then starts
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint32_t s_slow;
     uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_u);
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_u + PERMB);
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
     uint2 *s_list = reinterpret_cast<uint2 *>(s_u);
-    uint16_t *s_at = reinterpret_cast<uint16_t *>(s_u + LISTB);
     uint32_t *s_bm = reinterpret_cast<uint32_t *>(s_u + LISTB + ATB);
     uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + ATB + BMB);
+    // sub-bucket counts per quad of waves (u16 halves of word (quad >> 1) *
+    // RADIX + d), then each quad's first tile row of sub-bucket d
+    uint32_t *s_q = reinterpret_cast<uint32_t *>(s_u + QOFF);
 
     // persistent over tiles g = blockIdx.x + k * gridDim.x.  The next tile's
     // metadata chain (tinfo -> bucket -> first run-list entries) is issued
@@ -705,14 +719,18 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
     // this path (nothing issued after the load) with the back edge and hipcc
     // waits vmcnt(0) every tile, draining the previous tile's 64 KiB of stores
     asm volatile("" ::"v"(le));
-#pragma unroll
-    for (int k = 0; k < DPT / 2; k++) s_hist[DPT / 2 * tid + k] = 0;
     if (tid == 0) s_slow = 0;
+    // quad of waves of this thread, its count half and word row (recomputed
+    // where used: live across the tile loop they spilled)
+    auto quad_of = [&]() { return (uint32_t)opaque_tid() >> 8; };
     for (; g < ntl; g += gridDim.x) {
+        // per-lane values recomputed per tile (live across the loop they spill)
+        const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
         const uint32_t v0 = (uint32_t)(g - b.tile_base) * (uint32_t)T;
         const int nrows = (int)min((uint32_t)T, b.L - v0);
         const uint32_t q0 = ti.y;
         const int J = (int)runs_of(ti, b, g);
+        for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
         if (p.dbg & 32) goto lookups_done;
         if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
         for (int j = tid + NT; j < J; j += NT)  // > NT runs: rare
@@ -724,7 +742,6 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
             const uint32_t s0 = y > v0 ? y - v0 : 0u;
             const uint32_t e = j + 1 < J ? s_list[j + 1].y - v0 : (uint32_t)nrows;
             if (s0 < (uint32_t)nrows) {
-                s_at[s0] = (uint16_t)j;
                 atomicOr(&s_bm[s0 >> 5], 1u << (s0 & 31));
                 for (uint32_t bb = (s0 + 63) >> 6; (bb << 6) < e && (bb << 6) < (uint32_t)nrows; bb++)
                     s_bt[bb] = (uint16_t)j;
@@ -740,7 +757,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         for (int it = 0; it < ITEMS; it++) {
             const uint32_t r = (uint32_t)min(lrow0 + it * 64, nrows - 1), bb = r >> 6;
             const uint64_t m = ((uint64_t)s_bm[2 * bb + 1] << 32 | s_bm[2 * bb]) & ((2ull << (r & 63)) - 1ull) & ~1ull;
-            const uint32_t j = m ? s_at[(bb << 6) + 63 - __clzll((long long)m)] : s_bt[bb];
+            const uint32_t j = s_bt[bb] + (uint32_t)__popcll(m);  // run starts in (64 bb, r]
             const uint2 e = s_list[j];
             if (p.dbg & 4) {
 #pragma unroll
@@ -764,56 +781,74 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
-        // Atomic path: one packed-u16 LDS histogram, ranks in atomic order.
-        // Stability is restored per row below (sub-bucket runs of a tile are
-        // short); a tile with a sub-bucket over kPbFastMax rows takes the
-        // ballot path instead (wave_rank + per-wave counters).
+        // Atomic path: per quad of waves one u16 count per sub-bucket, ranks in
+        // atomic order.  Stability is restored per row below among the rows
+        // of its quad and sub-bucket (usually none or one other); a tile with
+        // a quad's sub-bucket over kPbFastMax rows takes the ballot path
+        // instead (wave_rank + per-wave counters).  (A whole-tile count and a
+        // fix-up over the tile's sub-bucket run cost ~2x the fix-up rounds.)
+        {
+            const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
 #pragma unroll
-        for (int it = 0; it < ITEMS; it++)
-            if ((vmask >> it) & 1u) {
-                const uint32_t d = dig[it], sh = 16u * (d & 1u);
-                dig[it] = d | (((atomicAdd(&s_hist[d >> 1], 1u << sh) >> sh) & 0xffffu) << 16);
-            }
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it];
+                    dig[it] = d | (((atomicAdd(&s_q[qrow + d], 1u << qsh) >> qsh) & 0xffffu) << 16);
+                }
+        }
         const MsdBucket bn = uni_bucket(p.bk, tin.x);  // prefetch 2: its bucket
         __syncthreads();
         PB_STAMP(2);
-        {  // thread t owns digits [DPT t, DPT t + DPT): counts -> starts, packed alike
-            uint32_t hw[DPT / 2], sum = 0, cmax = 0;
+        {  // counts -> per-quad first rows, in place; the tile's sub-bucket starts -> offsB
+            uint32_t sum = 0, cmax = 0;
 #pragma unroll
-            for (int k = 0; k < DPT / 2; k++) {
-                hw[k] = s_hist[DPT / 2 * tid + k];
-                const uint32_t lo = hw[k] & 0xffffu, hi = hw[k] >> 16;
-                sum += lo + hi;
-                cmax = max(cmax, max(lo, hi));
-            }
+            for (int k = 0; k < DPT; k++)
+#pragma unroll
+                for (int q2 = 0; q2 < QW; q2++) {
+                    const uint32_t w = s_q[q2 * RADIX + DPT * tid + k];
+                    sum += (w & 0xffffu) + (w >> 16);
+                    cmax = max(cmax, max(w & 0xffffu, w >> 16));
+                }
             if (cmax > (uint32_t)kPbFastMax || (p.dbg & 16)) s_slow = 1;
             uint32_t tot;
             uint32_t st = block_excl_scan_nb<NW>(sum, s_wsum, &tot);  // + barrier
+            uint32_t sw = 0;
 #pragma unroll
-            for (int k = 0; k < DPT / 2; k++) {
-                const uint32_t lo = hw[k] & 0xffffu, hi = hw[k] >> 16;
-                s_hist[DPT / 2 * tid + k] = st | ((st + lo) << 16);
-                st += lo + hi;
+            for (int k = 0; k < DPT; k++) {
+                sw = (k & 1) ? sw | (st << 16) : st;
+                if ((k & 1) && !(p.dbg & 8)) reinterpret_cast<uint32_t *>(p.offs + g * kOffsB)[DPT / 2 * tid + k / 2] = sw;
+#pragma unroll
+                for (int q2 = 0; q2 < QW; q2++) {
+                    const uint32_t w = s_q[q2 * RADIX + DPT * tid + k];
+                    const uint32_t b1 = st + (w & 0xffffu);
+                    s_q[q2 * RADIX + DPT * tid + k] = st | (b1 << 16);
+                    st = b1 + (w >> 16);
+                }
             }
+            static_assert(kOffsB % 2 == 0 && DPT % 2 == 0, "offsB rows 4-B aligned: starts leave two per word");
+            if (tid == 0 && !(p.dbg & 8)) p.offs[g * kOffsB + RADIX] = (uint16_t)nrows;
         }
         __syncthreads();
         const bool slow = s_slow != 0;
         if (!slow) {
+            const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
                 if ((vmask >> it) & 1u) {
-                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u);
-                    s_perm[((s_hist[d >> 1] >> sh) & 0xffffu) + (dig[it] >> 16)] = (uint16_t)(lrow0 + it * 64);
+                    const uint32_t d = dig[it] & 0xffffu;
+                    s_perm[((s_q[qrow + d] >> qsh) & 0xffffu) + (dig[it] >> 16)] = (uint16_t)(lrow0 + it * 64);
                 }
             __syncthreads();
-            // stable rank: the rows of the sub-bucket run that precede this one in the tile
+            // stable rank: the rows of this quad's sub-bucket group that precede this one
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
                 if ((vmask >> it) & 1u) {
-                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u), hw = s_hist[d >> 1];
-                    const uint32_t st = (hw >> sh) & 0xffffu;
-                    const uint32_t en = (d & 1u) ? (d + 1u < (uint32_t)RADIX ? (s_hist[(d + 1) >> 1] & 0xffffu) : (uint32_t)nrows)
-                                                 : (hw >> 16);
+                    const uint32_t d = dig[it] & 0xffffu, w = s_q[qrow + d];
+                    const uint32_t st = (w >> qsh) & 0xffffu;
+                    uint32_t en;  // the next quad's first row of d (quad is wave-uniform)
+                    if (!(quad & 1)) en = w >> 16;
+                    else if (quad + 1 < QN) en = s_q[qrow + RADIX + d] & 0xffffu;
+                    else en = d + 1u < (uint32_t)RADIX ? (s_q[d + 1] & 0xffffu) : (uint32_t)nrows;
                     const uint32_t r = (uint32_t)(lrow0 + it * 64);
                     uint32_t rank = 0;
                     if (en - st > 1u)
@@ -836,8 +871,8 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
                 if ((vmask >> it) & 1u) {
-                    const uint32_t d = dig[it] & 0xffffu, sh = 16u * (d & 1u);
-                    dig[it] = ((s_hist[d >> 1] >> sh) & 0xffffu) + (dig[it] >> 16);
+                    const uint32_t d = dig[it] & 0xffffu;
+                    dig[it] = (s_q[d] & 0xffffu) + (dig[it] >> 16);  // quad 0's first row = the sub-bucket start
                 }
         }
         __syncthreads();  // permutation / counters dead: the region becomes the staging tile
@@ -846,17 +881,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         for (int it = 0; it < ITEMS; it++)
             if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
         if (gn < ntl && (uint32_t)tid < runs_of(tin, bn, gn)) le = list64[tin.y + tid];  // prefetch 3: its runs
-        if (!(p.dbg & 8)) {
-            uint16_t *o = p.offs + g * kOffsB;
-            static_assert(kOffsB % 2 == 0, "offsB rows 4-B aligned: packed starts leave as u32 words");
-#pragma unroll
-            for (int k = 0; k < DPT / 2; k++)  // thread t's starts, two per word as packed in s_hist
-                reinterpret_cast<uint32_t *>(o)[DPT / 2 * tid + k] = s_hist[DPT / 2 * tid + k];
-            if (tid == 0) o[RADIX] = (uint16_t)nrows;
-        }
         __syncthreads();
-#pragma unroll
-        for (int k = 0; k < DPT / 2; k++) s_hist[DPT / 2 * tid + k] = 0;  // for the next tile
         if (tid == 0) s_slow = 0;
         PB_STAMP(4);
         int64_t *dst = p.out + g * T * COLS;
@@ -1922,14 +1947,6 @@ struct StSmem {
     uint32_t flag[2];
 };
 
-// threadIdx.x as a value the compiler may not hoist out of the group loop:
-// per-lane addresses are recomputed where used instead of living (spilled)
-// across the whole loop
-__device__ __forceinline__ int opaque_tid() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
 
 // Ablation bits of the staged kernel (timing only, output invalid), compiled
 // in with -DSMJ_ABLATE=1 (tools/final_ablate.py through smj_debug_final_time):
@@ -1974,7 +1991,9 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
 // run lists from the offsB values (union region), then the row gathers of
 // group g into registers (row v = tid + k * kStThreads).  Row v's range is
 // found in O(1): the range holding the wave's first row (btab) and the last
-// non-empty range starting in (64b, v] (bitmap word + at[]).
+// non-empty range starting in (64b, v] (bitmap word + at[]; the list also
+// holds the group's empty ranges, so a popcount of the bitmap would not
+// index it).
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
     const uint32_t tid = opaque_tid();
