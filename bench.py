@@ -134,7 +134,7 @@ def main():
     prof = ops.prof_report()
     if world == 1:
         log(f"msd stats (single-key groups, LSD-fallback groups, mR, mS): {ops.msd_stats()}; "
-            f"(groups, radix-tier, wide-tier): {ops.msd_groups()}")
+            f"(groups, radix-tier, wide-tier, in-LDS LSD): {ops.msd_groups()}")
 
     joined = int(res) if world == 1 else int(res.shape[0])
     t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=dev)

@@ -295,6 +295,9 @@ void smj_debug_msd_stats(int64_t *out4);
 /* Final-stage group counts of the last MSD pipeline call: out3[0] = LDS
  * (dense) groups, out3[1] = radix-tier groups, out3[2] = 64-bit-tier groups. */
 void smj_debug_msd_groups(int64_t *out3);
+/* The same plus out4[3] = staged groups whose equal-key runs (over 32 rows)
+ * were ordered by the in-LDS stable LSD instead of the transposition rounds. */
+void smj_debug_msd_tiers(int64_t *out4);
 /* Run every pipeline call in the partitioned mode with `parts` key-range
  * parts (tests); 0 = automatic (tables over 1.6e8 rows). */
 void smj_debug_force_parts(int parts);

@@ -480,7 +480,7 @@ struct MsdScratch {
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
-int64_t g_msd_groups[3] = {0, 0, 0};  // last pipeline: dense groups, radix-tier groups, wide-tier groups
+int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -913,6 +913,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         g_msd_groups[0] = ms->h_plan->ngroups;
         g_msd_groups[1] = ms->h_plan->nradix;
         g_msd_groups[2] = ms->h_plan->nwide;
+        g_msd_groups[3] = ms->h_plan->nlsd;
     }
     bool redo = false;
     SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
@@ -1229,6 +1230,10 @@ extern "C" int smj_debug_final_time(int dbg, int reps, float *ms) {
 // Diagnostic: final-stage group counts of the last MSD pipeline (smj.h).
 extern "C" void smj_debug_msd_groups(int64_t *out3) {
     for (int i = 0; i < 3; i++) out3[i] = g_msd_groups[i];
+}
+
+extern "C" void smj_debug_msd_tiers(int64_t *out4) {
+    for (int i = 0; i < 4; i++) out4[i] = g_msd_groups[i];
 }
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {

@@ -240,7 +240,7 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t ngroups;    // dense groups (key order)
     uint32_t nwide;      // groups for the 64-bit final path
     uint32_t nradix;     // groups for the radix-sort final path
-    uint32_t pad2;
+    uint32_t nlsd;       // staged groups sorted by the in-LDS LSD (equal-key runs over kMaxDupRun)
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)

@@ -2053,6 +2053,77 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
 
 __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key ? r.y : r.x; }
 
+// Stable LSD sort of a group's sort words by their residual (two 6-bit
+// digits) for groups whose equal-key runs are too long for the odd-even
+// rounds (Zipf-skewed keys: C5).  w[x][k] = the word of group row
+// v = tid + k * kStThreads (~0u: none; overwritten); words leave sorted in
+// sm.key[x].
+// A pass ranks each (item, wave) group of 64 rows by wave ballots on the
+// digit, prefixes the 16 groups' counts per digit (v order = item, wave,
+// lane) and scatters; pass 2 reads pass 1's order back the same way.
+// Counters: 2 x 16 x 64 words in the list region (idle during the sort).
+__device__ __forceinline__ void st_lsd(uint32_t (&cur)[2][kStIt], const int (&n)[2], StSmem &sm) {
+    constexpr int G = kStIt * kStWaves, DB = 6, D = 1 << DB;
+    static_assert(G * D * 4 <= (int)sizeof(sm.L.list) + (int)sizeof(sm.L.at), "LSD counters fit the list region");
+    static_assert(kStRange <= (1 << (2 * DB)), "two digits cover the residual");
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(&sm.L.list[0][0]);  // [g][d]
+    const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {  // one table at a time (register pressure)
+        if (n[x] == 0) continue;
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+            const int sh = kFinIdxBits + DB * pass;
+            for (int i = tid; i < G * D; i += kStThreads) cnt[i] = 0;
+            __syncthreads();
+            uint32_t rk[kStIt];
+#pragma unroll
+            for (int k = 0; k < kStIt; k++) {
+                const bool v = cur[x][k] != ~0u;
+                const uint32_t d = (cur[x][k] >> sh) & (D - 1);
+                const uint64_t act = __ballot(v);
+                uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
+#pragma unroll
+                for (int b = 0; b < DB; b++) {
+                    const uint32_t sb = (uint32_t)((int32_t)(d << (31 - b)) >> 31);
+                    const uint64_t bb = __ballot(sb != 0u);
+                    plo = peer_fold(plo, (uint32_t)bb, sb);
+                    phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
+                }
+                rk[k] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+                const uint64_t peers = ((uint64_t)phi << 32) | plo;
+                if (v && (peers >> lane) == 1ull) cnt[(k * kStWaves + wave) * D + d] = (uint32_t)__popcll(peers);
+            }
+            __syncthreads();
+            if (tid < D) {  // lane d: prefix over the groups in v order, then over the digits
+                uint32_t t = 0;
+#pragma unroll 4
+                for (int g = 0; g < G; g++) t += cnt[g * D + tid];
+                uint32_t run = wave_incl_scan(t, lane) - t;
+#pragma unroll 4
+                for (int g = 0; g < G; g++) {
+                    const uint32_t c = cnt[g * D + tid];
+                    cnt[g * D + tid] = run;
+                    run += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kStIt; k++)
+                if (cur[x][k] != ~0u)
+                    sm.key[x][cnt[(k * kStWaves + wave) * D + ((cur[x][k] >> sh) & (D - 1))] + rk[k]] = cur[x][k];
+            __syncthreads();
+            if (pass == 0) {
+#pragma unroll
+                for (int k = 0; k < kStIt; k++) {
+                    const int o = tid + k * kStThreads;
+                    cur[x][k] = o < n[x] ? sm.key[x][o] : ~0u;
+                }
+            }
+        }
+    }
+}
+
 // stage + counting sort of group g whose rows are in `rows`, then the zip
 // join lookups (mmask / part); false: an equal-key run over kMaxDupRun (the
 // group is handed to the radix list)
@@ -2063,7 +2134,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
-    uint32_t w[2][kStIt], rank[2][kStIt];
+    uint32_t w[2][kStIt];  // residual << 16 | atomic rank among its equal residuals (~0u: no row)
     if (tid == 0) sm.flag[wsb] = 0;  // longest equal-key run (0: none)
     // for the next group's st_issue_lists (the list region is idle until then;
     // the barriers below order this before its atomicOr)
@@ -2074,13 +2145,11 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
         for (int k = 0; k < kStIt; k++) {
             const int v = tid + k * kStThreads;
             w[x][k] = ~0u;
-            rank[x][k] = 0;
             if (v < n[x]) {
                 sm.pay[x][v] = p.tab[x].key ? rows[x][k].x : rows[x][k].y;
                 const uint32_t res = (uint32_t)((uint64_t)st_key(rows[x][k], p.tab[x].key) - (uint64_t)g.base);
-                w[x][k] = (res << kFinIdxBits) | (uint32_t)v;
                 const uint32_t sh = 16u * (res & 1u);
-                rank[x][k] = (atomicAdd(&sm.hist[x][res >> 1], 1u << sh) >> sh) & 0xffffu;
+                w[x][k] = (res << 16) | ((atomicAdd(&sm.hist[x][res >> 1], 1u << sh) >> sh) & 0xffffu);
             }
         }
     __syncthreads();
@@ -2119,10 +2188,8 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     const uint32_t fl = sm.flag[wsb];
     wsb ^= 1;
     ST_SUB(1);
-    if (fl > (uint32_t)kMaxDupRun) {
-        if (tid == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
-        return false;
-    }
+    const bool lsd = fl > (uint32_t)kMaxDupRun;  // block-uniform
+    if (lsd && tid == 0) atomicAdd(&p.plan->nlsd, 1u);
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);
@@ -2134,22 +2201,32 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
         }
     }
     __syncthreads();
+    if (lsd) {  // an equal-key run over kMaxDupRun: stable LSD instead of scatter + rounds
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+        for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int k = 0; k < kStIt; k++)
-            if (w[x][k] != ~0u) {
-                const uint32_t res = w[x][k] >> kFinIdxBits, sh = 16u * (res & 1u);
-                sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + rank[x][k]] = w[x][k];
-            }
-    __syncthreads();
+            for (int k = 0; k < kStIt; k++)
+                if (w[x][k] != ~0u) w[x][k] = ((w[x][k] >> 16) << kFinIdxBits) | (uint32_t)(tid + k * kStThreads);
+        st_lsd(w, n, sm);
+    } else {
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int k = 0; k < kStIt; k++)
+                if (w[x][k] != ~0u) {
+                    const uint32_t res = w[x][k] >> 16, sh = 16u * (res & 1u);
+                    sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + (w[x][k] & 0xffffu)] =
+                        (res << kFinIdxBits) | (uint32_t)(tid + k * kStThreads);
+                }
+        __syncthreads();
+    }
     ST_SUB(2);
     // equal residuals were placed in atomic order: odd-even transposition
     // rounds (as many as the longest run) order every run by group row.
     // (Measured slower: ranking each run member by a scan of its run, r01k;
     // the run's first thread insertion-sorting the run, r01ah: 2.81 vs 2.32 ms.)
     static_assert(kGroupCap / 2 <= kStThreads, "one compare-exchange per thread per table and round");
-    for (uint32_t rd = 0; rd < (ST_ABL(16) ? 0u : fl); rd++) {
+    for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd) ? 0u : fl); rd++) {
 #pragma unroll
         for (int x = 0; x < 2; x++) {
             const int q = 2 * tid + (int)(rd & 1u);

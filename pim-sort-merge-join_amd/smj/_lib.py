@@ -61,6 +61,7 @@ SIGNATURES = {
     "smj_zipf_zeta": (_D, [_L, _D]),
     "smj_debug_msd_stats": (None, [_PL]),
     "smj_debug_msd_groups": (None, [_PL]),
+    "smj_debug_msd_tiers": (None, [_PL]),
     "smj_debug_force_parts": (None, [_I]),
     "smj_prof_enable": (None, [_I]),
     "smj_prof_report": (_I, [ctypes.c_char_p, ctypes.c_size_t]),
@@ -99,6 +100,8 @@ def load(build_if_missing=True):
             raise ImportError(f"{LIB_PATH} is missing: run `make -C {PKG_DIR}`")
         lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("SMJ_LIB") and not hasattr(lib, name):
+                continue  # an older build loaded for a same-box A/B (tools/ab.sh)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -154,9 +154,14 @@ def msd_stats():
 
 
 def msd_groups():
-    """(dense groups, radix-tier groups, wide-tier groups) of the last MSD pipeline call."""
-    out = (ctypes.c_int64 * 3)()
-    _lib.load().smj_debug_msd_groups(out)
+    """(dense groups, radix-tier groups, wide-tier groups, in-LDS LSD groups) of the
+    last MSD pipeline call."""
+    out = (ctypes.c_int64 * 4)()
+    lib = _lib.load()
+    if hasattr(lib, "smj_debug_msd_tiers"):
+        lib.smj_debug_msd_tiers(out)
+    else:  # an older build under SMJ_LIB (A/B): no in-LDS LSD count
+        lib.smj_debug_msd_groups(out)
     return tuple(int(v) for v in out)
 
 

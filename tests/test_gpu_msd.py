@@ -133,6 +133,32 @@ def test_multi_key_oversized_group_falls_back(gpu, oracle_built):
     np.testing.assert_array_equal(host(gJ), J)
 
 
+@pytest.mark.parametrize("nkeys,n,cols", [(2_000, 200_000, 2), (30_000, 600_000, 2), (5_000, 150_000, 3)])
+def test_long_equal_key_runs_in_lds(gpu, oracle_built, nkeys, n, cols):
+    """Equal-key runs of 20-300 rows inside LDS-sized groups (the shape of
+    C5's Zipf tables below the heavy keys): the staged final kernel orders
+    them by its stable in-LDS LSD instead of handing the group to the radix
+    tier, bit-exact against the oracle."""
+    from smj import ops
+    rng = np.random.default_rng(nkeys + n)
+
+    def make(rows, pay0):
+        t = rng.integers(-(1 << 40), 1 << 40, size=(rows, cols), dtype=np.int64)
+        t[:, 0] = rng.integers(0, nkeys, size=rows) * 977 - 5_000_000
+        t[:, 1] = pay0 + np.arange(rows)
+        return t
+
+    R, S = make(n, 0), make(n * 3 // 4, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S))
+    dense, radix, wide, lsd = ops.msd_groups()
+    if cols == 2:  # (other widths take the generic final kernel)
+        assert lsd > 0 and radix == 0, (dense, radix, wide, lsd)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
 @pytest.mark.parametrize("c1,c2,sel", [(2, 2, None), (3, 4, (2, -(1 << 62) + (1 << 58)))])
 def test_many_oversized_groups_batched(gpu, oracle_built, c1, c2, sel):
     """Hundreds of oversized multi-key groups (the shape Zipf tables produce
