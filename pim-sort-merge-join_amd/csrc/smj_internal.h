@@ -229,7 +229,7 @@ struct MsdBucket {       // per pass-A bucket and table
     uint32_t nruns;      // run-list entries
     uint32_t tile_base;  // first pass-B tile
     uint32_t one_key;    // the bucket's interval is a single key value (a heavy key's bucket)
-    uint32_t pad_;
+    uint32_t s32;        // != 0 (interval < 2^32 keys): the digit is mulhi32(r, s32) instead
 };
 struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t m[2];       // selected rows per table

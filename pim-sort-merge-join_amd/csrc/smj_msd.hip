@@ -500,7 +500,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     // 2 x 448 = 896 of 1024 rows instead of 2 x 381 = 762 with D = kRadB.
     int64_t lo = 0;
     uint64_t scale = 0;
-    uint32_t maxspan = kRadB;
+    uint32_t maxspan = kRadB, s32 = 0;
     bool one_key = false;
     if (a < kBucketsA) {
         // bucket a = (spl[a-1], spl[a]] (open ends: the global min / max),
@@ -532,10 +532,16 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             }
             const unsigned __int128 q = ((unsigned __int128)D << 64) / ((unsigned __int128)range + 1u);
             scale = q >> 64 ? ~0ull : (uint64_t)q;
-            // keys per sub-bucket <= ceil((range + 1) / D) + 1 <= range / D + 2 =: w.  Group spans
-            // stay within the final kernel's counting range when one sub-bucket fits it,
-            // else below 2^48 (the radix tiers' sort word)
-            const uint64_t w = range / D + 2u;
+            // an interval under 2^32 keys takes a 32-bit digit, mulhi32(r, s32)
+            // (one multiply in part_b instead of a 64 x 64 high product)
+            if (range < 0xffffffffull) s32 = (uint32_t)(((uint64_t)D << 32) / (range + 1u));
+            // keys per sub-bucket <= ceil(2^K / scale) + 1 =: w (K = 64, or 32
+            // with s32; ~(range + 1) / D + 2).  Group spans stay within the final
+            // kernel's counting range when one sub-bucket fits it, else below
+            // 2^48 (the radix tiers' sort word); the group kernel computes the
+            // exact span of every group
+            const uint64_t w = s32 ? ((1ull << 32) + s32 - 1u) / s32 + 1u
+                                   : (uint64_t)((((unsigned __int128)1 << 64) + scale - 1u) / scale) + 1u;
             const uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
             maxspan = span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
         }
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             b.nruns = C;
             b.tile_base = tb;
             b.one_key = one_key ? 1u : 0u;
-            b.pad_ = 0;
+            b.s32 = s32;
             p.bk[x][a] = b;
         }
         if (a == 0) {
@@ -629,6 +635,7 @@ __device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a)
     MsdBucket r;
     r.lo = (int64_t)uni64((uint64_t)v.lo);
     r.scale = uni64(v.scale);
+    r.s32 = uni32(v.s32);
     r.maxspan = uni32(v.maxspan);
     r.L = uni32(v.L);
     r.row_start = uni32(v.row_start);
@@ -777,7 +784,9 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         for (int it = 0; it < ITEMS; it++) {
             const bool v = lrow0 + it * 64 < nrows;
             const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
-            const uint32_t d = b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1)) : (uint32_t)r;
+            const uint32_t d = b.s32     ? __umulhi((uint32_t)r, b.s32)  // < D: r < 2^32 in such a bucket
+                               : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1))
+                                         : (uint32_t)r;
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
@@ -1082,10 +1091,15 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         }
         // key interval of sub-buckets [b0, b1): residuals r = key - lo with
         // digit(r) = floor(r * scale / 2^64) in [b0, b1) satisfy rmin(b0) <= r < rmin(b1),
-        // rmin(b) = ceil(b * 2^64 / scale); with scale == 0 the digit is r itself
+        // rmin(b) = ceil(b * 2^64 / scale) (2^32 and s32 for a 32-bit digit);
+        // with scale == 0 the digit is r itself
         const uint64_t sc = p.bk[0][a].scale;
+        const uint32_t s32 = p.bk[0][a].s32;
         unsigned __int128 r0 = b0, r1 = b1;
-        if (sc) {
+        if (s32) {
+            r0 = (((uint64_t)b0 << 32) + s32 - 1u) / s32;
+            r1 = (((uint64_t)b1 << 32) + s32 - 1u) / s32;
+        } else if (sc) {
             r0 = (((unsigned __int128)b0 << 64) + sc - 1) / sc;
             r1 = (((unsigned __int128)b1 << 64) + sc - 1) / sc;
         }
@@ -2183,8 +2197,12 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
         b1 += u < wave ? sm.wsum[wsb][u] : 0u;
         b2 += u < wave ? sm.wlen[u] : 0u;
     }
-    const uint32_t ex = b1 + i1 - tot;
+    uint32_t ex = b1 + i1 - tot;
     nex = b2 + i2 - lens;
+    // materialise both prefixes here: left to the compiler, nex was summed
+    // from the eight loaded wave totals at its use in st_issue_lists, which
+    // kept 16 VGPRs live across the sort
+    asm volatile("" : "+v"(ex), "+v"(nex));
     const uint32_t fl = sm.flag[wsb];
     wsb ^= 1;
     ST_SUB(1);
