@@ -182,6 +182,9 @@ def main():
                 gbs = fetched / (d["ms"] / d["launches"] * 1e-3) / 1e9
                 sort_passes[name] = {"fetched_bytes_per_launch": round(fetched), "fetch_GBps": round(gbs, 1),
                                      "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        # each pass writes what it reads and HBM's data bus carries both
+        # directions: a pass can fetch at most half the peak
+        sort_passes["read_ceiling_frac_of_peak"] = 0.5
     # whole-pipeline roofline: 48 B per input row + 24 B per joined row
     b_alg = 48.0 * rows_step + 24.0 * joined
     pipe_gbs = b_alg / (dt / a.steps) / 1e9
