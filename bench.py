@@ -46,6 +46,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# stdout carries exactly one JSON line: the process's fd 1 points at stderr
+# for the whole run (RCCL prints a version banner to stdout when its first
+# communicator comes up), and the result goes to a private copy of the real
+# stdout
+_RESULT_FD = None
+
+
+def _claim_stdout():
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(line):
+    sys.stdout.flush()
+    os.write(_RESULT_FD if _RESULT_FD is not None else 1, (json.dumps(line) + "\n").encode())
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -58,6 +77,9 @@ def parse():
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
     p.add_argument("--cpu-mt", type=int, default=1,
                    help="time the multi-core CPU port (oracle/cpu_mt.cpp) on the full workload (0 = skip)")
+    p.add_argument("--loopback", action="store_true",
+                   help="N = 1 through the distributed path (smj.dist, RCCL process group of one rank, "
+                        "own segments sent to itself): the multi-GPU pipeline's cost without cross-GPU traffic")
     p.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field")
     return p.parse_args()
@@ -73,6 +95,7 @@ def step_single(R, S, bufs):
 
 def main():
     a = parse()
+    _claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -80,8 +103,14 @@ def main():
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world > 1 or a.loopback:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    distributed = world > 1 or a.loopback
 
     n = a.rows
     if a.workload != "c3" and world > 1:
@@ -99,7 +128,7 @@ def main():
         R = ops.gen_uniform(n, row0=rank * n, seed=1, key_range=key_range, device=dev)
         S = ops.gen_uniform(n, row0=rank * n, seed=2, key_range=key_range, device=dev)
     bufs = None
-    if world == 1:
+    if not distributed:
         bufs = {"R": torch.empty_like(R), "S": torch.empty_like(S),
                 "J": torch.empty((min(nr, ns), 3), dtype=torch.int64, device=dev)}
     torch.cuda.synchronize()
@@ -107,9 +136,9 @@ def main():
     lb = {}
 
     def step():
-        if world == 1:
+        if not distributed:
             return step_single(R, S, bufs)
-        return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS, stats=lb)
+        return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS, stats=lb, loopback=a.loopback)
 
     for _ in range(a.warmup):
         step()
@@ -136,7 +165,7 @@ def main():
         log(f"msd stats (single-key groups, LSD-fallback groups, mR, mS): {ops.msd_stats()}; "
             f"(groups, radix-tier, wide-tier, in-LDS LSD): {ops.msd_groups()}")
 
-    joined = int(res) if world == 1 else int(res.shape[0])
+    joined = int(res) if not distributed else int(res.shape[0])
     t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=dev)
     if world > 1:
         tt = t.clone()
@@ -231,7 +260,7 @@ def main():
                                     "c5": "C5's tables (|R|=1e8, |S|=1e9, Zipf 0.9 over 1e8 keys) on ONE GPU "
                                           "(partitioned mode), WHERE col0 > 5000"}[a.workload],
                        "rows_per_table_per_gpu": n if a.workload != "c5" else [nr, ns], "rows_per_table_total": total, "key_range": key_range,
-                       "joined_rows": joined, "parallelism": f"range-partition x{world}",
+                       "joined_rows": joined, "parallelism": f"range-partition x{world}" + (" (RCCL loopback)" if a.loopback else ""),
                        "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
                        "exchange_stages": lb.get("stages", 0)},
             "roofline": roof,
@@ -244,7 +273,7 @@ def main():
             "cpu_baseline_mt": cpu_mt,
             "sort_passes": sort_passes,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.destroy_process_group()
 

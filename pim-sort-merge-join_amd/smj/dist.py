@@ -49,6 +49,11 @@ INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
 MAX_BOUNDS = 63  # smj_dev_partition*: <= 64 buckets
 DEFAULT_STAGES = int(os.environ.get("SMJ_DIST_STAGES", "2"))
+# loopback: a rank's own segment also travels through the point-to-point
+# transport (send / receive to itself; RCCL only: gloo keeps the device copy)
+# instead of a device copy, and one rank runs the whole distributed path: the
+# RCCL exchange on a one-GPU box
+LOOPBACK = os.environ.get("SMJ_DIST_LOOPBACK", "0") == "1"
 
 
 class HipOps:
@@ -219,7 +224,7 @@ def _wait_all(pending):
     return out
 
 
-def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
+def post_stage(k, K, sends, offs, seg, rank, world, home, group=None, loopback=False):
     """Post stage k's exchange: segment d*K + k of every table goes to rank d.
     seg[t][r][j] = rows of src rank r's table-t buffer in segment j (known on
     every rank from the gathered counts, so no count exchange is needed);
@@ -227,6 +232,7 @@ def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
     wire device (_wire_device), None for a table not posted in this call;
     received rows are returned on `home`."""
     p2p, recvs = [], []
+    loopback = loopback and dist.get_backend(group) != "gloo"  # gloo pairs never connect a rank to itself
     for t, wire in enumerate(sends):
         if wire is None:
             recvs.append(None)
@@ -236,7 +242,7 @@ def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
         recv = torch.empty((sum(rc), wire.shape[1]), dtype=wire.dtype, device=wire.device)
         at = 0
         for r in range(world):
-            if rc[r] and r == rank:
+            if rc[r] and r == rank and not loopback:
                 recv[at: at + rc[r]].copy_(wire[offs[t][me]: offs[t][me] + rc[r]])
             elif rc[r]:
                 p2p.append(dist.P2POp(dist.irecv, recv[at: at + rc[r]], r, group, tag=t * 4096 + k))
@@ -244,7 +250,7 @@ def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
         for d in range(world):
             j = d * K + k
             c = seg[t][rank][j]
-            if c and d != rank:
+            if c and (d != rank or loopback):
                 p2p.append(dist.P2POp(dist.isend, wire[offs[t][j]: offs[t][j] + c], d, group, tag=t * 4096 + k))
         recvs.append(recv)
     works = dist.batch_isend_irecv(p2p) if p2p else []
@@ -252,13 +258,16 @@ def post_stage(k, K, sends, offs, seg, rank, world, home, group=None):
 
 
 def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, ops=None, samples=4096,
-                    stats=None, stages=None):
+                    stats=None, stages=None, loopback=None):
     """The distributed pipeline; returns this rank's slice of the result (the
     global result is the concatenation over ranks in rank order).  stats
     (optional dict) gets the rows this rank received per table and the
     max / mean load over ranks (load-balance report).  stages: key sub-ranges
     per rank whose exchange overlaps the previous one's sort + join
     (default SMJ_DIST_STAGES or 2; 1 = exchange everything, then compute).
+    loopback (default SMJ_DIST_LOOPBACK=1): the rank's own segments also go
+    through send / receive to itself, and a single rank takes the whole
+    distributed path (exercises the RCCL transport on one GPU).
     The local pipeline has a fixed cost per call: 1e8 rows per table take
     6.03 ms in one call, 6.37 ms in 2 and 8.53 ms in 4 (tools/part_probe.py)."""
     ops = ops or HipOps
@@ -266,7 +275,8 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     k1, k2 = keys
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if world == 1:
+    loopback = LOOPBACK if loopback is None else loopback
+    if world == 1 and not loopback:
         return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
     nseg = world * K
@@ -303,17 +313,17 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     ncols = R.shape[1] + S.shape[1] - 1
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
-    pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group)]  # R's stage 0
+    pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group, loopback)]  # R's stage 0
     cS2, rowsS = ops.partition(S, bt, k2, sc2, sv2)  # overlaps R's stage-0 exchange
     if list(cS2) != list(cS):
         raise RuntimeError("smj.dist: partition counts disagree with the counting pass")
     sends[1] = rowsS.to(wire)
     del rowsS
-    pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group))
+    pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group, loopback))
     for k in range(K):
         Rk, Sk = _wait_all(pending)
         if k + 1 < K:
-            pending = [post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group)]
+            pending = [post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group, loopback)]
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
             continue
         if into:

@@ -78,7 +78,10 @@ def _worker(rank, world, port, R, S, cfg, outdir):
     for p in (os.path.join(repo, "pim-sort-merge-join_amd"), os.path.join(repo, "oracle"), here):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    backend = cfg.get("backend", "gloo")
+    if backend == "nccl":  # RCCL: one rank per GPU, the only one here is cuda:0
+        torch.cuda.set_device(rank)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from smj import dist as sdist
     from test_dist_gloo import OracleOps as Ops
     # contiguous, uneven slices in input order
@@ -93,7 +96,7 @@ def _worker(rank, world, port, R, S, cfg, outdir):
         r, s, ops = r.cuda(), s.cuda(), None
     stats = {}
     out = sdist.sort_merge_join(r, s, select=cfg["select"], keys=cfg["keys"], ops=ops, samples=cfg["samples"],
-                                stats=stats, stages=cfg.get("stages"))
+                                stats=stats, stages=cfg.get("stages"), loopback=cfg.get("loopback"))
     np.save(os.path.join(outdir, f"rank{rank}.npy"), out.cpu().numpy())
     if rank == 0:
         np.save(os.path.join(outdir, "load.npy"), np.array([stats["load_max_over_mean"]]))
@@ -158,6 +161,28 @@ def test_distributed_hip_eight_ranks_one_gpu(tmp_path, oracle_built, pkg_built, 
     W K - 1 = 15 splitters, 2 stages per rank) on the product operators, the
     8 ranks sharing cuda:0 and the exchange staged through gloo."""
     _run_and_check(tmp_path, 8, kind, cfg, 800_000)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
+    """Loopback mode (each rank's own segments through send / receive to
+    itself; one rank takes the whole distributed path) gives the same result."""
+    _run_and_check(tmp_path, world, "uniform",
+                   {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 64, "loopback": True}, 30_000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,cfg", [
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
+    ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True, "stages": 4}),
+])
+def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
+    """The RCCL transport of smj/dist.py on the one GPU a test box has: one
+    rank under the nccl backend (RCCL) in loopback mode, so the partition,
+    the device-resident send buffers, the staged batch_isend_irecv over the
+    RCCL communicator (to itself) and the stage-overlapped local pipeline
+    all run as on the 8-GPU node, bit-exact against the oracle."""
+    _run_and_check(tmp_path, 1, kind, dict(cfg, backend="nccl", loopback=True), 1_000_000)
 
 
 def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):
