@@ -911,6 +911,265 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
     }
 }
 
+// ---- part_b, pipelined (2-column tables) ------------------------------------
+// The same tile work as msd_part_b_kernel, reordered so that the NEXT tile's
+// rows are gathered before THIS tile's rows are stored: its run list goes to
+// a region of its own (s_nl, up to one entry per thread), built while this
+// tile is ranked, and its gathers are issued between this tile's staging and
+// its stores.  A vector-memory wait on gfx950 retires every older load AND
+// store, so in the plain kernel the rank phase of tile k + 1 waited behind
+// tile k's 64 KiB of stores; here the stores are younger than the gathers
+// they used to hold up.  A next tile with more runs than threads is
+// gathered after the stores, through the main region (the plain order).
+#ifndef SMJ_PB_PIPE
+#define SMJ_PB_PIPE 1
+#endif
+
+// row -> run lookups of a tile (run list lst, start bitmap bm, 64-row block
+// table bt) and the row gathers into registers
+template <int COLS, int ITEMS>
+__device__ __forceinline__ void pb_gather(const MsdPartBParams &p, const uint2 *lst, const uint32_t *bm,
+                                          const uint16_t *bt, uint32_t v0, int nrows, int lrow0,
+                                          int64_t (&rows)[ITEMS][COLS]) {
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t r = (uint32_t)min(lrow0 + it * 64, nrows - 1), bb = r >> 6;
+        const uint64_t m = ((uint64_t)bm[2 * bb + 1] << 32 | bm[2 * bb]) & ((2ull << (r & 63)) - 1ull) & ~1ull;
+        const uint32_t j = bt[bb] + (uint32_t)__popcll(m);  // run starts in (64 bb, r]
+        const uint2 e = lst[j];
+        if (p.dbg & 4) {
+#pragma unroll
+            for (int c = 0; c < COLS; c++) rows[it][c] = (int64_t)((v0 + r) * 7u);
+        } else {
+            load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
+        }
+    }
+}
+
+// the start bitmap (zeroed) and block table of a run list of J entries
+template <int NT>
+__device__ __forceinline__ void pb_marks(const uint2 *lst, uint32_t *bm, uint16_t *bt, int J, uint32_t v0,
+                                         int nrows) {
+    for (int j = opaque_tid(); j < J; j += NT) {  // runs are non-empty: starts strictly increase
+        const uint32_t y = lst[j].y;
+        const uint32_t s0 = y > v0 ? y - v0 : 0u;
+        const uint32_t e = j + 1 < J ? lst[j + 1].y - v0 : (uint32_t)nrows;
+        if (s0 < (uint32_t)nrows) {
+            atomicOr(&bm[s0 >> 5], 1u << (s0 & 31));
+            for (uint32_t bb = (s0 + 63) >> 6; (bb << 6) < e && (bb << 6) < (uint32_t)nrows; bb++) bt[bb] = (uint16_t)j;
+        }
+    }
+}
+
+template <int COLS>
+__global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(const MsdPartBParams p) {
+    constexpr int NT = pb_threads(COLS), NW = NT / 64, T = msd_tile_b(COLS), ITEMS = T / NT, RADIX = kRadB;
+    constexpr int DPT = RADIX / NT;
+    static_assert(T % NT == 0 && RADIX % (2 * NT) == 0, "tile / histogram split");
+    constexpr int LISTB = (T + 1) * 8, BMB = T / 8, BTB = T / 64 * 2;
+    constexpr int ROWB = T * COLS * 8, PERMB = T * 2, CNTB = RADIX * 4, LKB = LISTB + BMB + BTB;
+    static_assert(NW % 4 == 0, "quads of waves");
+    constexpr int QN = NW / 4, QW = (QN + 1) / 2, QB = QW * RADIX * 4;
+    constexpr int QOFF0 = LKB > PERMB + CNTB ? LKB : PERMB + CNTB, QOFF = (QOFF0 + 15) / 16 * 16;
+    constexpr int UB = ROWB > QOFF + QB ? ROWB : QOFF + QB;
+    __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
+    __shared__ uint2 s_nl[NT];          // the next tile's run list (<= NT entries)
+    __shared__ uint32_t s_nbm[T / 32];  // its start bitmap
+    __shared__ uint16_t s_nbt[T / 64];  // its 64-row block table
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint32_t s_slow;
+    uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_u);
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_u + PERMB);
+    int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
+    uint2 *s_list = reinterpret_cast<uint2 *>(s_u);
+    uint32_t *s_bm = reinterpret_cast<uint32_t *>(s_u + LISTB);
+    uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + BMB);
+    uint32_t *s_q = reinterpret_cast<uint32_t *>(s_u + QOFF);
+
+    const int64_t ntl = (int64_t)p.plan->ntilesB[p.x];
+    int64_t g = blockIdx.x;
+    if (g >= ntl) return;
+    const uint64_t *list64 = reinterpret_cast<const uint64_t *>(p.list);
+    auto runs_of = [&](const uint2 &t, const MsdBucket &bb, int64_t gg) {  // run-list entries of tile gg
+        const uint32_t vv = (uint32_t)(gg - bb.tile_base) * (uint32_t)T;
+        const uint32_t nr = min((uint32_t)T, bb.L - vv);
+        return min(bb.list_base + bb.nruns - t.y, nr + 1u);
+    };
+    auto tile_v0 = [&](const MsdBucket &bb, int64_t gg) { return (uint32_t)(gg - bb.tile_base) * (uint32_t)T; };
+    auto tile_rows = [&](const MsdBucket &bb, int64_t gg) { return (int)min((uint32_t)T, bb.L - tile_v0(bb, gg)); };
+    auto quad_of = [&]() { return (uint32_t)opaque_tid() >> 8; };
+    // the plain order's list build in the main region (entries past the
+    // first NT come straight from global memory); ends with a barrier
+    auto build_main = [&](const uint2 &t, const MsdBucket &bb, int64_t gg, uint64_t le) {
+        const int tid = opaque_tid();
+        const int J = (int)runs_of(t, bb, gg);
+        if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
+        for (int j = tid + NT; j < J; j += NT) reinterpret_cast<uint64_t *>(s_list)[j] = list64[t.y + j];
+        for (int i = tid; i < T / 32; i += NT) s_bm[i] = 0;
+        __syncthreads();
+        pb_marks<NT>(s_list, s_bm, s_bt, J, tile_v0(bb, gg), tile_rows(bb, gg));
+        __syncthreads();
+    };
+
+    uint2 ti = uni_tinfo(p.tinfo, g);
+    MsdBucket b = uni_bucket(p.bk, ti.x);
+    int64_t rows[ITEMS][COLS];
+    {  // prologue: tile g's run list and gathers
+        const int tid = opaque_tid(), lrow0 = (tid >> 6) * ITEMS * 64 + (tid & 63);
+        uint64_t le = 0;
+        if ((uint32_t)tid < runs_of(ti, b, g)) le = list64[ti.y + tid];
+        build_main(ti, b, g, le);
+        pb_gather<COLS, ITEMS>(p, s_list, s_bm, s_bt, tile_v0(b, g), tile_rows(b, g), lrow0, rows);
+    }
+    uint2 tn = uni_tinfo(p.tinfo, min(g + (int64_t)gridDim.x, ntl - 1));  // the next tile's info
+    if (opaque_tid() == 0) s_slow = 0;
+    __syncthreads();  // the main list region is dead
+    for (; g < ntl; g += gridDim.x) {
+        const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+        const int64_t gn = g + gridDim.x;
+        const uint32_t v0 = tile_v0(b, g);
+        const int nrows = tile_rows(b, g);
+        const int lrow0 = wave * ITEMS * 64 + lane;
+        for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
+        for (int i = tid; i < T / 32; i += NT) s_nbm[i] = 0;
+        const MsdBucket bn = uni_bucket(p.bk, tn.x);  // the next tile's bucket
+        __syncthreads();
+
+        uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
+        uint32_t vmask = 0;
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const bool v = lrow0 + it * 64 < nrows;
+            const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
+            const uint32_t d = b.s32     ? __umulhi((uint32_t)r, b.s32)
+                               : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1))
+                                         : (uint32_t)r;
+            dig[it] = v ? d & (RADIX - 1) : 0u;
+            vmask |= v ? (1u << it) : 0u;
+        }
+        {
+            const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it];
+                    dig[it] = d | (((atomicAdd(&s_q[qrow + d], 1u << qsh) >> qsh) & 0xffffu) << 16);
+                }
+        }
+        const bool more = gn < ntl;
+        const int Jn = more ? (int)runs_of(tn, bn, gn) : 0;
+        uint64_t le = 0;  // the next tile's run-list entries
+        if (tid < Jn) le = list64[tn.y + tid];
+        __syncthreads();
+        {  // counts -> per-quad first rows, in place; the tile's sub-bucket starts -> offsB
+            uint32_t sum = 0, cmax = 0;
+#pragma unroll
+            for (int k = 0; k < DPT; k++)
+#pragma unroll
+                for (int q2 = 0; q2 < QW; q2++) {
+                    const uint32_t w = s_q[q2 * RADIX + DPT * tid + k];
+                    sum += (w & 0xffffu) + (w >> 16);
+                    cmax = max(cmax, max(w & 0xffffu, w >> 16));
+                }
+            if (cmax > (uint32_t)kPbFastMax || (p.dbg & 16)) s_slow = 1;
+            uint32_t tot;
+            uint32_t st = block_excl_scan_nb<NW>(sum, s_wsum, &tot);  // + barrier
+            uint32_t sw = 0;
+#pragma unroll
+            for (int k = 0; k < DPT; k++) {
+                sw = (k & 1) ? sw | (st << 16) : st;
+                if ((k & 1) && !(p.dbg & 8)) reinterpret_cast<uint32_t *>(p.offs + g * kOffsB)[DPT / 2 * tid + k / 2] = sw;
+#pragma unroll
+                for (int q2 = 0; q2 < QW; q2++) {
+                    const uint32_t w = s_q[q2 * RADIX + DPT * tid + k];
+                    const uint32_t b1 = st + (w & 0xffffu);
+                    s_q[q2 * RADIX + DPT * tid + k] = st | (b1 << 16);
+                    st = b1 + (w >> 16);
+                }
+            }
+            if (tid == 0 && !(p.dbg & 8)) p.offs[g * kOffsB + RADIX] = (uint16_t)nrows;
+        }
+        __syncthreads();
+        const bool slow = s_slow != 0;
+        if (!slow) {
+            const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu;
+                    s_perm[((s_q[qrow + d] >> qsh) & 0xffffu) + (dig[it] >> 16)] = (uint16_t)(lrow0 + it * 64);
+                }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu, w = s_q[qrow + d];
+                    const uint32_t st = (w >> qsh) & 0xffffu;
+                    uint32_t en;
+                    if (!(quad & 1)) en = w >> 16;
+                    else if (quad + 1 < QN) en = s_q[qrow + RADIX + d] & 0xffffu;
+                    else en = d + 1u < (uint32_t)RADIX ? (s_q[d + 1] & 0xffffu) : (uint32_t)nrows;
+                    const uint32_t r = (uint32_t)(lrow0 + it * 64);
+                    uint32_t rank = 0;
+                    if (en - st > 1u)
+                        for (uint32_t j = st; j < en; j++) rank += (uint32_t)s_perm[j] < r;
+                    dig[it] = st + rank;
+                }
+        } else {
+#pragma unroll
+            for (int k = 0; k < RADIX / NT; k++) s_cnt[tid + k * NT] = 0;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) dig[it] &= 0xffffu;
+            __syncthreads();
+            for (int w = 0; w < NW; w++) {
+                if (wave == w) wave_rank<ITEMS, kBitsB>(dig, vmask, s_cnt, lane);
+                __syncthreads();
+            }
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu;
+                    dig[it] = (s_q[d] & 0xffffu) + (dig[it] >> 16);
+                }
+        }
+        __syncthreads();  // permutation / counters dead: the region becomes the staging tile
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+        const bool early = more && Jn <= NT;  // block-uniform
+        if (early && tid < Jn) reinterpret_cast<uint64_t *>(s_nl)[tid] = le;
+        __syncthreads();  // staging tile and the next run list written
+        if (tid == 0) s_slow = 0;
+        uint2 tn2 = tn;
+        if (early) {  // the next tile's gathers, ahead of this tile's stores
+            pb_marks<NT>(s_nl, s_nbm, s_nbt, Jn, tile_v0(bn, gn), tile_rows(bn, gn));
+            __syncthreads();
+            pb_gather<COLS, ITEMS>(p, s_nl, s_nbm, s_nbt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
+            tn2 = uni_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
+        }
+        int64_t *dst = p.out + g * T * COLS;
+        if (!(p.dbg & 2)) {
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const int s = min(tid + it * NT, nrows - 1);
+                int64_t r[COLS];
+                load_row<COLS>(s_rows + (size_t)s * COLS, r);
+                store_row_nt<COLS>(dst + (size_t)s * COLS, r);
+            }
+        }
+        __syncthreads();  // staging region read out
+        if (more && !early) {  // over NT runs: the plain order, through the main region
+            build_main(tn, bn, gn, le);
+            pb_gather<COLS, ITEMS>(p, s_list, s_bm, s_bt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
+            tn2 = uni_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
+            __syncthreads();  // the main list region is dead
+        }
+        ti = tn;
+        tn = tn2;
+        b = bn;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // group: pack the sub-buckets of every bucket into final groups
 // ---------------------------------------------------------------------------
@@ -2869,7 +3128,13 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
     SMJ_COLS_SWITCH(cols, {
         const unsigned grid =
             (unsigned)std::min<int64_t>(max_tiles, resident_blocks(msd_part_b_kernel<C>, pb_threads(C), pad));
-        hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(pb_threads(C)), pad, s, p);
+        if (C == 2 && SMJ_PB_PIPE) {
+            const unsigned gp = (unsigned)std::min<int64_t>(
+                max_tiles, resident_blocks(msd_part_b_pipe_kernel<2>, pb_threads(2), pad));
+            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
+        } else {
+            hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(pb_threads(C)), pad, s, p);
+        }
     });
     return hipGetLastError();
 }
