@@ -630,6 +630,30 @@ __device__ __forceinline__ uint2 uni_tinfo(const uint2 *t, int64_t g) {
     const uint2 v = t[g];
     return make_uint2(uni32(v.x), uni32(v.y));
 }
+// The same through scalar (SMEM) loads, for addresses that are wave-uniform
+// (the data was written by an earlier launch: the scalar cache starts each
+// launch invalidated).  SMEM loads count on lgkmcnt, so waiting for one does
+// not retire the vector loads and stores in flight, as a vector load's
+// vmcnt(0) did in part_b's tile loop.
+#define SMJ_CONST(T) const __attribute__((address_space(4))) T
+__device__ __forceinline__ uint2 sc_tinfo(const uint2 *t, int64_t g) {
+    const uint64_t w = *(SMJ_CONST(uint64_t) *)uni64((uint64_t)(t + g));
+    return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+}
+static_assert(sizeof(MsdBucket) == 48 && offsetof(MsdBucket, maxspan) == 16 && offsetof(MsdBucket, s32) == 44,
+              "sc_bucket reads MsdBucket as six words");
+__device__ __forceinline__ MsdBucket sc_bucket(const MsdBucket *bk, uint32_t a) {
+    SMJ_CONST(uint64_t) *q = (SMJ_CONST(uint64_t) *)uni64((uint64_t)(bk + a));
+    const uint64_t w2 = q[2], w3 = q[3], w4 = q[4], w5 = q[5];
+    MsdBucket r;
+    r.lo = (int64_t)q[0];
+    r.scale = q[1];
+    r.maxspan = (uint32_t)w2, r.L = (uint32_t)(w2 >> 32);
+    r.row_start = (uint32_t)w3, r.list_base = (uint32_t)(w3 >> 32);
+    r.nruns = (uint32_t)w4, r.tile_base = (uint32_t)(w4 >> 32);
+    r.one_key = (uint32_t)w5, r.s32 = (uint32_t)(w5 >> 32);
+    return r;
+}
 __device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a) {
     const MsdBucket v = bk[a];
     MsdBucket r;
@@ -924,12 +948,15 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 #ifndef SMJ_PB_PIPE
 #define SMJ_PB_PIPE 1
 #endif
+#ifndef SMJ_PB_NOSTORE
+#define SMJ_PB_NOSTORE 0
+#endif
 
 // row -> run lookups of a tile (run list lst, start bitmap bm, 64-row block
 // table bt) and the row gathers into registers
 template <int COLS, int ITEMS>
-__device__ __forceinline__ void pb_gather(const MsdPartBParams &p, const uint2 *lst, const uint32_t *bm,
-                                          const uint16_t *bt, uint32_t v0, int nrows, int lrow0,
+__device__ __forceinline__ void pb_gather(const MsdPartBParams &p, const MsdBucket &bk, const uint2 *lst,
+                                          const uint32_t *bm, const uint16_t *bt, uint32_t v0, int nrows, int lrow0,
                                           int64_t (&rows)[ITEMS][COLS]) {
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
@@ -939,7 +966,7 @@ __device__ __forceinline__ void pb_gather(const MsdPartBParams &p, const uint2 *
         const uint2 e = lst[j];
         if (p.dbg & 4) {
 #pragma unroll
-            for (int c = 0; c < COLS; c++) rows[it][c] = (int64_t)((v0 + r) * 7u);
+            for (int c = 0; c < COLS; c++) rows[it][c] = bk.lo + (int64_t)((v0 + r) * 7u % (bk.L + 1u));
         } else {
             load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
         }
@@ -1011,17 +1038,23 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         __syncthreads();
     };
 
-    uint2 ti = uni_tinfo(p.tinfo, g);
-    MsdBucket b = uni_bucket(p.bk, ti.x);
+    uint2 ti = sc_tinfo(p.tinfo, g);
+    MsdBucket b = sc_bucket(p.bk, ti.x);
     int64_t rows[ITEMS][COLS];
     {  // prologue: tile g's run list and gathers
         const int tid = opaque_tid(), lrow0 = (tid >> 6) * ITEMS * 64 + (tid & 63);
         uint64_t le = 0;
         if ((uint32_t)tid < runs_of(ti, b, g)) le = list64[ti.y + tid];
         build_main(ti, b, g, le);
-        pb_gather<COLS, ITEMS>(p, s_list, s_bm, s_bt, tile_v0(b, g), tile_rows(b, g), lrow0, rows);
+        pb_gather<COLS, ITEMS>(p, b, s_list, s_bm, s_bt, tile_v0(b, g), tile_rows(b, g), lrow0, rows);
+        // consumed here, so the loop top's wait counts only the back edge's
+        // stores (vmcnt(stores)) instead of merging this path's vmcnt(0)
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+#pragma unroll
+            for (int c = 0; c < COLS; c++) asm volatile("" ::"v"(rows[it][c]));
     }
-    uint2 tn = uni_tinfo(p.tinfo, min(g + (int64_t)gridDim.x, ntl - 1));  // the next tile's info
+    uint2 tn = sc_tinfo(p.tinfo, min(g + (int64_t)gridDim.x, ntl - 1));  // the next tile's info
     if (opaque_tid() == 0) s_slow = 0;
     __syncthreads();  // the main list region is dead
     for (; g < ntl; g += gridDim.x) {
@@ -1032,7 +1065,11 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         const int lrow0 = wave * ITEMS * 64 + lane;
         for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
         for (int i = tid; i < T / 32; i += NT) s_nbm[i] = 0;
-        const MsdBucket bn = uni_bucket(p.bk, tn.x);  // the next tile's bucket
+        const MsdBucket bn = sc_bucket(p.bk, tn.x);  // the next tile's bucket
+        // and the info of the tile after it (scalar loads: a vector load here,
+        // or after the next tile's gathers as before, is waited with vmcnt(0),
+        // which also retires the gathers and the previous tile's stores)
+        const uint2 tn2 = sc_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
         __syncthreads();
 
         uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
@@ -1078,7 +1115,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
 #pragma unroll
             for (int k = 0; k < DPT; k++) {
                 sw = (k & 1) ? sw | (st << 16) : st;
-                if ((k & 1) && !(p.dbg & 8)) reinterpret_cast<uint32_t *>(p.offs + g * kOffsB)[DPT / 2 * tid + k / 2] = sw;
+                if (k & 1) reinterpret_cast<uint32_t *>(p.offs + g * kOffsB)[DPT / 2 * tid + k / 2] = sw;
 #pragma unroll
                 for (int q2 = 0; q2 < QW; q2++) {
                     const uint32_t w = s_q[q2 * RADIX + DPT * tid + k];
@@ -1087,7 +1124,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                     st = b1 + (w >> 16);
                 }
             }
-            if (tid == 0 && !(p.dbg & 8)) p.offs[g * kOffsB + RADIX] = (uint16_t)nrows;
+            if (tid == 0) p.offs[g * kOffsB + RADIX] = (uint16_t)nrows;
         }
         __syncthreads();
         const bool slow = s_slow != 0;
@@ -1140,15 +1177,16 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         if (early && tid < Jn) reinterpret_cast<uint64_t *>(s_nl)[tid] = le;
         __syncthreads();  // staging tile and the next run list written
         if (tid == 0) s_slow = 0;
-        uint2 tn2 = tn;
         if (early) {  // the next tile's gathers, ahead of this tile's stores
             pb_marks<NT>(s_nl, s_nbm, s_nbt, Jn, tile_v0(bn, gn), tile_rows(bn, gn));
             __syncthreads();
-            pb_gather<COLS, ITEMS>(p, s_nl, s_nbm, s_nbt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
-            tn2 = uni_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
+            pb_gather<COLS, ITEMS>(p, bn, s_nl, s_nbm, s_nbt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
         }
+        // the stores are unconditional (a run-time ablation bit around them
+        // made hipcc's wait for the next tile's rows a vmcnt(0) that also
+        // retired these stores); SMJ_PB_NOSTORE=1 builds the no-store ablation
         int64_t *dst = p.out + g * T * COLS;
-        if (!(p.dbg & 2)) {
+        if (!SMJ_PB_NOSTORE) {
 #pragma unroll
             for (int it = 0; it < ITEMS; it++) {
                 const int s = min(tid + it * NT, nrows - 1);
@@ -1160,8 +1198,13 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         __syncthreads();  // staging region read out
         if (more && !early) {  // over NT runs: the plain order, through the main region
             build_main(tn, bn, gn, le);
-            pb_gather<COLS, ITEMS>(p, s_list, s_bm, s_bt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
-            tn2 = uni_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
+            pb_gather<COLS, ITEMS>(p, bn, s_list, s_bm, s_bt, tile_v0(bn, gn), tile_rows(bn, gn), lrow0, rows);
+            // consumed on this path (rows younger than the stores): the loop
+            // top then waits only for the early path's gathers, vmcnt(stores)
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+#pragma unroll
+                for (int c = 0; c < COLS; c++) asm volatile("" ::"v"(rows[it][c]));
             __syncthreads();  // the main list region is dead
         }
         ti = tn;
