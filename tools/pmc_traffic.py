@@ -29,7 +29,7 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_final_kernel<", "msd_final", False),
     (r"msd_final_wide_kernel", "msd_final", False),
     (r"msd_part_a_kernel", "msd_part_a", True),
-    (r"msd_part_b_kernel", "msd_part_b", True),
+    (r"msd_part_b(_pipe)?_kernel", "msd_part_b", True),
     (r"msd_bases_kernel", "msd_runs", True),
     (r"msd_runs_seg_kernel", "msd_runs", False),
     (r"msd_runs_apply_kernel", "msd_runs", False),
