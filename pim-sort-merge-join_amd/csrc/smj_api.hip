@@ -481,6 +481,7 @@ struct MsdScratch {
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
 int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
+int64_t g_msd_bigdev = 0;                // last pipeline: oversized multi-key groups sorted on the device
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -588,15 +589,41 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
         HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
     }
-    if (pl.nbig) {
-        // all oversized multi-key groups at once: gather (in key order) ->
-        // one stable sort per table -> copy back to each group's output rows;
-        // with join, one zip join of the two sorted buffers split per group
+    // oversized multi-key groups of a small key span were sorted (and joined)
+    // on the device by msd_big_stage_kernel (2-column tables); the rest here
+    const bool two = in[0].cols == 2 && (ntab == 1 || in[1].cols == 2);
+    std::vector<uint32_t> host_bigs;
+    for (uint32_t slot : bigs) {
+        const MsdGroup &g = groups[slot];
+        if (!(two && msd_big_on_device(g.span, g.nR, ntab > 1 ? g.nS : 0u) && g.kt[0] <= (uint32_t)kGroupCap &&
+              g.kt[1] <= (uint32_t)kGroupCap))
+            host_bigs.push_back(slot);
+    }
+    if (getenv("SMJ_DEBUG_BIG")) {  // size distribution of the oversized multi-key groups (rows, log2 bins)
+        int64_t hist[2][33] = {}, rows[2][33] = {};
+        for (uint32_t slot : bigs) {
+            const MsdGroup &g = groups[slot];
+            const uint32_t m = std::max(g.nR, g.nS);
+            const int b = 31 - __builtin_clz(std::max(m, 1u)), d = g.span <= (uint32_t)kStageRange ? 0 : 1;
+            hist[d][b]++;
+            rows[d][b] += (int64_t)g.nR + g.nS;
+        }
+        for (int d = 0; d < 2; d++)
+            for (int b = 0; b < 33; b++)
+                if (hist[d][b])
+                    fprintf(stderr, "smj big groups span%s4096 rows 2^%d: %lld groups, %lld rows\n", d ? ">" : "<=", b,
+                            (long long)hist[d][b], (long long)rows[d][b]);
+    }
+    if (!host_bigs.empty()) {
+        // all remaining oversized multi-key groups at once: gather (in key
+        // order) -> one stable sort per table -> copy back to each group's
+        // output rows; with join, one zip join of the two sorted buffers split
+        // per group
         constexpr uint32_t kSeg = 4096;  // rows per copy-back work item
-        std::sort(bigs.begin(), bigs.end());  // dense group index = key order (the list is filled by atomics)
+        std::sort(host_bigs.begin(), host_bigs.end());  // dense group index = key order (the list is filled by atomics)
         std::vector<uint4> gw[2], cw[2], bw;
         int64_t tot[2] = {0, 0};
-        for (uint32_t slot : bigs) {
+        for (uint32_t slot : host_bigs) {
             const MsdGroup &g = groups[slot];
             const uint32_t nx[2] = {g.nR, ntab > 1 ? g.nS : 0u};
             const uint32_t ox[2] = {g.outR, g.outS};
@@ -913,6 +940,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         g_msd_groups[0] = ms->h_plan->ngroups;
         g_msd_groups[1] = ms->h_plan->nradix;
         g_msd_groups[2] = ms->h_plan->nwide;
+        g_msd_bigdev = ms->h_plan->nbigdev;
         g_msd_groups[3] = ms->h_plan->nlsd;
     }
     bool redo = false;
@@ -1235,6 +1263,10 @@ extern "C" void smj_debug_msd_groups(int64_t *out3) {
 extern "C" void smj_debug_msd_tiers(int64_t *out4) {
     for (int i = 0; i < 4; i++) out4[i] = g_msd_groups[i];
 }
+
+// Diagnostic only (not part of smj.h): oversized multi-key groups of the last
+// pipeline call that msd_big_stage_kernel sorted (the rest: host fallback)
+extern "C" int64_t smj_debug_msd_bigdev(void) { return g_msd_bigdev; }
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {
     for (int i = 0; i < 4; i++) out4[i] = g_msd_stats[i];

@@ -179,6 +179,15 @@ constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
 constexpr int kOffsB = kRadB + 8;          // offsB row (u16): 2048 starts + the tile's row count, padded to 16 B
 constexpr int kGroupCap = 1024;            // rows per table in one final group (LDS)
 constexpr int kStageRange = 4096;          // key range of the staged final path's counting sort
+#ifndef SMJ_BG_MAX_ROWS
+#define SMJ_BG_MAX_ROWS 131072
+#endif
+constexpr uint32_t kBgMaxRows = SMJ_BG_MAX_ROWS;  // rows per table of an oversized group msd_big_stage_kernel takes
+// an oversized multi-key group sorted on the device (msd_big_stage_kernel);
+// the others take the host-driven fallback (smj_api.hip msd_fallback)
+__host__ __device__ inline bool msd_big_on_device(uint32_t span, uint32_t nR, uint32_t nS) {
+    return span <= (uint32_t)kStageRange && nR <= kBgMaxRows && nS <= kBgMaxRows;
+}
 constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
@@ -241,6 +250,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t nwide;      // groups for the 64-bit final path
     uint32_t nradix;     // groups for the radix-sort final path
     uint32_t nlsd;       // staged groups sorted by the in-LDS LSD (equal-key runs over kMaxDupRun)
+    uint32_t nbigdev;    // oversized multi-key groups sorted on the device (msd_big_stage_kernel)
+    uint32_t bgticket[2];// msd_big_stage_kernel's group tickets (large groups first, then the rest)
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)

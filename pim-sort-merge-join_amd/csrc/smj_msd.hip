@@ -2772,6 +2772,251 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const Ms
     }
 }
 
+// ---------------------------------------------------------------------------
+// oversized multi-key groups of a small key span (2-column tables)
+// ---------------------------------------------------------------------------
+// A sub-bucket over kGroupCap rows that holds more than one key value (a
+// Zipf-skewed table, BASELINE C5: a key with thousands of rows next to light
+// ones) used to leave the device pipeline for the host-driven fallback
+// (gather, 64-bit LSD sort, zip join of every such group).  When its keys
+// span at most kStRange values (and it has at most kBgMaxRows rows per
+// table) it is sorted here instead, one workgroup per group, by a two-pass
+// counting sort over the residual r = key - base: pass 1 counts every r of
+// both tables through LDS atomics; the counts become exclusive output starts
+// (and the zip join's per-r pair counts min(cR, cS) an exclusive prefix of
+// join rows); pass 2 streams the rows again in chunks of kGroupCap, and the
+// waves of the workgroup take turns in input order: a wave ranks its rows
+// among equal residuals with wave ballots (wave_rank) on top of the running
+// start of each r and advances it -- so equal keys keep their input order --
+// and every row is stored straight to its place.  The join rows are then
+// built from the two sorted output ranges (occurrence i of r in R with
+// occurrence i in S, cpu_app.c:204-266) into the group's slot range, and
+// counts[g] = their number, as the staged kernel does.
+constexpr int kBgIt = kGroupCap / kMsdThreads;  // chunk rows per thread
+#ifndef SMJ_BG_ABL
+#define SMJ_BG_ABL 0  // timing ablation (output invalid): 1 = no counting pass, 2 = no row pass, 4 = no join rows
+#endif
+constexpr uint32_t kBgLarge = 8 * kGroupCap;  // groups over this many rows (either table) are dealt first
+struct BgSmem {
+    uint32_t end[2][kStRange];   // per residual: row count, then the running start of its output rows
+    uint32_t jst[kStRange + 1];  // exclusive prefix over residuals of min(countR, countS) (join rows)
+    uint2 list[2][kGroupCap];    // per table: {tempB row, group row} of each pass-B tile's run
+    uint32_t nl[2];              // runs per table
+    uint32_t wsum[kMsdWaves];
+    uint32_t ticket;
+};
+
+__device__ __forceinline__ bool bg_ok(const MsdGroup &g) {
+    return g.flags == kGroupBig && msd_big_on_device(g.span, g.nR, g.nS) && g.kt[0] <= (uint32_t)kGroupCap &&
+           g.kt[1] <= (uint32_t)kGroupCap;
+}
+
+// wave_rank with 32-bit positions: pos[it] = wc[digit] + the row's rank among
+// the wave's earlier rows of its digit (items in order, lanes in order);
+// the wave's last row of each digit advances wc[digit]
+template <int ITEMS, int DBITS>
+__device__ __forceinline__ void bg_rank(const uint32_t (&dig)[ITEMS], uint32_t vmask, uint32_t *wc, int lane,
+                                        uint32_t (&pos)[ITEMS]) {
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const bool v = (vmask >> it) & 1u;
+        const uint64_t act = __ballot(v);
+        uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
+        const uint32_t dd = dig[it];
+#pragma unroll
+        for (int b = 0; b < DBITS; b++) {
+            const uint32_t sb = (uint32_t)((int32_t)(dd << (31 - b)) >> 31);  // ~0 iff bit b
+            const uint64_t bb = __ballot(sb != 0u);
+            plo = peer_fold(plo, (uint32_t)bb, sb);
+            phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
+        }
+        if (v) {
+            const uint32_t base = wc[dd];
+            pos[it] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, base));
+            const uint64_t peers = ((uint64_t)phi << 32) | plo;
+            if ((peers >> lane) == 1ull) wc[dd] = base + (uint32_t)__popcll(peers);
+        }
+    }
+}
+
+// row v of table x's group sequence: its tempB row (the last run starting at or before v)
+__device__ __forceinline__ uint32_t bg_src(const uint2 *lst, uint32_t nl, uint32_t v) {
+    uint32_t lo = 0, hi = nl - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (lst[mid].y <= v) lo = mid; else hi = mid - 1;
+    }
+    const uint2 e = lst[lo];
+    return e.x + (v - e.y);
+}
+
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const MsdFinalParams p) {
+    __shared__ BgSmem sm;
+    const uint32_t nbig = p.plan->nbig;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int RP = kStRange / kMsdThreads;  // residuals per thread in the scans
+    // dynamic tickets over the (unordered) list, twice: the groups over
+    // kBgLarge rows first, so that the longest ones do not start last
+    for (int round = 0; round < 2; round++)
+    for (;;) {
+        __syncthreads();  // LDS of the previous group / ticket read out
+        if (tid == 0) sm.ticket = atomicAdd(&p.plan->bgticket[round], 1u);
+        __syncthreads();
+        const uint32_t bi = sm.ticket;
+        if (bi >= nbig) break;
+        const uint32_t gi = p.big_list[bi];
+        const MsdGroup g = p.groups[gi];
+        if (!bg_ok(g)) continue;  // block-uniform: left to the host fallback
+        if ((max(g.nR, g.nS) > kBgLarge) != (round == 0)) continue;
+        const uint32_t nS = p.ntab > 1 ? g.nS : 0u;
+        for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
+        // the runs of the group in each table's pass-B tiles (one block scan per table)
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            if (x >= p.ntab) break;
+            const MsdTab &tb = p.tab[x];
+            uint32_t src[kBgIt], len[kBgIt], sum = 0;
+#pragma unroll
+            for (int i = 0; i < kBgIt; i++) {
+                const uint32_t j = (uint32_t)tid * kBgIt + i;
+                src[i] = len[i] = 0;
+                if (j < g.kt[x]) {
+                    const int64_t id = (int64_t)g.tb[x] + j;
+                    const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
+                    src[i] = (uint32_t)id * (uint32_t)tb.tile + lo;
+                    len[i] = hi - lo;
+                }
+                sum += len[i];
+            }
+            uint32_t total;
+            uint32_t ex = block_excl_scan<kMsdWaves>(sum, sm.wsum, &total);
+#pragma unroll
+            for (int i = 0; i < kBgIt; i++) {
+                const uint32_t j = (uint32_t)tid * kBgIt + i;
+                if (j < g.kt[x]) sm.list[x][j] = make_uint2(src[i], ex);
+                ex += len[i];
+            }
+            if (tid == 0) sm.nl[x] = g.kt[x];
+        }
+        __syncthreads();
+        // pass 1: residual counts of both tables
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            if (x >= p.ntab || (SMJ_BG_ABL & 1)) break;
+            const MsdTab &tb = p.tab[x];
+            const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
+            const uint32_t nx = x ? nS : g.nR;
+            for (uint32_t v0 = 0; v0 < nx; v0 += kGroupCap) {
+                int64_t k[kBgIt];
+#pragma unroll
+                for (int i = 0; i < kBgIt; i++) {
+                    const uint32_t v = v0 + tid + i * kMsdThreads;
+                    k[i] = 0;
+                    if (v < nx) {
+                        const i64x2 r = tB[bg_src(sm.list[x], sm.nl[x], v)];
+                        k[i] = tb.key ? r.y : r.x;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < kBgIt; i++)
+                    if (v0 + tid + i * kMsdThreads < nx) atomicAdd(&sm.end[x][(uint32_t)((uint64_t)k[i] - (uint64_t)g.base)], 1u);
+            }
+        }
+        __syncthreads();
+        // counts -> exclusive output starts per table; min(cR, cS) -> join-row starts
+        const bool join = p.join && p.ntab > 1;
+        {
+            uint32_t c[3][RP], sum[3] = {0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < RP; j++) {
+                const int r = tid * RP + j;
+                c[0][j] = sm.end[0][r];
+                c[1][j] = sm.end[1][r];
+                c[2][j] = join ? min(c[0][j], c[1][j]) : 0u;
+#pragma unroll
+                for (int q = 0; q < 3; q++) sum[q] += c[q][j];
+            }
+            uint32_t ex[3], tot[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) ex[q] = block_excl_scan<kMsdWaves>(sum[q], sm.wsum, &tot[q]);
+#pragma unroll
+            for (int j = 0; j < RP; j++) {
+                const int r = tid * RP + j;
+                sm.end[0][r] = ex[0];
+                sm.end[1][r] = ex[1];
+                sm.jst[r] = ex[2];
+#pragma unroll
+                for (int q = 0; q < 3; q++) ex[q] += c[q][j];
+            }
+            if (tid == 0) {
+                sm.jst[kStRange] = tot[2];
+                p.counts[gi] = tot[2];
+                atomicAdd(&p.plan->nbigdev, 1u);
+            }
+        }
+        __syncthreads();
+        // pass 2: chunks in input order; the waves take turns (wave-major,
+        // item, lane = input order within the chunk)
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            if (x >= p.ntab || (SMJ_BG_ABL & 2)) break;
+            const MsdTab &tb = p.tab[x];
+            const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
+            i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (x ? g.outS : g.outR);
+            const uint32_t nx = x ? nS : g.nR;
+            for (uint32_t v0 = 0; v0 < nx; v0 += kGroupCap) {
+                i64x2 rows[kBgIt];
+                uint32_t dig[kBgIt], vmask = 0;
+#pragma unroll
+                for (int i = 0; i < kBgIt; i++) {
+                    const uint32_t v = v0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
+                    rows[i] = i64x2{0, 0};
+                    dig[i] = 0;
+                    if (v < nx) {
+                        rows[i] = tB[bg_src(sm.list[x], sm.nl[x], v)];
+                        dig[i] = (uint32_t)((uint64_t)(tb.key ? rows[i].y : rows[i].x) - (uint64_t)g.base);
+                        vmask |= 1u << i;
+                    }
+                }
+                uint32_t pos[kBgIt];
+                for (int w = 0; w < kMsdWaves; w++) {
+                    if (wave == w) bg_rank<kBgIt, 12>(dig, vmask, sm.end[x], lane, pos);
+                    __syncthreads();
+                }
+#pragma unroll
+                for (int i = 0; i < kBgIt; i++)  // plain stores: the join below reads them back through L1
+                    if ((vmask >> i) & 1u) dst[pos[i]] = rows[i];
+            }
+        }
+        if (join && !(SMJ_BG_ABL & 4)) {  // join rows from the sorted output ranges (written above by this workgroup)
+            // workgroup scope is enough: only this workgroup's own rows are read
+            // back, from the CU that wrote them.  (__threadfence()'s agent scope
+            // writes back the XCD's whole L2 on gfx950 -- 20 of C5's ms.)
+            __threadfence_block();
+            __syncthreads();
+            const uint32_t J = sm.jst[kStRange];
+            const i64x2 *oR = reinterpret_cast<const i64x2 *>(p.tab[0].out) + g.outR;
+            const i64x2 *oS = reinterpret_cast<const i64x2 *>(p.tab[1].out) + g.outS;
+            const int ks = p.tab[1].key;
+            int64_t *slot = p.slots + (int64_t)g.outR * 3;
+            for (uint32_t j = tid; j < J; j += kMsdThreads) {
+                int lo = 0, hi = kStRange - 1;  // the residual of join row j: last r with jst[r] <= j
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sm.jst[mid] <= j) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t i = j - sm.jst[lo];
+                // after pass 2 end[x][r] = the end of r's rows = the start of r + 1
+                const uint32_t sR = lo ? sm.end[0][lo - 1] : 0u, sS = lo ? sm.end[1][lo - 1] : 0u;
+                const i64x2 rr = oR[sR + i], rs = oS[sS + i];
+                slot[3 * (int64_t)j] = rr.x;
+                slot[3 * (int64_t)j + 1] = rr.y;
+                slot[3 * (int64_t)j + 2] = ks ? rs.x : rs.y;
+            }
+        }
+    }
+}
+
 static const unsigned long long zero8_pb[8] = {0};
 hipError_t read_msd_phases(unsigned long long *out16) {
     hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fin_phase), sizeof(unsigned long long) * 10);
@@ -3204,6 +3449,9 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
         q.radix_list = nullptr;
         hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+        // oversized multi-key groups of a small key span (the rest: host fallback)
+        static const unsigned bg_grid = (unsigned)resident_blocks(msd_big_stage_kernel, kMsdThreads, 0);
+        hipLaunchKernelGGL(msd_big_stage_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
     } else {
         MsdFinalParams q = p;
         q.radix_list = nullptr;  // contiguous mode

@@ -153,6 +153,17 @@ def msd_stats():
     return tuple(int(v) for v in out)
 
 
+def msd_bigdev():
+    """Oversized multi-key groups of the last MSD pipeline call sorted on the
+    device (msd_big_stage_kernel); the other oversized ones took the host-driven
+    fallback."""
+    lib = _lib.load()
+    if not hasattr(lib, "smj_debug_msd_bigdev"):
+        return 0
+    lib.smj_debug_msd_bigdev.restype = ctypes.c_int64
+    return int(lib.smj_debug_msd_bigdev())
+
+
 def msd_groups():
     """(dense groups, radix-tier groups, wide-tier groups, in-LDS LSD groups) of the
     last MSD pipeline call."""

@@ -190,6 +190,43 @@ def test_many_oversized_groups_batched(gpu, oracle_built, c1, c2, sel):
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
 
 
+@pytest.mark.parametrize("kc,sel", [(0, None), (1, (1, 1 << 22))])
+def test_small_span_oversized_groups_on_device(gpu, oracle_built, kc, sel):
+    """Oversized multi-key groups whose keys span few values (C5's Zipf shape:
+    a key with 1,100-6,000 rows next to light keys in a narrow sub-bucket) are
+    sorted and joined by msd_big_stage_kernel on the device -- a counting
+    sort over the residual in input-order chunks -- bit-exact against the
+    oracle, including keys heavy in one table only, adjacent heavy keys in one
+    sub-bucket, a group of several chunks, the key in column 1 and a WHERE."""
+    from smj import ops
+    rng = np.random.default_rng(11 + kc)
+    span = 1 << 24
+    heavy = rng.choice(span - 2, 240, replace=False)
+
+    def make(n, pay0, drop):
+        keys = [rng.integers(0, span, n)]
+        for i, v in enumerate(heavy):
+            if i % 9 == drop:  # heavy in the other table only
+                continue
+            keys.append(np.full(1100 + (i * 37) % 2400, v))
+            if i % 5 == 0:  # a second heavy key in the same sub-bucket
+                keys.append(np.full(1050 + (i * 53) % 900, v + 1))
+        keys.append(np.full(9000, heavy[7]))  # one group of several chunks, dealt in the large-first round
+        k = rng.permutation(np.concatenate(keys))
+        t = np.empty((len(k), 2), dtype=np.int64)
+        t[:, kc] = k
+        t[:, 1 - kc] = pay0 + np.arange(len(k))  # payload = row id: stability is visible
+        return t
+
+    R, S = make(3_000_000, 0, 2), make(2_500_000, 10 ** 9, 4)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, sel)
+    assert ops.msd_stats()[1] > 50 and ops.msd_bigdev() > 50, (ops.msd_stats(), ops.msd_bigdev())
+    Rs, Ss, J = ref_pipeline(R, S, kc, kc, sel, sel)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
 @pytest.mark.parametrize("n,cols,kind", [(100_000, 2, "uniform"), (70_000, 3, "dups"), (4097, 2, "wide")])
 def test_lsd_select_sort_matches_oracle(gpu, oracle_built, n, cols, kind):
     from smj import ops
