@@ -477,6 +477,8 @@ struct MsdScratch {
     int64_t *d_tmp = nullptr;
     int64_t *lspl = nullptr;    // partitioned mode: the part splitters (device)
     int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
+    void *giant = nullptr, *gmap = nullptr, *gh = nullptr;  // msd_giant_*: groups, job map, job counts
+    size_t c_giant = 0, c_gmap = 0, c_gh = 0;
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
@@ -490,6 +492,13 @@ struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
 PbLast g_pb_last[2];
 int g_pb_ntab = 0;
 MsdFinalParams g_fin_last{};  // last pipeline call's final launch (smj_debug_final_time)
+
+MsdBgLimits msd_bg_limits() {  // read per call: a test may change them between calls
+    MsdBgLimits r{kBgMaxRows, kBgSeg};
+    if (const char *e = getenv("SMJ_BG_MAX_ROWS")) r.max_rows = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = getenv("SMJ_BG_SEG")) r.seg = (uint32_t)std::max(1, atoi(e) / kGroupCap) * kGroupCap;
+    return r;
+}
 
 int msd_scratch(MsdScratch **out) {
     int dev = 0;
@@ -532,7 +541,7 @@ void msd_free_all() {
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
-                        (void *)m.lspl})
+                        (void *)m.lspl, m.giant, m.gmap, m.gh})
             hipFree(p);
         hipHostFree(m.h_plan);
         hipHostFree(m.h_samp);
@@ -589,15 +598,18 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
         HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
     }
-    // oversized multi-key groups of a small key span were sorted (and joined)
-    // on the device by msd_big_stage_kernel (2-column tables); the rest here
+    // oversized multi-key groups of a small key span are sorted (and joined)
+    // on the device (msd_big_stage_kernel, msd_giant_*; 2-column tables),
+    // launched here where the plan shows some; the rest on the host path below
     const bool two = in[0].cols == 2 && (ntab == 1 || in[1].cols == 2);
+    if (pl.nbig && two) {
+        ProfScope ps("msd_big_dev", 0, s);
+        HIP_TRY(launch_msd_big(fp, s));
+    }
     std::vector<uint32_t> host_bigs;
     for (uint32_t slot : bigs) {
         const MsdGroup &g = groups[slot];
-        if (!(two && msd_big_on_device(g.span, g.nR, ntab > 1 ? g.nS : 0u) && g.kt[0] <= (uint32_t)kGroupCap &&
-              g.kt[1] <= (uint32_t)kGroupCap))
-            host_bigs.push_back(slot);
+        if (!(two && msd_big_on_device(g.span, g.kt[0], g.kt[1]))) host_bigs.push_back(slot);
     }
     if (getenv("SMJ_DEBUG_BIG")) {  // size distribution of the oversized multi-key groups (rows, log2 bins)
         int64_t hist[2][33] = {}, rows[2][33] = {};
@@ -759,6 +771,13 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
     if (join) SMJ_TRY(grow(&ms->slots, &ms->c_slots, std::max<size_t>(1, in[0].n) * tc * 8));
+    {  // oversized groups split into jobs (msd_giant_*): their worst-case count for this call
+        const MsdBgLimits bl = msd_bg_limits();
+        const int64_t rows_all = in[0].n + (ntab > 1 ? in[1].n : 0), jobs = msd_giant_jobs_max(rows_all, bl);
+        SMJ_TRY(grow(&ms->giant, &ms->c_giant, (size_t)(rows_all / bl.max_rows + 2) * sizeof(uint4)));
+        SMJ_TRY(grow(&ms->gmap, &ms->c_gmap, (size_t)jobs * 4));
+        SMJ_TRY(grow(&ms->gh, &ms->c_gh, (size_t)jobs * 2 * kStageRange * 4));
+    }
     HIP_TRY(hipMemsetAsync(ms->plan, 0, sizeof(MsdPlan), s));
     auto segL = [&](int x) { return (uint32_t *)ms->t[x].seg; };
     auto segC = [&](int x) { return (uint32_t *)ms->t[x].seg + kMsdSegs * kOffsA; };
@@ -902,6 +921,12 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.big_list = ms->big_list;
     fp.wide_list = ms->wide_list;
     fp.radix_list = ms->radix_list;
+    fp.giant = (uint4 *)ms->giant;
+    fp.gmap = (uint32_t *)ms->gmap;
+    fp.gh = (uint32_t *)ms->gh;
+    const MsdBgLimits bl = msd_bg_limits();
+    fp.bg_max = bl.max_rows;
+    fp.bg_seg = bl.seg;
     fp.ntab = ntab;
     fp.join = join;
     fp.key2 = key2;
@@ -948,8 +973,9 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     if (redo) {
         SMJ_TRY(compact(1));
         pc = prof_last();
-        HIP_TRY(hipMemcpyAsync(&ms->h_plan->joined, &ms->plan->joined, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));  // joined, nbigdev
         HIP_TRY(hipStreamSynchronize(s));
+        if (t_slot < 0) g_msd_bigdev = ms->h_plan->nbigdev;
     }
     const MsdPlan &pl = *ms->h_plan;
     double pa_bytes = 0.0;

@@ -182,11 +182,25 @@ constexpr int kStageRange = 4096;          // key range of the staged final path
 #ifndef SMJ_BG_MAX_ROWS
 #define SMJ_BG_MAX_ROWS 131072
 #endif
-constexpr uint32_t kBgMaxRows = SMJ_BG_MAX_ROWS;  // rows per table of an oversized group msd_big_stage_kernel takes
-// an oversized multi-key group sorted on the device (msd_big_stage_kernel);
-// the others take the host-driven fallback (smj_api.hip msd_fallback)
-__host__ __device__ inline bool msd_big_on_device(uint32_t span, uint32_t nR, uint32_t nS) {
-    return span <= (uint32_t)kStageRange && nR <= kBgMaxRows && nS <= kBgMaxRows;
+constexpr uint32_t kBgMaxRows = SMJ_BG_MAX_ROWS;  // rows per table of an oversized group one workgroup sorts
+constexpr uint32_t kBgSeg = 32768;               // rows per table of a job of a larger group (msd_giant_*)
+// an oversized multi-key group sorted on the device (msd_big_stage_kernel /
+// msd_giant_*, 2-column tables): keys spanning <= kStageRange values and a
+// run list that fits LDS; the others take the host-driven fallback
+// (smj_api.hip msd_fallback)
+__host__ __device__ inline bool msd_big_on_device(uint32_t span, uint32_t ktR, uint32_t ktS) {
+    return span <= (uint32_t)kStageRange && ktR <= (uint32_t)kGroupCap && ktS <= (uint32_t)kGroupCap;
+}
+// the thresholds in force: kBgMaxRows / kBgSeg, or SMJ_BG_MAX_ROWS / SMJ_BG_SEG
+// from the environment (tests: giant groups at small sizes; the segment a
+// multiple of kGroupCap)
+struct MsdBgLimits {
+    uint32_t max_rows, seg;
+};
+MsdBgLimits msd_bg_limits();
+// jobs the giant groups of tables of `rows` rows in all can need
+inline int64_t msd_giant_jobs_max(int64_t rows, const MsdBgLimits &l) {
+    return rows / l.seg + rows / (int64_t)l.max_rows + 2;
 }
 constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
@@ -252,6 +266,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t nlsd;       // staged groups sorted by the in-LDS LSD (equal-key runs over kMaxDupRun)
     uint32_t nbigdev;    // oversized multi-key groups sorted on the device (msd_big_stage_kernel)
     uint32_t bgticket[2];// msd_big_stage_kernel's group tickets (large groups first, then the rest)
+    uint32_t ngiant;     // groups over kBgMaxRows rows registered as jobs
+    uint32_t njobs;      // their jobs
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)
@@ -314,6 +330,10 @@ struct MsdFinalParams {
     uint32_t *big_list;
     uint32_t *wide_list; // dense indices of groups for msd_final_wide_kernel
     uint32_t *radix_list;// groups for the radix tier (msd_final_kernel in list mode; nullptr = contiguous mode)
+    uint4 *giant;        // groups over kBgMaxRows rows: {dense group, first job, jobs}
+    uint32_t *gmap;      // job -> its giant entry
+    uint32_t *gh;        // [job][2][kStageRange] residual counts of each job's rows
+    uint32_t bg_max, bg_seg;  // msd_bg_limits()
     int ntab, join, key2, dbg;
 };
 
@@ -355,6 +375,7 @@ hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, in
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
+hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
 // batched fallback (oversized multi-key groups): see smj_msd.hip
 hipError_t launch_msd_gather_list(const MsdTab &tb, const MsdGroup *groups, const uint4 *work, int64_t nwork,

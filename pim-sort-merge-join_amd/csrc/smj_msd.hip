@@ -2797,6 +2797,7 @@ constexpr int kBgIt = kGroupCap / kMsdThreads;  // chunk rows per thread
 #define SMJ_BG_ABL 0  // timing ablation (output invalid): 1 = no counting pass, 2 = no row pass, 4 = no join rows
 #endif
 constexpr uint32_t kBgLarge = 8 * kGroupCap;  // groups over this many rows (either table) are dealt first
+static_assert(kBgSeg % kGroupCap == 0 && kStRange % (4 * kMsdThreads) == 0, "giant jobs: whole chunks, uint4 counts");
 struct BgSmem {
     uint32_t end[2][kStRange];   // per residual: row count, then the running start of its output rows
     uint32_t jst[kStRange + 1];  // exclusive prefix over residuals of min(countR, countS) (join rows)
@@ -2806,9 +2807,14 @@ struct BgSmem {
     uint32_t ticket;
 };
 
-__device__ __forceinline__ bool bg_ok(const MsdGroup &g) {
-    return g.flags == kGroupBig && msd_big_on_device(g.span, g.nR, g.nS) && g.kt[0] <= (uint32_t)kGroupCap &&
-           g.kt[1] <= (uint32_t)kGroupCap;
+__device__ __forceinline__ bool bg_dev(const MsdGroup &g) {  // sorted on the device (either kernel)
+    return g.flags == kGroupBig && msd_big_on_device(g.span, g.kt[0], g.kt[1]);
+}
+__device__ __forceinline__ bool bg_giant(const MsdGroup &g, uint32_t bg_max) {  // by jobs (msd_giant_*)
+    return bg_dev(g) && max(g.nR, g.nS) > bg_max;
+}
+__device__ __forceinline__ bool bg_ok(const MsdGroup &g, uint32_t bg_max) {  // by one workgroup (msd_big_stage_kernel)
+    return bg_dev(g) && max(g.nR, g.nS) <= bg_max;
 }
 
 // wave_rank with 32-bit positions: pos[it] = wc[digit] + the row's rank among
@@ -2850,11 +2856,161 @@ __device__ __forceinline__ uint32_t bg_src(const uint2 *lst, uint32_t nl, uint32
     return e.x + (v - e.y);
 }
 
+// the group's run list per table (one block scan each), then a barrier
+__device__ __forceinline__ void bg_lists(const MsdFinalParams &p, const MsdGroup &g, BgSmem &sm) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        if (x >= p.ntab) break;
+        const MsdTab &tb = p.tab[x];
+        uint32_t src[kBgIt], len[kBgIt], sum = 0;
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t j = (uint32_t)tid * kBgIt + i;
+            src[i] = len[i] = 0;
+            if (j < g.kt[x]) {
+                const int64_t id = (int64_t)g.tb[x] + j;
+                const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
+                src[i] = (uint32_t)id * (uint32_t)tb.tile + lo;
+                len[i] = hi - lo;
+            }
+            sum += len[i];
+        }
+        uint32_t total;
+        uint32_t ex = block_excl_scan<kMsdWaves>(sum, sm.wsum, &total);
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t j = (uint32_t)tid * kBgIt + i;
+            if (j < g.kt[x]) sm.list[x][j] = make_uint2(src[i], ex);
+            ex += len[i];
+        }
+        if (tid == 0) sm.nl[x] = g.kt[x];
+    }
+    __syncthreads();
+}
+
+// residual counts of rows [v0, v1) of table X into cnt (LDS atomics)
+template <int X>
+__device__ __forceinline__ void bg_count(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
+                                         BgSmem &sm, uint32_t *cnt) {
+    const MsdTab &tb = p.tab[X];
+    const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
+    const int tid = threadIdx.x;
+    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
+        int64_t k[kBgIt];
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t v = c0 + tid + i * kMsdThreads;
+            k[i] = 0;
+            if (v < v1) {
+                const i64x2 r = tB[bg_src(sm.list[X], sm.nl[X], v)];
+                k[i] = tb.key ? r.y : r.x;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++)
+            if (c0 + tid + i * kMsdThreads < v1) atomicAdd(&cnt[(uint32_t)((uint64_t)k[i] - (uint64_t)g.base)], 1u);
+    }
+}
+
+// rows [v0, v1) of table X to their places: chunks in input order, the
+// waves taking turns (wave-major, item, lane = input order within a chunk);
+// end[r] = the next output row of residual r, advanced
+template <int X>
+__device__ __forceinline__ void bg_scatter(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
+                                           BgSmem &sm) {
+    const MsdTab &tb = p.tab[X];
+    const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
+    i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (X ? g.outS : g.outR);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
+        i64x2 rows[kBgIt];
+        uint32_t dig[kBgIt], vmask = 0;
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
+            rows[i] = i64x2{0, 0};
+            dig[i] = 0;
+            if (v < v1) {
+                rows[i] = tB[bg_src(sm.list[X], sm.nl[X], v)];
+                dig[i] = (uint32_t)((uint64_t)(tb.key ? rows[i].y : rows[i].x) - (uint64_t)g.base);
+                vmask |= 1u << i;
+            }
+        }
+        uint32_t pos[kBgIt];
+        for (int w = 0; w < kMsdWaves; w++) {
+            if (wave == w) bg_rank<kBgIt, 12>(dig, vmask, sm.end[X], lane, pos);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++)  // plain stores: a join read-back goes through L1
+            if ((vmask >> i) & 1u) dst[pos[i]] = rows[i];
+    }
+}
+
+// join rows [j0, j1) of group g: row j of residual r (jst[r] <= j < jst[r + 1])
+// pairs occurrence i = j - jst[r] of r in R and in S, whose sorted output
+// rows start at startR(r), startS(r) (ends: those of r - 1)
+__device__ __forceinline__ void bg_join(const MsdFinalParams &p, const MsdGroup &g, uint32_t j0, uint32_t j1,
+                                        const BgSmem &sm, bool ends) {
+    const i64x2 *oR = reinterpret_cast<const i64x2 *>(p.tab[0].out) + g.outR;
+    const i64x2 *oS = reinterpret_cast<const i64x2 *>(p.tab[1].out) + g.outS;
+    const int ks = p.tab[1].key;
+    int64_t *slot = p.slots + (int64_t)g.outR * 3;
+    for (uint32_t j = j0 + threadIdx.x; j < j1; j += kMsdThreads) {
+        int lo = 0, hi = kStRange - 1;  // the residual of join row j: last r with jst[r] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sm.jst[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t i = j - sm.jst[lo];
+        const uint32_t sR = ends ? (lo ? sm.end[0][lo - 1] : 0u) : sm.end[0][lo];
+        const uint32_t sS = ends ? (lo ? sm.end[1][lo - 1] : 0u) : sm.end[1][lo];
+        const i64x2 rr = oR[sR + i], rs = oS[sS + i];
+        slot[3 * (int64_t)j] = rr.x;
+        slot[3 * (int64_t)j + 1] = rr.y;
+        slot[3 * (int64_t)j + 2] = ks ? rs.x : rs.y;
+    }
+}
+
+// per-residual counts c[x][r] in sm.end -> exclusive output starts, and
+// min(cR, cS) -> the join-row prefix jst (jst[kStRange] = the join rows);
+// returns the join rows.  Ends with a barrier.
+__device__ __forceinline__ uint32_t bg_starts(BgSmem &sm, bool join) {
+    constexpr int RP = kStRange / kMsdThreads;
+    const int tid = threadIdx.x;
+    uint32_t c[3][RP], sum[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < RP; j++) {
+        const int r = tid * RP + j;
+        c[0][j] = sm.end[0][r];
+        c[1][j] = sm.end[1][r];
+        c[2][j] = join ? min(c[0][j], c[1][j]) : 0u;
+#pragma unroll
+        for (int q = 0; q < 3; q++) sum[q] += c[q][j];
+    }
+    uint32_t ex[3], tot[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) ex[q] = block_excl_scan<kMsdWaves>(sum[q], sm.wsum, &tot[q]);
+#pragma unroll
+    for (int j = 0; j < RP; j++) {
+        const int r = tid * RP + j;
+        sm.end[0][r] = ex[0];
+        sm.end[1][r] = ex[1];
+        sm.jst[r] = ex[2];
+#pragma unroll
+        for (int q = 0; q < 3; q++) ex[q] += c[q][j];
+    }
+    if (tid == 0) sm.jst[kStRange] = tot[2];
+    __syncthreads();
+    return tot[2];
+}
+
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
     const uint32_t nbig = p.plan->nbig;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int RP = kStRange / kMsdThreads;  // residuals per thread in the scans
+    const int tid = threadIdx.x;
+    const bool join = p.join && p.ntab > 1;
     // dynamic tickets over the (unordered) list, twice: the groups over
     // kBgLarge rows first, so that the longest ones do not start last
     for (int round = 0; round < 2; round++)
@@ -2866,127 +3022,35 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
         if (bi >= nbig) break;
         const uint32_t gi = p.big_list[bi];
         const MsdGroup g = p.groups[gi];
-        if (!bg_ok(g)) continue;  // block-uniform: left to the host fallback
-        if ((max(g.nR, g.nS) > kBgLarge) != (round == 0)) continue;
-        const uint32_t nS = p.ntab > 1 ? g.nS : 0u;
-        for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
-        // the runs of the group in each table's pass-B tiles (one block scan per table)
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            if (x >= p.ntab) break;
-            const MsdTab &tb = p.tab[x];
-            uint32_t src[kBgIt], len[kBgIt], sum = 0;
-#pragma unroll
-            for (int i = 0; i < kBgIt; i++) {
-                const uint32_t j = (uint32_t)tid * kBgIt + i;
-                src[i] = len[i] = 0;
-                if (j < g.kt[x]) {
-                    const int64_t id = (int64_t)g.tb[x] + j;
-                    const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
-                    src[i] = (uint32_t)id * (uint32_t)tb.tile + lo;
-                    len[i] = hi - lo;
-                }
-                sum += len[i];
-            }
-            uint32_t total;
-            uint32_t ex = block_excl_scan<kMsdWaves>(sum, sm.wsum, &total);
-#pragma unroll
-            for (int i = 0; i < kBgIt; i++) {
-                const uint32_t j = (uint32_t)tid * kBgIt + i;
-                if (j < g.kt[x]) sm.list[x][j] = make_uint2(src[i], ex);
-                ex += len[i];
-            }
-            if (tid == 0) sm.nl[x] = g.kt[x];
-        }
-        __syncthreads();
-        // pass 1: residual counts of both tables
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            if (x >= p.ntab || (SMJ_BG_ABL & 1)) break;
-            const MsdTab &tb = p.tab[x];
-            const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
-            const uint32_t nx = x ? nS : g.nR;
-            for (uint32_t v0 = 0; v0 < nx; v0 += kGroupCap) {
-                int64_t k[kBgIt];
-#pragma unroll
-                for (int i = 0; i < kBgIt; i++) {
-                    const uint32_t v = v0 + tid + i * kMsdThreads;
-                    k[i] = 0;
-                    if (v < nx) {
-                        const i64x2 r = tB[bg_src(sm.list[x], sm.nl[x], v)];
-                        k[i] = tb.key ? r.y : r.x;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < kBgIt; i++)
-                    if (v0 + tid + i * kMsdThreads < nx) atomicAdd(&sm.end[x][(uint32_t)((uint64_t)k[i] - (uint64_t)g.base)], 1u);
-            }
-        }
-        __syncthreads();
-        // counts -> exclusive output starts per table; min(cR, cS) -> join-row starts
-        const bool join = p.join && p.ntab > 1;
-        {
-            uint32_t c[3][RP], sum[3] = {0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < RP; j++) {
-                const int r = tid * RP + j;
-                c[0][j] = sm.end[0][r];
-                c[1][j] = sm.end[1][r];
-                c[2][j] = join ? min(c[0][j], c[1][j]) : 0u;
-#pragma unroll
-                for (int q = 0; q < 3; q++) sum[q] += c[q][j];
-            }
-            uint32_t ex[3], tot[3];
-#pragma unroll
-            for (int q = 0; q < 3; q++) ex[q] = block_excl_scan<kMsdWaves>(sum[q], sm.wsum, &tot[q]);
-#pragma unroll
-            for (int j = 0; j < RP; j++) {
-                const int r = tid * RP + j;
-                sm.end[0][r] = ex[0];
-                sm.end[1][r] = ex[1];
-                sm.jst[r] = ex[2];
-#pragma unroll
-                for (int q = 0; q < 3; q++) ex[q] += c[q][j];
-            }
+        if (round == 0 && bg_giant(g, p.bg_max)) {  // over kBgMaxRows rows: split into jobs (msd_giant_*)
+            const uint32_t nseg = (max(g.nR, p.ntab > 1 ? g.nS : 0u) + p.bg_seg - 1) / p.bg_seg;
             if (tid == 0) {
-                sm.jst[kStRange] = tot[2];
-                p.counts[gi] = tot[2];
-                atomicAdd(&p.plan->nbigdev, 1u);
+                const uint32_t base = atomicAdd(&p.plan->njobs, nseg), idx = atomicAdd(&p.plan->ngiant, 1u);
+                p.giant[idx] = make_uint4(gi, base, nseg, 0u);
+                sm.ticket = base;
+                sm.nl[0] = idx;
             }
+            __syncthreads();
+            for (uint32_t k = tid; k < nseg; k += kMsdThreads) p.gmap[sm.ticket + k] = sm.nl[0];
+            continue;
+        }
+        if (!bg_ok(g, p.bg_max)) continue;  // block-uniform: a giant, or left to the host fallback
+        if ((max(g.nR, g.nS) > kBgLarge) != (round == 0)) continue;
+        for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
+        bg_lists(p, g, sm);
+        if (!(SMJ_BG_ABL & 1)) {  // pass 1: residual counts of both tables
+            bg_count<0>(p, g, 0, g.nR, sm, sm.end[0]);
+            if (p.ntab > 1) bg_count<1>(p, g, 0, g.nS, sm, sm.end[1]);
         }
         __syncthreads();
-        // pass 2: chunks in input order; the waves take turns (wave-major,
-        // item, lane = input order within the chunk)
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            if (x >= p.ntab || (SMJ_BG_ABL & 2)) break;
-            const MsdTab &tb = p.tab[x];
-            const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
-            i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (x ? g.outS : g.outR);
-            const uint32_t nx = x ? nS : g.nR;
-            for (uint32_t v0 = 0; v0 < nx; v0 += kGroupCap) {
-                i64x2 rows[kBgIt];
-                uint32_t dig[kBgIt], vmask = 0;
-#pragma unroll
-                for (int i = 0; i < kBgIt; i++) {
-                    const uint32_t v = v0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
-                    rows[i] = i64x2{0, 0};
-                    dig[i] = 0;
-                    if (v < nx) {
-                        rows[i] = tB[bg_src(sm.list[x], sm.nl[x], v)];
-                        dig[i] = (uint32_t)((uint64_t)(tb.key ? rows[i].y : rows[i].x) - (uint64_t)g.base);
-                        vmask |= 1u << i;
-                    }
-                }
-                uint32_t pos[kBgIt];
-                for (int w = 0; w < kMsdWaves; w++) {
-                    if (wave == w) bg_rank<kBgIt, 12>(dig, vmask, sm.end[x], lane, pos);
-                    __syncthreads();
-                }
-#pragma unroll
-                for (int i = 0; i < kBgIt; i++)  // plain stores: the join below reads them back through L1
-                    if ((vmask >> i) & 1u) dst[pos[i]] = rows[i];
-            }
+        const uint32_t J = bg_starts(sm, join);
+        if (tid == 0) {
+            p.counts[gi] = J;
+            atomicAdd(&p.plan->nbigdev, 1u);
+        }
+        if (!(SMJ_BG_ABL & 2)) {  // pass 2
+            bg_scatter<0>(p, g, 0, g.nR, sm);
+            if (p.ntab > 1) bg_scatter<1>(p, g, 0, g.nS, sm);
         }
         if (join && !(SMJ_BG_ABL & 4)) {  // join rows from the sorted output ranges (written above by this workgroup)
             // workgroup scope is enough: only this workgroup's own rows are read
@@ -2994,26 +3058,115 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
             // writes back the XCD's whole L2 on gfx950 -- 20 of C5's ms.)
             __threadfence_block();
             __syncthreads();
-            const uint32_t J = sm.jst[kStRange];
-            const i64x2 *oR = reinterpret_cast<const i64x2 *>(p.tab[0].out) + g.outR;
-            const i64x2 *oS = reinterpret_cast<const i64x2 *>(p.tab[1].out) + g.outS;
-            const int ks = p.tab[1].key;
-            int64_t *slot = p.slots + (int64_t)g.outR * 3;
-            for (uint32_t j = tid; j < J; j += kMsdThreads) {
-                int lo = 0, hi = kStRange - 1;  // the residual of join row j: last r with jst[r] <= j
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sm.jst[mid] <= j) lo = mid; else hi = mid - 1;
+            bg_join(p, g, 0, J, sm, true);
+        }
+    }
+}
+
+// Groups over kBgMaxRows rows (the largest Zipf groups: up to ~1e6 rows, one
+// workgroup would take ~17 ms): the same counting sort split into jobs of
+// kBgSeg rows per table, in three launches -- per-job residual counts to
+// global memory (gh[job][table][r]); each job's output starts (the group's
+// totals scanned + the counts of its earlier jobs) and its rows scattered;
+// the join rows, kBgSeg per job.  Jobs of one group are numbered
+// giant[i].y + s; gmap[job] = i.
+struct GiantJob {
+    uint32_t gi, s, nseg, job0;
+};
+__device__ __forceinline__ GiantJob giant_job(const MsdFinalParams &p, uint32_t t) {
+    const uint4 e = p.giant[p.gmap[t]];
+    return GiantJob{e.x, t - e.y, e.z, e.y};
+}
+
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_count_kernel(const MsdFinalParams p) {
+    __shared__ BgSmem sm;
+    const uint32_t nj = p.plan->njobs;
+    for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
+        const GiantJob jb = giant_job(p, t);
+        const MsdGroup g = p.groups[jb.gi];
+        for (int i = threadIdx.x; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
+        bg_lists(p, g, sm);
+        const uint32_t v0 = jb.s * p.bg_seg;
+        bg_count<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm, sm.end[0]);
+        if (p.ntab > 1) bg_count<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm, sm.end[1]);
+        __syncthreads();
+        uint32_t *h = p.gh + (int64_t)t * 2 * kStRange;
+        for (int i = threadIdx.x; i < 2 * kStRange; i += kMsdThreads) h[i] = (&sm.end[0][0])[i];
+        __syncthreads();
+    }
+}
+
+// the group's residual totals (all its jobs) into sm.end, and into pre[x][r]
+// (per thread: residuals tid * RP + j) the counts of the jobs before s
+__device__ __forceinline__ void giant_totals(const MsdFinalParams &p, const GiantJob &jb, BgSmem &sm,
+                                             uint32_t (&pre)[2][kStRange / kMsdThreads]) {
+    constexpr int RP = kStRange / kMsdThreads;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t tot[RP];
+#pragma unroll
+        for (int j = 0; j < RP; j++) tot[j] = pre[x][j] = 0;
+        for (uint32_t q = 0; q < jb.nseg; q++) {
+            const uint4 *h = reinterpret_cast<const uint4 *>(p.gh + ((int64_t)(jb.job0 + q) * 2 + x) * kStRange) + tid * (RP / 4);
+#pragma unroll
+            for (int u = 0; u < RP / 4; u++) {
+                const uint4 v = h[u];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    tot[4 * u + k] += w[k];
+                    if (q < jb.s) pre[x][4 * u + k] += w[k];
                 }
-                const uint32_t i = j - sm.jst[lo];
-                // after pass 2 end[x][r] = the end of r's rows = the start of r + 1
-                const uint32_t sR = lo ? sm.end[0][lo - 1] : 0u, sS = lo ? sm.end[1][lo - 1] : 0u;
-                const i64x2 rr = oR[sR + i], rs = oS[sS + i];
-                slot[3 * (int64_t)j] = rr.x;
-                slot[3 * (int64_t)j + 1] = rr.y;
-                slot[3 * (int64_t)j + 2] = ks ? rs.x : rs.y;
             }
         }
+#pragma unroll
+        for (int j = 0; j < RP; j++) sm.end[x][tid * RP + j] = tot[j];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const MsdFinalParams p) {
+    __shared__ BgSmem sm;
+    constexpr int RP = kStRange / kMsdThreads;
+    const uint32_t nj = p.plan->njobs;
+    const bool join = p.join && p.ntab > 1;
+    for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
+        const GiantJob jb = giant_job(p, t);
+        const MsdGroup g = p.groups[jb.gi];
+        uint32_t pre[2][RP];
+        giant_totals(p, jb, sm, pre);
+        bg_starts(sm, join);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int j = 0; j < RP; j++) sm.end[x][threadIdx.x * RP + j] += pre[x][j];
+        bg_lists(p, g, sm);  // (its barrier also orders the starts above)
+        const uint32_t v0 = jb.s * p.bg_seg;
+        bg_scatter<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm);
+        if (p.ntab > 1) bg_scatter<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_join_kernel(const MsdFinalParams p) {
+    __shared__ BgSmem sm;
+    constexpr int RP = kStRange / kMsdThreads;
+    const uint32_t nj = p.plan->njobs;
+    const bool join = p.join && p.ntab > 1;
+    for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
+        const GiantJob jb = giant_job(p, t);
+        const MsdGroup g = p.groups[jb.gi];
+        uint32_t pre[2][RP];
+        giant_totals(p, jb, sm, pre);
+        const uint32_t J = bg_starts(sm, join);  // sm.end = the starts
+        if (jb.s == 0 && threadIdx.x == 0) {
+            p.counts[jb.gi] = J;
+            atomicAdd(&p.plan->nbigdev, 1u);
+        }
+        const uint32_t j0 = jb.s * p.bg_seg;
+        if (join && j0 < J) bg_join(p, g, j0, min(J, j0 + p.bg_seg), sm, false);
+        __syncthreads();
     }
 }
 
@@ -3434,6 +3587,18 @@ hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// oversized multi-key groups of a small key span (2-column tables; the
+// rest: host fallback), launched by the host once the plan shows some
+hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s) {
+    static const unsigned bg_grid = (unsigned)resident_blocks(msd_big_stage_kernel, kMsdThreads, 0);
+    hipLaunchKernelGGL(msd_big_stage_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
+    // the groups over the one-workgroup limit it registered, as jobs (no-ops without)
+    hipLaunchKernelGGL(msd_giant_count_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
+    hipLaunchKernelGGL(msd_giant_scatter_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
+    hipLaunchKernelGGL(msd_giant_join_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
     MsdFinalParams p = p_in;
@@ -3449,9 +3614,6 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
         q.radix_list = nullptr;
         hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
-        // oversized multi-key groups of a small key span (the rest: host fallback)
-        static const unsigned bg_grid = (unsigned)resident_blocks(msd_big_stage_kernel, kMsdThreads, 0);
-        hipLaunchKernelGGL(msd_big_stage_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
     } else {
         MsdFinalParams q = p;
         q.radix_list = nullptr;  // contiguous mode

@@ -190,15 +190,22 @@ def test_many_oversized_groups_batched(gpu, oracle_built, c1, c2, sel):
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
 
 
-@pytest.mark.parametrize("kc,sel", [(0, None), (1, (1, 1 << 22))])
-def test_small_span_oversized_groups_on_device(gpu, oracle_built, kc, sel):
+@pytest.mark.parametrize("kc,sel,giant", [(0, None, False), (1, (1, 1 << 22), False), (0, None, True),
+                                          (1, (1, 1 << 22), True)])
+def test_small_span_oversized_groups_on_device(gpu, oracle_built, monkeypatch, kc, sel, giant):
     """Oversized multi-key groups whose keys span few values (C5's Zipf shape:
     a key with 1,100-6,000 rows next to light keys in a narrow sub-bucket) are
     sorted and joined by msd_big_stage_kernel on the device -- a counting
     sort over the residual in input-order chunks -- bit-exact against the
     oracle, including keys heavy in one table only, adjacent heavy keys in one
-    sub-bucket, a group of several chunks, the key in column 1 and a WHERE."""
+    sub-bucket, a group of several chunks, the key in column 1 and a WHERE.
+    giant: the groups over the one-workgroup limit (lowered here from 131072
+    to 2048 rows) go through the job split (msd_giant_*: per-job counts,
+    scatter and join launches; jobs of 2048 rows)."""
     from smj import ops
+    if giant:
+        monkeypatch.setenv("SMJ_BG_MAX_ROWS", "2048")
+        monkeypatch.setenv("SMJ_BG_SEG", "2048")
     rng = np.random.default_rng(11 + kc)
     span = 1 << 24
     heavy = rng.choice(span - 2, 240, replace=False)
