@@ -846,9 +846,22 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     if (pa_fused) pa[0] = prof_last();
     {
         ProfScope ps("msd_runs", 0, s);
-        for (int x = 0; x < ntab; x++)
-            HIP_TRY(launch_msd_runs_seg((const uint32_t *)ms->t[x].offsA, tilesA[x], segL(x), segC(x),
-                                        (const int64_t *)ms->t[x].tmm, segMM(x), s));
+        MsdRunsArgs ra{};
+        for (int x = 0; x < ntab; x++) {
+            ra.offs[x] = (const uint32_t *)ms->t[x].offsA;
+            ra.ntiles[x] = tilesA[x];
+            ra.segL[x] = segL(x);
+            ra.segC[x] = segC(x);
+            ra.tmm[x] = (const int64_t *)ms->t[x].tmm;
+            ra.segmm[x] = segMM(x);
+            ra.T[x] = T_[x];
+            ra.TB[x] = TB_[x];
+            ra.bk[x] = (const MsdBucket *)ms->t[x].bk;
+            ra.list[x] = (uint2 *)ms->t[x].list;
+            ra.tinfo[x] = (uint2 *)ms->t[x].tinfo;
+        }
+        ra.ntab = ntab;
+        HIP_TRY(launch_msd_runs_seg(ra, s));
         uint32_t *sa[4], *ta[4];
         for (int x = 0; x < ntab; x++) {
             sa[2 * x] = segL(x);
@@ -871,10 +884,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         bp.spl = ms->spl;
         bp.plan = ms->plan;
         HIP_TRY(launch_msd_bases(bp, s));
-        for (int x = 0; x < ntab; x++)
-            HIP_TRY(launch_msd_runs_apply((const uint32_t *)ms->t[x].offsA, tilesA[x], T_[x], TB_[x], segL(x), segC(x),
-                                          (const MsdBucket *)ms->t[x].bk, (uint2 *)ms->t[x].list,
-                                          (uint2 *)ms->t[x].tinfo, s));
+        HIP_TRY(launch_msd_runs_apply(ra, s));
     }
     size_t pb[2] = {(size_t)-1, (size_t)-1};
     for (int x = 0; x < ntab; x++) {

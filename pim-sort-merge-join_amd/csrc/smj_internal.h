@@ -365,13 +365,21 @@ hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p, int cols, int64_t t0
 hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s);
 // per-bucket run sums and counts per segment; also the selected-key min / max
 // per (segment, wave): segmm[kMsdSegs * 4][2] (256 entries, INT64_MAX / MIN when empty)
-hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
-                               const int64_t *tmm, int64_t *segmm, hipStream_t s);
+struct MsdRunsArgs {     // msd_runs_seg / msd_runs_apply over both tables (blockIdx.z = table)
+    const uint32_t *offs[2];
+    int64_t ntiles[2];
+    uint32_t *segL[2], *segC[2];
+    const int64_t *tmm[2];
+    int64_t *segmm[2];
+    int T[2], TB[2];
+    const MsdBucket *bk[2];
+    uint2 *list[2], *tinfo[2];
+    int ntab;
+};
+hipError_t launch_msd_runs_seg(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int narr, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
-hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
-                                 const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
-                                 hipStream_t s);
+hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);

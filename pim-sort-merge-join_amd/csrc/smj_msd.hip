@@ -380,7 +380,7 @@ __device__ __forceinline__ void msd_seg_range(int64_t ntiles, int64_t &c0, int64
 
 // grid (ceil(nb / 64), kMsdSegs) x 256: lane = bucket; rows summed and
 // non-empty runs counted per segment
-__global__ __launch_bounds__(256) void msd_runs_seg_kernel(const uint32_t *__restrict__ offs, int64_t ntiles,
+__device__ __forceinline__ void runs_seg_body(const uint32_t *__restrict__ offs, int64_t ntiles,
                                                            int width, int nb, uint32_t *__restrict__ segL,
                                                            uint32_t *__restrict__ segC, const int64_t *__restrict__ tmm,
                                                            int64_t *__restrict__ segmm) {
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
 // list entries (coalesced; a lane-per-bucket loop wrote 64 scattered 8-B
 // entries per store, 90 us per table at C3).  The offsA loads are strided,
 // but a 128-B line of a tile's row serves 32 buckets' waves from L2.
-__global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__restrict__ offs, int64_t ntiles,
+__device__ __forceinline__ void runs_apply_body(const uint32_t *__restrict__ offs, int64_t ntiles,
                                                              int T, int TB, const uint32_t *__restrict__ segL,
                                                              const uint32_t *__restrict__ segC,
                                                              const MsdBucket *__restrict__ bk,
@@ -615,6 +615,22 @@ __global__ __launch_bounds__(256) void msd_runs_apply_kernel(const uint32_t *__r
         P += (uint32_t)__shfl((int)il, 63, 64);
         Q += (uint32_t)__shfl((int)iq, 63, 64);
     }
+}
+
+// both tables in one launch (blockIdx.z = table): one ramp and tail instead of two
+__global__ __launch_bounds__(256) void msd_runs_seg_kernel(const MsdRunsArgs a) {
+    const int x = blockIdx.z;
+    if (x >= a.ntab) return;
+    runs_seg_body(x ? a.offs[1] : a.offs[0], x ? a.ntiles[1] : a.ntiles[0], kOffsARow, kBucketsA,
+                  x ? a.segL[1] : a.segL[0], x ? a.segC[1] : a.segC[0], x ? a.tmm[1] : a.tmm[0],
+                  x ? a.segmm[1] : a.segmm[0]);
+}
+__global__ __launch_bounds__(256) void msd_runs_apply_kernel(const MsdRunsArgs a) {
+    const int x = blockIdx.z;
+    if (x >= a.ntab) return;
+    runs_apply_body(x ? a.offs[1] : a.offs[0], x ? a.ntiles[1] : a.ntiles[0], x ? a.T[1] : a.T[0],
+                    x ? a.TB[1] : a.TB[0], x ? a.segL[1] : a.segL[0], x ? a.segC[1] : a.segC[0],
+                    x ? a.bk[1] : a.bk[0], x ? a.list[1] : a.list[0], x ? a.tinfo[1] : a.tinfo[0]);
 }
 
 // ---------------------------------------------------------------------------
@@ -3510,11 +3526,9 @@ hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_msd_runs_seg(const uint32_t *offs, int64_t ntiles, uint32_t *segL, uint32_t *segC,
-                               const int64_t *tmm, int64_t *segmm, hipStream_t s) {
-    const dim3 grid((kBucketsA + 63) / 64, kMsdSegs);
-    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, offs, ntiles, kOffsARow, kBucketsA, segL, segC, tmm,
-                       segmm);
+hipError_t launch_msd_runs_seg(const MsdRunsArgs &a, hipStream_t s) {
+    const dim3 grid((kBucketsA + 63) / 64, kMsdSegs, a.ntab);
+    hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -3533,12 +3547,10 @@ hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_msd_runs_apply(const uint32_t *offs, int64_t ntiles, int T, int TB, const uint32_t *segL,
-                                 const uint32_t *segC, const MsdBucket *bk, uint2 *list, uint2 *tinfo,
-                                 hipStream_t s) {
+hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s) {
     static_assert(kBucketsA % 4 == 0, "four buckets (waves) per workgroup");
-    const dim3 grid(kBucketsA / 4, kMsdSegs);
-    hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, offs, ntiles, T, TB, segL, segC, bk, list, tinfo);
+    const dim3 grid(kBucketsA / 4, kMsdSegs, a.ntab);
+    hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
