@@ -983,7 +983,9 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     if (redo) {
         SMJ_TRY(compact(1));
         pc = prof_last();
-        HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));  // joined, nbigdev
+    }
+    if (redo || ms->h_plan->nbig) {  // joined (after the redo), the device big-group count
+        HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (t_slot < 0) g_msd_bigdev = ms->h_plan->nbigdev;
     }

@@ -232,6 +232,10 @@ def test_small_span_oversized_groups_on_device(gpu, oracle_built, monkeypatch, k
     np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
     np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    # one table alone (smj_dev_select_sort: the same tiers without a join)
+    gS1 = ops.select_sort(dev(S), kc, *(sel if sel else (0, None)))
+    assert ops.msd_bigdev() > 20, ops.msd_bigdev()
+    np.testing.assert_array_equal(host(gS1), Ss.reshape(-1, 2))
 
 
 @pytest.mark.parametrize("n,cols,kind", [(100_000, 2, "uniform"), (70_000, 3, "dups"), (4097, 2, "wide")])
