@@ -459,7 +459,7 @@ struct MsdScratch {
     int dev = -1;
     MsdTabScratch t[2];
     int64_t *spl = nullptr, *samp = nullptr;
-    MsdGroup *groups = nullptr, *slot_groups = nullptr;
+    MsdGroup *groups = nullptr;
     uint32_t *gpart = nullptr;  // group_sum partials
     uint32_t *cpart = nullptr;  // count_scan chunk sums
     uint32_t *counts = nullptr, *offs = nullptr, *single_list = nullptr, *big_list = nullptr, *ngrp = nullptr,
@@ -510,7 +510,6 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
         HIP_TRY(hipMalloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
         HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
-        HIP_TRY(hipMalloc(&m.slot_groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
         HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * kOffsA));
         HIP_TRY(hipMalloc(&m.cpart, sizeof(uint32_t) * 256));
@@ -539,7 +538,7 @@ void msd_free_all() {
         for (auto &t : m.t)
             for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb, t.fb2})
                 hipFree(p);
-        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.slot_groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                         (void *)m.lspl, m.giant, m.gmap, m.gh})
             hipFree(p);
@@ -910,7 +909,6 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         }
         gp.ntab = ntab;
         gp.part = ms->gpart;
-        gp.slot_groups = ms->slot_groups;
         gp.ngrp = ms->ngrp;
         gp.groups = ms->groups;
         gp.counts = ms->counts;

@@ -307,9 +307,8 @@ struct MsdGroupParams {
     int tile[2];
     int ntab;
     uint32_t *part;         // [2][kBucketsA][kGroupSlices][kRadB] partial sub-bucket totals
-    MsdGroup *slot_groups;  // [kBucketsA][kRadB]: bucket a's groups at slots a * kRadB + j
-    uint32_t *ngrp;         // [kBucketsA] groups per bucket
-    MsdGroup *groups;       // dense, key order (msd_group_pack)
+    uint32_t *ngrp;         // [kBucketsA] groups per bucket | kGrpReady (published for the later buckets)
+    MsdGroup *groups;       // dense, key order
     uint32_t *counts;       // dense: join rows per group (single-key groups: known here)
     MsdPlan *plan;
     uint32_t *single_list, *big_list;  // dense group indices

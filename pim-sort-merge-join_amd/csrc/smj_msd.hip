@@ -1234,14 +1234,16 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
 // ---------------------------------------------------------------------------
 // one workgroup of 1024 threads per bucket a; thread t owns sub-buckets
 // [t*SB, t*SB + SB): per-table sub-bucket totals and prefixes, then greedy
-// packing into groups written to slots a * kRadB + j.  msd_group_pack_kernel
-// then lays them out densely.
+// packing into groups, written densely in key order: bucket a's groups start
+// after the groups of buckets < a, whose counts each workgroup publishes as
+// soon as it has them (a look-back over at most 255 words).
 // grid (kBucketsA, kGroupSlices) x 256: partial sub-bucket totals of a slice
 // of the bucket's pass-B tiles (thread t owns sub-buckets [8t, 8t + 8))
 
 __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams p) {
     constexpr int SB = kRadB / 256;
     const int a = blockIdx.x, sl = blockIdx.y, t = threadIdx.x;
+    if (sl == 0 && t == 0) p.ngrp[a] = 0;  // msd_group_kernel's publication word (previous call: flagged)
     for (int x = 0; x < p.ntab; x++) {
         uint32_t tot[SB];
 #pragma unroll
@@ -1271,6 +1273,7 @@ __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams
 }
 
 constexpr int kGroupThreads = 1024;
+constexpr uint32_t kGrpReady = 0x80000000u;  // ngrp[a]: bucket a's group count is published
 constexpr int kGroupLevels = 11;  // 2^11 = kRadB: binary-lifting levels over the group starts
 static_assert((1 << kGroupLevels) == kRadB, "one level per bit of a group index");
 __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroupParams p) {
@@ -1279,6 +1282,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     __shared__ uint16_t s_lift[kGroupLevels][kRadB + 1];  // f^(2^k): next group start after a start
     __shared__ uint16_t s_nz[kRadB + 1];            // positions of the non-empty sub-buckets, in order
     __shared__ uint16_t s_cnz[kRadB + 1];           // non-empty sub-buckets before position q
+    __shared__ uint32_t s_base;
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];   // groups: sub-buckets [b0, b1)
     __shared__ int s_ng;
@@ -1386,9 +1390,38 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         int ng = 0;
         for (int w = 0; w < NW; w++) ng = max(ng, (int)s_wsum[w]);
         s_ng = ng;
-        p.ngrp[a] = (uint32_t)ng;
+        // publish this bucket's group count (msd_group_sum zeroed the word):
+        // the later buckets add it to their dense base
+        atomicExch(&p.ngrp[a], (uint32_t)ng | kGrpReady);
     }
-    __syncthreads();
+    // dense base = the group counts of buckets < a, as they are published
+    // (workgroups wait only on earlier, already dispatched ones).  Relaxed
+    // atomics: nothing else this kernel writes is read back in it.
+    {
+        uint32_t v = 0;
+        if (t < a) {
+            // bounded (a bug shows as a wrong result in the parity tests, never as a hang)
+            for (uint32_t spin = 0; spin < (1u << 26); spin++) {
+                v = __hip_atomic_load(&p.ngrp[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v & kGrpReady) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            v &= ~kGrpReady;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        __syncthreads();  // s_wsum read out above
+        if ((t & 63) == 0) s_wsum[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t base = 0;
+            for (int w = 0; w < NW; w++) base += s_wsum[w];
+            s_base = base;
+            if (a == kBucketsA - 1) p.plan->ngroups = base + s_ng;
+        }
+        __syncthreads();
+    }
+    const uint32_t base = s_base;
     for (int j = t; j < s_ng; j += kGroupThreads) {
         const uint32_t b0 = s_g0[j], b1 = s_g1[j];
         MsdGroup gr{};
@@ -1424,34 +1457,14 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.base = (int64_t)((uint64_t)p.bk[0][a].lo + (uint64_t)r0);
         const unsigned __int128 sp = r1 - r0;
         gr.span = sp > 0xffffffffu ? 0xffffffffu : (uint32_t)sp;
-        p.slot_groups[(int64_t)a * kRadB + j] = gr;
-    }
-}
-
-// grid kBucketsA x 256: bucket a's groups -> dense (key-ordered) indices
-// base_a + j; join counts of single-key groups; fallback lists
-__global__ __launch_bounds__(256) void msd_group_pack_kernel(const MsdGroupParams p) {
-    __shared__ uint32_t s_base;
-    const int a = blockIdx.x, tid = threadIdx.x;
-    if (tid < 64) {
-        uint32_t v = 0;
-        for (int i = tid; i < a; i += 64) v += p.ngrp[i];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (tid == 0) s_base = v;
-    }
-    __syncthreads();
-    const uint32_t base = s_base, ng = p.ngrp[a];
-    if (a == kBucketsA - 1 && tid == 0) p.plan->ngroups = base + ng;
-    for (uint32_t j = tid; j < ng; j += 256) {
-        const MsdGroup g = p.slot_groups[(int64_t)a * kRadB + j];
-        const uint32_t gi = base + j;
-        p.groups[gi] = g;
+        // dense, key-ordered index; the streamed / oversized lists
+        const uint32_t gi = base + (uint32_t)j;
+        p.groups[gi] = gr;
         uint32_t cnt = 0;
-        if (g.flags == kGroupSingle) {
-            cnt = min(g.nR, g.nS);
+        if (gr.flags == kGroupSingle) {
+            cnt = min(gr.nR, gr.nS);
             p.single_list[atomicAdd(&p.plan->nsingle, 1u)] = gi;
-        } else if (g.flags == kGroupBig) {
+        } else if (gr.flags == kGroupBig) {
             p.big_list[atomicAdd(&p.plan->nbig, 1u)] = gi;
         }
         p.counts[gi] = cnt;
@@ -3595,7 +3608,6 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
     hipLaunchKernelGGL(msd_group_sum_kernel, dim3(kBucketsA, kGroupSlices), dim3(256), 0, s, p);
     hipLaunchKernelGGL(msd_group_kernel, dim3(kBucketsA), dim3(kGroupThreads), 0, s, p);
-    hipLaunchKernelGGL(msd_group_pack_kernel, dim3(kBucketsA), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

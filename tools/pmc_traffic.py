@@ -35,7 +35,6 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_runs_apply_kernel", "msd_runs", False),
     (r"msd_group_kernel", "msd_group", True),
     (r"msd_group_sum_kernel", "msd_group", False),
-    (r"msd_group_pack_kernel", "msd_group", False),
     (r"msd_sample_kernel", "msd_sample", True),
     (r"msd_count_scan_kernel", "msd_count_scan", True),
     (r"msd_compact_kernel", "msd_compact", True),
