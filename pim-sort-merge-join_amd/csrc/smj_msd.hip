@@ -2827,10 +2827,13 @@ constexpr int kBgIt = kGroupCap / kMsdThreads;  // chunk rows per thread
 #endif
 constexpr uint32_t kBgLarge = 8 * kGroupCap;  // groups over this many rows (either table) are dealt first
 static_assert(kBgSeg % kGroupCap == 0 && kStRange % (4 * kMsdThreads) == 0, "giant jobs: whole chunks, uint4 counts");
-struct BgSmem {
+struct BgSmem {                 // 48.5 KiB: three workgroups per CU
     uint32_t end[2][kStRange];   // per residual: row count, then the running start of its output rows
-    uint32_t jst[kStRange + 1];  // exclusive prefix over residuals of min(countR, countS) (join rows)
-    uint2 list[2][kGroupCap];    // per table: {tempB row, group row} of each pass-B tile's run
+    union {
+        uint2 list[2][kGroupCap];    // per table: {tempB row, group row} of each pass-B tile's run
+        uint32_t jst[kStRange + 1];  // once the rows are placed: the exclusive prefix over residuals of
+                                     // min(countR, countS) (join rows)
+    };
     uint32_t nl[2];              // runs per table
     uint32_t wsum[kMsdWaves];
     uint32_t ticket;
@@ -3005,7 +3008,7 @@ __device__ __forceinline__ void bg_join(const MsdFinalParams &p, const MsdGroup 
 // per-residual counts c[x][r] in sm.end -> exclusive output starts, and
 // min(cR, cS) -> the join-row prefix jst (jst[kStRange] = the join rows);
 // returns the join rows.  Ends with a barrier.
-__device__ __forceinline__ uint32_t bg_starts(BgSmem &sm, bool join) {
+__device__ __forceinline__ uint32_t bg_starts(BgSmem &sm, bool join, bool with_jst) {
     constexpr int RP = kStRange / kMsdThreads;
     const int tid = threadIdx.x;
     uint32_t c[3][RP], sum[3] = {0, 0, 0};
@@ -3026,16 +3029,43 @@ __device__ __forceinline__ uint32_t bg_starts(BgSmem &sm, bool join) {
         const int r = tid * RP + j;
         sm.end[0][r] = ex[0];
         sm.end[1][r] = ex[1];
-        sm.jst[r] = ex[2];
+        if (with_jst) sm.jst[r] = ex[2];
 #pragma unroll
         for (int q = 0; q < 3; q++) ex[q] += c[q][j];
     }
-    if (tid == 0) sm.jst[kStRange] = tot[2];
+    if (tid == 0 && with_jst) sm.jst[kStRange] = tot[2];
     __syncthreads();
     return tot[2];
 }
 
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const MsdFinalParams p) {
+// after the rows are placed (sm.end = the end of each residual's rows): the
+// join-row prefix jst, into the run lists' (now idle) region.  Ends with a barrier.
+__device__ __forceinline__ void bg_jst_from_ends(BgSmem &sm) {
+    constexpr int RP = kStRange / kMsdThreads;
+    const int tid = threadIdx.x;
+    uint32_t c[RP], sum = 0;
+    uint32_t pR = tid ? sm.end[0][tid * RP - 1] : 0u, pS = tid ? sm.end[1][tid * RP - 1] : 0u;
+#pragma unroll
+    for (int j = 0; j < RP; j++) {
+        const int r = tid * RP + j;
+        const uint32_t eR = sm.end[0][r], eS = sm.end[1][r];
+        c[j] = min(eR - pR, eS - pS);
+        pR = eR;
+        pS = eS;
+        sum += c[j];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan<kMsdWaves>(sum, sm.wsum, &tot);  // (its barriers: the run lists are dead)
+#pragma unroll
+    for (int j = 0; j < RP; j++) {
+        sm.jst[tid * RP + j] = ex;
+        ex += c[j];
+    }
+    if (tid == 0) sm.jst[kStRange] = tot;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kMsdThreads, 3) void msd_big_stage_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
     const uint32_t nbig = p.plan->nbig;
     const int tid = threadIdx.x;
@@ -3072,7 +3102,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
             if (p.ntab > 1) bg_count<1>(p, g, 0, g.nS, sm, sm.end[1]);
         }
         __syncthreads();
-        const uint32_t J = bg_starts(sm, join);
+        const uint32_t J = bg_starts(sm, join, false);
         if (tid == 0) {
             p.counts[gi] = J;
             atomicAdd(&p.plan->nbigdev, 1u);
@@ -3087,6 +3117,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
             // writes back the XCD's whole L2 on gfx950 -- 20 of C5's ms.)
             __threadfence_block();
             __syncthreads();
+            bg_jst_from_ends(sm);
             bg_join(p, g, 0, J, sm, true);
         }
     }
@@ -3165,7 +3196,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const
         const MsdGroup g = p.groups[jb.gi];
         uint32_t pre[2][RP];
         giant_totals(p, jb, sm, pre);
-        bg_starts(sm, join);
+        bg_starts(sm, join, false);
 #pragma unroll
         for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -3188,7 +3219,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_join_kernel(const Ms
         const MsdGroup g = p.groups[jb.gi];
         uint32_t pre[2][RP];
         giant_totals(p, jb, sm, pre);
-        const uint32_t J = bg_starts(sm, join);  // sm.end = the starts
+        const uint32_t J = bg_starts(sm, join, true);  // sm.end = the starts
         if (jb.s == 0 && threadIdx.x == 0) {
             p.counts[jb.gi] = J;
             atomicAdd(&p.plan->nbigdev, 1u);
