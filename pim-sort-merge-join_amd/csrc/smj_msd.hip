@@ -2925,13 +2925,14 @@ __device__ __forceinline__ void bg_lists(const MsdFinalParams &p, const MsdGroup
 template <int X>
 __device__ __forceinline__ void bg_count(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
                                          BgSmem &sm, uint32_t *cnt) {
+    constexpr int U = 4 * kBgIt;  // rows per thread in flight (four chunks): the pass is latency-bound
     const MsdTab &tb = p.tab[X];
     const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
     const int tid = threadIdx.x;
-    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
-        int64_t k[kBgIt];
+    for (uint32_t c0 = v0; c0 < v1; c0 += U * kMsdThreads) {
+        int64_t k[U];
 #pragma unroll
-        for (int i = 0; i < kBgIt; i++) {
+        for (int i = 0; i < U; i++) {
             const uint32_t v = c0 + tid + i * kMsdThreads;
             k[i] = 0;
             if (v < v1) {
@@ -2940,7 +2941,7 @@ __device__ __forceinline__ void bg_count(const MsdFinalParams &p, const MsdGroup
             }
         }
 #pragma unroll
-        for (int i = 0; i < kBgIt; i++)
+        for (int i = 0; i < U; i++)
             if (c0 + tid + i * kMsdThreads < v1) atomicAdd(&cnt[(uint32_t)((uint64_t)k[i] - (uint64_t)g.base)], 1u);
     }
 }
@@ -2955,20 +2956,31 @@ __device__ __forceinline__ void bg_scatter(const MsdFinalParams &p, const MsdGro
     const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
     i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (X ? g.outS : g.outR);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
-        i64x2 rows[kBgIt];
-        uint32_t dig[kBgIt], vmask = 0;
+    // the chunk's rows of this thread (input order: wave, item, lane)
+    auto load = [&](uint32_t c0, i64x2 (&rows)[kBgIt], uint32_t &vm) {
+        vm = 0;
 #pragma unroll
         for (int i = 0; i < kBgIt; i++) {
             const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
             rows[i] = i64x2{0, 0};
-            dig[i] = 0;
             if (v < v1) {
                 rows[i] = tB[bg_src(sm.list[X], sm.nl[X], v)];
-                dig[i] = (uint32_t)((uint64_t)(tb.key ? rows[i].y : rows[i].x) - (uint64_t)g.base);
-                vmask |= 1u << i;
+                vm |= 1u << i;
             }
         }
+    };
+    i64x2 cur[kBgIt];
+    uint32_t vmask;
+    load(v0, cur, vmask);
+    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
+        // the next chunk's rows are in flight while this one is ranked and stored
+        i64x2 nxt[kBgIt];
+        uint32_t vnext = 0;
+        if (c0 + kGroupCap < v1) load(c0 + kGroupCap, nxt, vnext);
+        uint32_t dig[kBgIt];
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++)
+            dig[i] = ((vmask >> i) & 1u) ? (uint32_t)((uint64_t)(tb.key ? cur[i].y : cur[i].x) - (uint64_t)g.base) : 0u;
         uint32_t pos[kBgIt];
         for (int w = 0; w < kMsdWaves; w++) {
             if (wave == w) bg_rank<kBgIt, 12>(dig, vmask, sm.end[X], lane, pos);
@@ -2976,7 +2988,10 @@ __device__ __forceinline__ void bg_scatter(const MsdFinalParams &p, const MsdGro
         }
 #pragma unroll
         for (int i = 0; i < kBgIt; i++)  // plain stores: a join read-back goes through L1
-            if ((vmask >> i) & 1u) dst[pos[i]] = rows[i];
+            if ((vmask >> i) & 1u) dst[pos[i]] = cur[i];
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) cur[i] = nxt[i];
+        vmask = vnext;
     }
 }
 
