@@ -27,6 +27,23 @@ __device__ __forceinline__ void load_row(const int64_t *__restrict__ p, int64_t 
     }
 }
 
+// load_row with nontemporal (streaming) loads
+template <int COLS>
+__device__ __forceinline__ void load_row_nt(const int64_t *__restrict__ p, int64_t (&r)[COLS]) {
+    if constexpr (COLS % 2 == 0) {
+        const i64x2 *q = reinterpret_cast<const i64x2 *>(p);
+#pragma unroll
+        for (int c = 0; c < COLS / 2; c++) {
+            const i64x2 t = __builtin_nontemporal_load(q + c);
+            r[2 * c] = t.x;
+            r[2 * c + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < COLS; c++) r[c] = __builtin_nontemporal_load(p + c);
+    }
+}
+
 // store_row with nontemporal (streaming) stores: for tiles written once and
 // read back only by a later pass, after gigabytes of other traffic
 template <int COLS>

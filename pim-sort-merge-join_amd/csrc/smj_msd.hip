@@ -287,6 +287,12 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 // ---------------------------------------------------------------------------
 // part_a: select + stable tile-local partition by pass-A bucket
 // ---------------------------------------------------------------------------
+#ifndef SMJ_PA_NTLOAD
+#define SMJ_PA_NTLOAD 0  // A/B switch: part_a's input rows through nontemporal loads
+#endif
+#ifndef SMJ_PB_NTLOAD
+#define SMJ_PB_NTLOAD 0  // A/B switch: the pipelined part_b's gathers through nontemporal loads
+#endif
 template <int COLS>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPartA2 q) {
     // one launch may cover both tables (the same column count): blocks past
@@ -315,7 +321,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     int64_t rows[ITEMS][COLS];
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
-        load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
     __syncthreads();  // splitters
 
     uint32_t dig[ITEMS];
@@ -984,7 +991,8 @@ __device__ __forceinline__ void pb_gather(const MsdPartBParams &p, const MsdBuck
 #pragma unroll
             for (int c = 0; c < COLS; c++) rows[it][c] = bk.lo + (int64_t)((v0 + r) * 7u % (bk.L + 1u));
         } else {
-            load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
+            if (SMJ_PB_NTLOAD) load_row_nt<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
+            else load_row<COLS>(p.srcA + (int64_t)(e.x + (v0 + r - e.y)) * COLS, rows[it]);
         }
     }
 }
