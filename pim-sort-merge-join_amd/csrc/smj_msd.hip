@@ -974,6 +974,9 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 #ifndef SMJ_PB_NOSTORE
 #define SMJ_PB_NOSTORE 0
 #endif
+#ifndef SMJ_PB_ONEKEY
+#define SMJ_PB_ONEKEY 1  // heavy-key buckets skip the tile's counting and ranking
+#endif
 
 // row -> run lookups of a tile (run list lst, start bitmap bm, 64-row block
 // table bt) and the row gathers into registers
@@ -1108,7 +1111,12 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
-        {
+        // a heavy key's own bucket (one key value): every row falls in
+        // sub-bucket 0 and the tile's gather order is already its stable
+        // order -- no counting atomics (all on one LDS word) and no ranking
+        // (cmax > kPbFastMax would take the slow wave-by-wave path)
+        const bool one_key = SMJ_PB_ONEKEY && b.one_key != 0u;  // block-uniform (SMEM)
+        if (!one_key) {
             const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
@@ -1116,6 +1124,8 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                     const uint32_t d = dig[it];
                     dig[it] = d | (((atomicAdd(&s_q[qrow + d], 1u << qsh) >> qsh) & 0xffffu) << 16);
                 }
+        } else if (tid == 0) {
+            s_q[0] = (uint32_t)nrows;  // quad 0, sub-bucket 0: the whole tile (the offsB scan below)
         }
         const bool more = gn < ntl;
         const int Jn = more ? (int)runs_of(tn, bn, gn) : 0;
@@ -1152,7 +1162,10 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         }
         __syncthreads();
         const bool slow = s_slow != 0;
-        if (!slow) {
+        if (one_key) {
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) dig[it] = (uint32_t)(lrow0 + it * 64);  // identity (valid rows)
+        } else if (!slow) {
             const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
 #pragma unroll
             for (int it = 0; it < ITEMS; it++)
