@@ -716,6 +716,13 @@ __device__ __forceinline__ int opaque_tid() {
 }
 
 constexpr int kPbFastMax = 16;  // longest sub-bucket run of a tile the atomic-rank path orders
+// the same limit in msd_part_b_pipe_kernel (per quad of waves): runs up to
+// 128 rows are still cheaper ranked by the scan than by the wave-by-wave
+// ballot path (C5's Zipf tiles: part_b 13.8 -> 12.9 ms at 128, 13.9 at 256,
+// 22.5 at 1024; C3 unchanged -- profiles/r02bu, r02bv)
+#ifndef SMJ_PB_FASTMAX
+#define SMJ_PB_FASTMAX 128
+#endif
 
 template <int COLS>
 __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4) void msd_part_b_kernel(
@@ -1114,7 +1121,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // a heavy key's own bucket (one key value): every row falls in
         // sub-bucket 0 and the tile's gather order is already its stable
         // order -- no counting atomics (all on one LDS word) and no ranking
-        // (cmax > kPbFastMax would take the slow wave-by-wave path)
+        // (cmax > SMJ_PB_FASTMAX would take the slow wave-by-wave path)
         const bool one_key = SMJ_PB_ONEKEY && b.one_key != 0u;  // block-uniform (SMEM)
         if (!one_key) {
             const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
@@ -1142,7 +1149,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                     sum += (w & 0xffffu) + (w >> 16);
                     cmax = max(cmax, max(w & 0xffffu, w >> 16));
                 }
-            if (cmax > (uint32_t)kPbFastMax || (p.dbg & 16)) s_slow = 1;
+            if (cmax > (uint32_t)SMJ_PB_FASTMAX || (p.dbg & 16)) s_slow = 1;
             uint32_t tot;
             uint32_t st = block_excl_scan_nb<NW>(sum, s_wsum, &tot);  // + barrier
             uint32_t sw = 0;
