@@ -1771,6 +1771,9 @@ static_assert(kGroupCap == (1 << kFinIdxBits), "sort word = residual << 10 | gro
 
 constexpr int kCountRange = 4096;  // counting-sort residual range (packed u16 bins)
 constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re-orders
+#ifndef SMJ_ST_MAXRUN
+#define SMJ_ST_MAXRUN kMaxDupRun  // the staged kernel: longer runs take the in-LDS LSD (<= kMaxDupRun)
+#endif
 
 struct FinSmem {
     uint32_t key[2][kGroupCap];   // sort words, sorted in place (via tmp)
@@ -2565,7 +2568,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     const uint32_t fl = sm.flag[wsb];
     wsb ^= 1;
     ST_SUB(1);
-    const bool lsd = fl > (uint32_t)kMaxDupRun;  // block-uniform
+    const bool lsd = fl > (uint32_t)SMJ_ST_MAXRUN;  // block-uniform
     if (lsd && tid == 0) atomicAdd(&p.plan->nlsd, 1u);
 #pragma unroll
     for (int x = 0; x < 2; x++) {
