@@ -65,21 +65,23 @@ struct ProfRec {
     const char *name;
     hipEvent_t a, b;
     double bytes;
+    int dev;  // the device the events were created on (the pool they return to)
 };
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
-std::vector<hipEvent_t> g_event_pool;
+std::map<int, std::vector<hipEvent_t>> g_event_pool;  // per device: an event records only on its own device's streams
 std::mutex g_mu;  // scratch maps and profiler records (the host API drives devices from worker threads)
 thread_local int t_slot = -1;  // smj::set_scratch_slot
 
-hipEvent_t take_event() {
-    if (!g_event_pool.empty()) {
-        hipEvent_t e = g_event_pool.back();
-        g_event_pool.pop_back();
+hipEvent_t take_event(int dev) {
+    std::vector<hipEvent_t> &pool = g_event_pool[dev];
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
         return e;
     }
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;  // on the calling thread's current device = dev
     return e;
 }
 
@@ -91,16 +93,20 @@ struct ProfScope {
         if (!on) return;
         rec.name = name;
         rec.bytes = bytes;
+        if (hipGetDevice(&rec.dev) != hipSuccess) {
+            on = false;
+            return;
+        }
         {
             std::lock_guard<std::mutex> lk(g_mu);
-            rec.a = take_event();
-            rec.b = take_event();
+            rec.a = take_event(rec.dev);
+            rec.b = take_event(rec.dev);
         }
-        if (rec.a) hipEventRecord(rec.a, s);
+        if (rec.a && hipEventRecord(rec.a, s) != hipSuccess) on = false;
     }
     ~ProfScope() {
         if (!on || !rec.a || !rec.b) return;
-        hipEventRecord(rec.b, s);
+        if (hipEventRecord(rec.b, s) != hipSuccess) return;  // a missing record is dropped, never misread
         std::lock_guard<std::mutex> lk(g_mu);
         g_prof.push_back(rec);
     }
@@ -157,8 +163,8 @@ extern "C" int smj_prof_report(char *buf, size_t buflen) {
     if (!buf || buflen < out.size() + 1) return (int)out.size() + 1;
     memcpy(buf, out.c_str(), out.size() + 1);
     for (auto &r : g_prof) {
-        g_event_pool.push_back(r.a);
-        g_event_pool.push_back(r.b);
+        g_event_pool[r.dev].push_back(r.a);
+        g_event_pool[r.dev].push_back(r.b);
     }
     g_prof.clear();
     return SMJ_OK;
@@ -361,7 +367,6 @@ extern "C" int smj_dev_select(const T *in, int64_t n, int cols, int sel_col, T s
     Counters c;
     HIP_TRY(hipMemcpyAsync(&c, &sc->ctr[1], sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (c.err) return SMJ_ERR_TIMEOUT;
     *out_rows = c.count;
     return SMJ_OK;
 }
@@ -602,8 +607,28 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
     // launched here where the plan shows some; the rest on the host path below
     const bool two = in[0].cols == 2 && (ntab == 1 || in[1].cols == 2);
     if (pl.nbig && two) {
+        // the job split's buffers (msd_giant_*), sized from this call's
+        // oversized groups: a group over bg_max rows per table becomes
+        // ceil(rows / seg) jobs with 2 x kStageRange residual counts each
+        const MsdBgLimits bl = msd_bg_limits();
+        int64_t ngiant = 0, njobs = 0;
+        for (uint32_t slot : bigs) {
+            const MsdGroup &g = groups[slot];
+            const uint32_t m = std::max(g.nR, ntab > 1 ? g.nS : 0u);
+            if (std::max(g.nR, g.nS) > bl.max_rows) {
+                ngiant++;
+                njobs += (m + bl.seg - 1) / bl.seg;
+            }
+        }
+        SMJ_TRY(grow(&ms->giant, &ms->c_giant, (size_t)(ngiant + 1) * sizeof(uint4)));
+        SMJ_TRY(grow(&ms->gmap, &ms->c_gmap, (size_t)(njobs + 1) * 4));
+        SMJ_TRY(grow(&ms->gh, &ms->c_gh, (size_t)(njobs + 1) * 2 * kStageRange * 4));
+        MsdFinalParams fb = fp;
+        fb.giant = (uint4 *)ms->giant;
+        fb.gmap = (uint32_t *)ms->gmap;
+        fb.gh = (uint32_t *)ms->gh;
         ProfScope ps("msd_big_dev", 0, s);
-        HIP_TRY(launch_msd_big(fp, s));
+        HIP_TRY(launch_msd_big(fb, s));
     }
     std::vector<uint32_t> host_bigs;
     for (uint32_t slot : bigs) {
@@ -770,13 +795,6 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
     if (join) SMJ_TRY(grow(&ms->slots, &ms->c_slots, std::max<size_t>(1, in[0].n) * tc * 8));
-    {  // oversized groups split into jobs (msd_giant_*): their worst-case count for this call
-        const MsdBgLimits bl = msd_bg_limits();
-        const int64_t rows_all = in[0].n + (ntab > 1 ? in[1].n : 0), jobs = msd_giant_jobs_max(rows_all, bl);
-        SMJ_TRY(grow(&ms->giant, &ms->c_giant, (size_t)(rows_all / bl.max_rows + 2) * sizeof(uint4)));
-        SMJ_TRY(grow(&ms->gmap, &ms->c_gmap, (size_t)jobs * 4));
-        SMJ_TRY(grow(&ms->gh, &ms->c_gh, (size_t)jobs * 2 * kStageRange * 4));
-    }
     HIP_TRY(hipMemsetAsync(ms->plan, 0, sizeof(MsdPlan), s));
     auto segL = [&](int x) { return (uint32_t *)ms->t[x].seg; };
     auto segC = [&](int x) { return (uint32_t *)ms->t[x].seg + kMsdSegs * kOffsA; };
@@ -929,9 +947,9 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.big_list = ms->big_list;
     fp.wide_list = ms->wide_list;
     fp.radix_list = ms->radix_list;
-    fp.giant = (uint4 *)ms->giant;
-    fp.gmap = (uint32_t *)ms->gmap;
-    fp.gh = (uint32_t *)ms->gh;
+    fp.giant = nullptr;  // the job split's buffers: sized and set by msd_fallback
+    fp.gmap = nullptr;
+    fp.gh = nullptr;
     const MsdBgLimits bl = msd_bg_limits();
     fp.bg_max = bl.max_rows;
     fp.bg_seg = bl.seg;
@@ -965,6 +983,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (ms->h_plan->err) return SMJ_ERR_TIMEOUT;
     if (t_slot < 0) {
         g_msd_stats[0] = ms->h_plan->nsingle;
         g_msd_stats[1] = ms->h_plan->nbig;
@@ -1656,7 +1675,8 @@ void smj::api_free_all() {
     msd_free_all();
     idx_free_all();
     typed_free_all();
-    for (auto e : g_event_pool) hipEventDestroy(e);
+    for (auto &kv : g_event_pool)
+        for (auto e : kv.second) hipEventDestroy(e);
     g_event_pool.clear();
 }
 

@@ -104,23 +104,6 @@ __device__ __forceinline__ void st_status(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Poll one look-back status word until a predecessor has published it.
-// Bounded: after ~2^22 polls (seconds) the wait gives up, flags the error
-// word and returns an inclusive 0 so that the grid always drains.
-__device__ __forceinline__ uint32_t spin_status(const uint32_t *p, uint32_t *err) {
-    uint32_t w = ld_status(p);
-    uint32_t spins = 0;
-    while ((w & (kFlagAgg | kFlagInc)) == 0) {
-        __builtin_amdgcn_s_sleep(1);
-        w = ld_status(p);
-        if (++spins > (1u << 22)) {
-            atomicOr(err, 1u);
-            return kFlagInc;
-        }
-    }
-    return w;
-}
-
 // Inclusive wave64 scan on DPP (row_shr 1/2/4/8 inside each row of 16
 // lanes, then row_bcast:15 / row_bcast:31 across rows): VALU-only, no LDS
 // permutes.  `lane` is unused; kept for call-site symmetry.

@@ -60,17 +60,15 @@ struct SortPlan {
     uint32_t m;          // rows that passed the select
     int32_t npasses;     // radix passes to run (>= 1 when m > 0)
     int32_t pos[8];      // digit position (0..kNumPos-1) of pass k
-    uint32_t err;        // set by kernels when a look-back wait timed out
-    uint32_t pad;
+    uint32_t pad[2];
 };
 
 // Device scratch counters.  {tile, count} are zeroed before every launch
-// (8-byte memset); err is sticky for the whole API call.
+// (8-byte memset).
 struct Counters {
     uint32_t tile;       // dynamic tile id
     uint32_t count;      // rows emitted (select-only passes)
-    uint32_t err;        // look-back wait timed out
-    uint32_t pad;
+    uint32_t pad[2];
 };
 
 // ---- launchers (smj_kernels.hip) ------------------------------------------
@@ -198,10 +196,6 @@ struct MsdBgLimits {
     uint32_t max_rows, seg;
 };
 MsdBgLimits msd_bg_limits();
-// jobs the giant groups of tables of `rows` rows in all can need
-inline int64_t msd_giant_jobs_max(int64_t rows, const MsdBgLimits &l) {
-    return rows / l.seg + rows / (int64_t)l.max_rows + 2;
-}
 constexpr int kSlots = kBucketsA * kRadB;  // group slots (bucket-major = key order); groups <= kSlots
 constexpr int kFinThreads = 256;           // final kernel workgroup (4 per CU)
 constexpr int kFinWaves = kFinThreads / 64;
@@ -268,6 +262,7 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t bgticket[2];// msd_big_stage_kernel's group tickets (large groups first, then the rest)
     uint32_t ngiant;     // groups over kBgMaxRows rows registered as jobs
     uint32_t njobs;      // their jobs
+    uint32_t err;        // != 0: a cross-workgroup wait gave up (msd_group_kernel) -> SMJ_ERR_TIMEOUT
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)

@@ -1428,12 +1428,16 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     {
         uint32_t v = 0;
         if (t < a) {
-            // bounded (a bug shows as a wrong result in the parity tests, never as a hang)
-            for (uint32_t spin = 0; spin < (1u << 26); spin++) {
+            // bounded, so the grid always drains: on exhaustion the plan's error
+            // word is set and msd_run returns SMJ_ERR_TIMEOUT instead of a join
+            // built on a wrong dense base
+            uint32_t spin = 0;
+            for (; spin < (1u << 26); spin++) {
                 v = __hip_atomic_load(&p.ngrp[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v & kGrpReady) break;
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (!(v & kGrpReady)) atomicOr(&p.plan->err, 1u);
             v &= ~kGrpReady;
         }
 #pragma unroll

@@ -275,7 +275,9 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     k1, k2 = keys
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    loopback = LOOPBACK if loopback is None else loopback
+    # loopback needs a process group (a one-rank RCCL group sending to itself);
+    # without one the single-rank call is the local pipeline
+    loopback = (LOOPBACK if loopback is None else loopback) and dist.is_initialized()
     if world == 1 and not loopback:
         return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)

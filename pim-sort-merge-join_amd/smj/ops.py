@@ -178,7 +178,7 @@ def msd_groups():
 
 def force_parts(parts=0):
     """Diagnostic: run every pipeline call in the partitioned mode with `parts`
-    key-range parts (0 = automatic: only tables over 2^28 rows are split)."""
+    key-range parts (0 = automatic: only tables over 1.6e8 rows are split, kMsdSingleMax)."""
     _lib.load().smj_debug_force_parts(int(parts))
 
 
