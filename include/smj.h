@@ -214,6 +214,24 @@ int smj_dev_partition(const int64_t *in, int64_t n_rows, int col_num, int use_se
                       int64_t select_val, int key_col, const int64_t *d_splitters, int n_split, int64_t *out,
                       int64_t *h_counts, void *stream);
 
+/* The same partition split for a distributed driver that must not stall
+ * the stream (smj/dist.py): splitters are HOST values, nothing synchronises.
+ * smj_dev_partition_plan counts the selected rows per (chunk, bucket) into
+ * d_plan (smj_partition_plan_bytes(n_rows, col_num, n_split) bytes of device
+ * memory, caller-owned) and turns them into absolute stable output starts;
+ * the n_split + 1 bucket counts land in d_counts (DEVICE int64).
+ * smj_dev_partition_apply then writes the bucket-contiguous copy from that
+ * plan (same table, splitters and select).  A plan outlives other calls, so
+ * a caller can count every table first, exchange the counts, and scatter
+ * later without reading a table a third time. */
+size_t smj_partition_plan_bytes(int64_t n_rows, int col_num, int n_split);
+int smj_dev_partition_plan(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                           int64_t select_val, int key_col, const int64_t *h_splitters, int n_split, void *d_plan,
+                           int64_t *d_counts, void *stream);
+int smj_dev_partition_apply(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                            int64_t select_val, int key_col, const int64_t *h_splitters, int n_split,
+                            const void *d_plan, int64_t *out, void *stream);
+
 /* Synthetic 2-column table (key, payload) for rows [row0, row0 + rows):
  * key = 1 + floor(splitmix64(g + seed * 0xD1B54A32D192ED03) * key_range / 2^64),
  * payload = g (the global row index).  Identical to the oracle's
@@ -301,6 +319,10 @@ void smj_debug_msd_tiers(int64_t *out4);
 /* Run every pipeline call in the partitioned mode with `parts` key-range
  * parts (tests); 0 = automatic (tables over 1.6e8 rows). */
 void smj_debug_force_parts(int parts);
+/* Rows (R + S, after the WHERE clause) each device of the set received in
+ * the last sharded call (load balance); returns the device count, writes at
+ * most `max` entries. */
+int smj_debug_shard_rows(int64_t *out, int max);
 
 /* ---- profiling ---------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by hipEvents recorded on

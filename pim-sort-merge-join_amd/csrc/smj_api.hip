@@ -598,7 +598,13 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         }
         SMJ_TRY(grow(&ms->work, &ms->c_work, work.size() * sizeof(uint2)));
         HIP_TRY(hipMemcpyAsync(ms->work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
-        ProfScope ps("msd_single", 0, s);
+        double b = 0;  // rows read + written once, join rows min(nR, nS) (single key: all pair up)
+        for (uint32_t slot : singles) {
+            const MsdGroup &g = groups[slot];
+            b += 2.0 * 8.0 * ((double)g.nR * in[0].cols + (ntab > 1 ? (double)g.nS * in[1].cols : 0.0));
+            if (join) b += 8.0 * (in[0].cols + in[1].cols - 1) * (double)std::min(g.nR, g.nS);
+        }
+        ProfScope ps("msd_single", b, s);
         HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
         HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
     }
@@ -627,8 +633,28 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         fb.giant = (uint4 *)ms->giant;
         fb.gmap = (uint32_t *)ms->gmap;
         fb.gh = (uint32_t *)ms->gh;
-        ProfScope ps("msd_big_dev", 0, s);
-        HIP_TRY(launch_msd_big(fb, s));
+        {
+            ProfScope ps("msd_big_dev", 0, s);
+            HIP_TRY(launch_msd_big(fb, s));
+        }
+        if (g_prof_on) {
+            // algorithmic bytes of the device tiers: every row of
+            // the groups they sort read and written once, plus the join rows
+            // they write (the groups' counts, read back: profiling steps only)
+            const size_t pi = prof_last();
+            std::vector<uint32_t> cnt(std::max<uint32_t>(pl.ngroups, 1));
+            HIP_TRY(hipMemcpyAsync(cnt.data(), ms->counts, 4 * (size_t)pl.ngroups, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            const int tcb = join ? in[0].cols + in[1].cols - 1 : 0;
+            double b = 0;
+            for (uint32_t slot : bigs) {
+                const MsdGroup &g = groups[slot];
+                if (!msd_big_on_device(g.span, g.kt[0], g.kt[1])) continue;
+                b += 2.0 * 8.0 * ((double)g.nR * in[0].cols + (ntab > 1 ? (double)g.nS * in[1].cols : 0.0));
+                b += 8.0 * tcb * (double)cnt[slot];
+            }
+            prof_set_bytes(pi, b);
+        }
     }
     std::vector<uint32_t> host_bigs;
     for (uint32_t slot : bigs) {
@@ -1374,14 +1400,17 @@ int smj::msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int s
                                     const int64_t *hS, int64_t ns, int c2, int sc2, int64_t sv2, int key2, int64_t *dR,
                                     int64_t *dS, int64_t *dRs, int64_t *dSs, int64_t *dJ, int64_t *h_rows,
                                     hipStream_t s, hipStream_t copy, hipEvent_t landed) {
+    const int64_t lcm = 4 * 5 * 3 * 7 * 8192;  // every pass-A tile (msd_tile: 512 x {16, 8, 5, 4, 3, 2} rows) divides it
+    const int64_t chunk = lcm * std::max<int64_t>(1, (int64_t)(1 << 22) / lcm);
+    // tables that fit one chunk gain nothing from staging (one copy each is
+    // faster: tools/h2d_overlap.py, 1e6 rows 0.96 vs 1.36 ms)
     if (c1 > kDirectCols || c2 > kDirectCols || nr == 0 || ns == 0 || nr > kMsdSingleMax || ns > kMsdSingleMax ||
-        g_force_parts > 0)
+        g_force_parts > 0 || std::max(nr, ns) <= chunk)
         return SMJ_ERR_UNSUPPORTED;
     SMJ_TRY(check_table(nr, c1, sc1, key1));
     SMJ_TRY(check_table(ns, c2, sc2, key2));
     const MsdIn t[2] = {{dR, nr, c1, 1, sc1, key1, sv1, dRs}, {dS, ns, c2, 1, sc2, key2, sv2, dSs}};
-    const int64_t lcm = 4 * 5 * 3 * 7 * 8192;  // every pass-A tile (msd_tile: 512 x {16, 8, 5, 4, 3, 2} rows) divides it
-    const MsdStage stg{{hR, hS}, copy, lcm * std::max<int64_t>(1, (int64_t)(1 << 22) / lcm), landed};
+    const MsdStage stg{{hR, hS}, copy, chunk, landed};
     return msd_run(t, 2, 1, key2, dJ, h_rows, s, &stg);
 }
 
@@ -1621,6 +1650,87 @@ extern "C" int smj_dev_partition(const T *in, int64_t n, int cols, int use_selec
     HIP_TRY(hipMemcpyAsync(sc->h_small, d_cnt, sizeof(int64_t) * (n_split + 1), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     for (int b = 0; b <= n_split; b++) h_counts[b] = sc->h_small[b];
+    return SMJ_OK;
+}
+
+// the plan / apply split (smj.h): host splitters, device counts, no stream sync
+namespace {
+int partition_spec(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val, int key_col,
+                   const T *h_spl, int n_split, PassSpec &ps) {
+    SMJ_TRY(check_table(n, cols, use_select ? sel_col : 0, key_col));
+    SMJ_TRY(direct_only(cols));
+    if (n_split < 0 || n_split > kMaxSplitters || (n_split && !h_spl)) return SMJ_ERR_INVALID;
+    for (int i = 1; i < n_split; i++)
+        if (h_spl[i] < h_spl[i - 1]) return SMJ_ERR_INVALID;  // the bucket search needs sorted splitters
+    ps = PassSpec{};
+    ps.src = in;
+    ps.nsrc = n;
+    ps.cols = cols;
+    ps.use_select = use_select;
+    ps.sel_col = sel_col;
+    ps.key_col = key_col;
+    ps.sel_val = sel_val;
+    ps.kind = DIGIT_BUCKET;
+    ps.spl = h_spl;
+    ps.nspl = n_split;
+    return SMJ_OK;
+}
+}  // namespace
+
+extern "C" size_t smj_partition_plan_bytes(int64_t n, int cols, int n_split) {
+    if (n < 0 || cols < 1 || cols > kDirectCols || n_split < 0 || n_split > kMaxSplitters) return 0;
+    PassSpec ps{};
+    ps.nsrc = std::max<int64_t>(n, 1);
+    ps.cols = cols;
+    ps.kind = DIGIT_BUCKET;
+    ps.nspl = n_split;
+    return (size_t)pass_chunks(ps) * pass_radix(ps) * sizeof(uint32_t);
+}
+
+extern "C" int smj_dev_partition_plan(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                                      int key_col, const T *h_spl, int n_split, void *d_plan, int64_t *d_counts,
+                                      void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    PassSpec ps;
+    SMJ_TRY(partition_spec(in, n, cols, use_select, sel_col, sel_val, key_col, h_spl, n_split, ps));
+    if (!d_counts || (n && (!in || !d_plan))) return SMJ_ERR_INVALID;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * (n_split + 1), s));
+        return SMJ_OK;
+    }
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    ps.trash = sc->trash;
+    uint32_t *table = (uint32_t *)d_plan;
+    uint32_t *d_base = (uint32_t *)sc->dcount;                            // [64] u32
+    unsigned long long *d_cnt = (unsigned long long *)(sc->dcount + 64);  // [64] u64
+    {
+        ProfScope p1("partition_hist", 8.0 * cols * n, s);
+        HIP_TRY(launch_chunk_hist(ps, table, s));
+    }
+    {
+        ProfScope p2("partition_scan", 0, s);
+        HIP_TRY(launch_chunk_scan_dev(ps, table, sc->segsum, d_base, d_cnt, s));
+    }
+    HIP_TRY(hipMemcpyAsync(d_counts, d_cnt, sizeof(int64_t) * (n_split + 1), hipMemcpyDeviceToDevice, s));
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_partition_apply(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                                       int key_col, const T *h_spl, int n_split, const void *d_plan, T *out,
+                                       void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    PassSpec ps;
+    SMJ_TRY(partition_spec(in, n, cols, use_select, sel_col, sel_val, key_col, h_spl, n_split, ps));
+    if (n == 0) return SMJ_OK;
+    if (!in || !out || in == out || !d_plan) return SMJ_ERR_INVALID;
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    ps.dst = out;
+    ps.trash = sc->trash;
+    HIP_TRY(hipMemsetAsync(&sc->ctr[3], 0, sizeof(Counters), s));
+    ProfScope p3("partition_scatter", 8.0 * cols * 2 * n, s);  // bytes assume every row selected
+    HIP_TRY(launch_chunk_scatter(ps, (uint32_t *)d_plan, &sc->ctr[3], s));
     return SMJ_OK;
 }
 

@@ -70,10 +70,22 @@ struct HostDev {
     int phys = -1;            // HIP device
     hipStream_t st = nullptr;
     hipStream_t cp = nullptr;  // staged H2D copies (overlapping the first pass)
+    // exchange: one stream per source device, so the pulls from all sources
+    // run at once (one xGMI link each) and join st through the events
+    std::vector<hipStream_t> px;
+    std::vector<hipEvent_t> pe;
+    hipEvent_t in_ev[2] = {nullptr, nullptr};  // table x's slice has landed (cp -> st)
+    // result D2H (d2h_result): per copy thread a stream, two pinned slots
+    // and their events, made on the first large result
+    std::vector<hipStream_t> ds;
+    std::vector<hipEvent_t> de;
+    std::vector<char *> dslot;
     void *b[B_N] = {};
     size_t c[B_N] = {};
 };
 std::vector<HostDev> g_devs;
+int64_t g_shard_rows[64];  // rows (R + S) each device of the last sharded call received
+int g_shard_n = 0;
 
 int hgrow(HostDev &d, int i, size_t need) {
     need = std::max<size_t>(need, 64);
@@ -159,6 +171,81 @@ void *result_alloc(size_t bytes) {
     madvise(p, bytes, MADV_HUGEPAGE);
     return p;
 }
+// Device -> host copy of a result into pageable (malloc'd) memory.  A plain
+// hipMemcpy into pageable memory ran at 13-17 GB/s (tools/h2d_overlap.py:
+// 35 ms for C3's 0.59 GB of joined rows): the runtime's single host thread
+// copies each bounce buffer into the destination, first-touch page faults
+// included.  Large results are cut into kD2HThreads contiguous parts; a
+// thread per part pulls its part through two pinned slots on a stream of its
+// own (DMA of chunk k + 1 while chunk k is copied into place), so the PCIe
+// transfer and the host-side copies and page faults run in parallel.  The
+// device's stream st must have produced src already (the caller synchronised).
+constexpr int kD2HThreads = 8;
+constexpr size_t kD2HSlot = (size_t)8 << 20;  // bytes per pinned slot (2 per thread: 128 MiB pinned per device)
+constexpr size_t kD2HMin = (size_t)64 << 20;  // smaller results take one plain copy
+
+int d2h_result(HostDev &hd, void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return SMJ_OK;
+    const char *mn = getenv("SMJ_D2H_MIN");  // tests: the threaded path at small sizes
+    if (bytes < (mn ? (size_t)atoll(mn) : kD2HMin)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, hd.st));
+        HIP_TRY(hipStreamSynchronize(hd.st));
+        return SMJ_OK;
+    }
+    if (hd.ds.empty()) {
+        hd.ds.assign(kD2HThreads, nullptr);
+        hd.de.assign(2 * kD2HThreads, nullptr);
+        hd.dslot.assign(2 * kD2HThreads, nullptr);
+        for (int t = 0; t < kD2HThreads; t++) HIP_TRY(hipStreamCreateWithFlags(&hd.ds[t], hipStreamNonBlocking));
+        for (int i = 0; i < 2 * kD2HThreads; i++) {
+            HIP_TRY(hipEventCreateWithFlags(&hd.de[i], hipEventDisableTiming));
+            HIP_TRY(hipHostMalloc((void **)&hd.dslot[i], kD2HSlot, hipHostMallocDefault));
+        }
+    }
+    std::vector<int> rc(kD2HThreads, SMJ_OK);
+    auto part = [&](int t) {
+        if (hipSetDevice(hd.phys) != hipSuccess) {
+            rc[t] = SMJ_ERR_HIP;
+            return;
+        }
+        const size_t p0 = bytes * t / kD2HThreads / 8 * 8, p1 = t + 1 == kD2HThreads ? bytes : bytes * (t + 1) / kD2HThreads / 8 * 8;
+        const size_t nch = (p1 - p0 + kD2HSlot - 1) / kD2HSlot;
+        auto chunk = [&](size_t k, size_t &o, size_t &len) {
+            o = p0 + k * kD2HSlot;
+            len = std::min(kD2HSlot, p1 - o);
+        };
+        auto issue = [&](size_t k) -> hipError_t {
+            size_t o, len;
+            chunk(k, o, len);
+            hipError_t e = hipMemcpyAsync(hd.dslot[2 * t + (k & 1)], (const char *)src + o, len, hipMemcpyDeviceToHost, hd.ds[t]);
+            return e == hipSuccess ? hipEventRecord(hd.de[2 * t + (k & 1)], hd.ds[t]) : e;
+        };
+        if (nch && issue(0) != hipSuccess) {
+            rc[t] = SMJ_ERR_HIP;
+            return;
+        }
+        for (size_t k = 0; k < nch; k++) {
+            // slot (k + 1) & 1 last held chunk k - 1, already copied out
+            if (k + 1 < nch && issue(k + 1) != hipSuccess) {
+                rc[t] = SMJ_ERR_HIP;
+                return;
+            }
+            if (hipEventSynchronize(hd.de[2 * t + (k & 1)]) != hipSuccess) {
+                rc[t] = SMJ_ERR_HIP;
+                return;
+            }
+            size_t o, len;
+            chunk(k, o, len);
+            memcpy((char *)dst + o, hd.dslot[2 * t + (k & 1)], len);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < kD2HThreads; t++) th.emplace_back(part, t);
+    for (auto &x : th) x.join();
+    for (int t = 0; t < kD2HThreads; t++)
+        if (rc[t] != SMJ_OK) return rc[t];
+    return SMJ_OK;
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -198,6 +285,15 @@ extern "C" int smj_init_devices(const int *device_ids, int n) {
         HIP_TRY(hipSetDevice(device_ids[d]));
         HIP_TRY(hipStreamCreateWithFlags(&g_devs[d].st, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&g_devs[d].cp, hipStreamNonBlocking));
+        for (int x = 0; x < 2; x++) HIP_TRY(hipEventCreateWithFlags(&g_devs[d].in_ev[x], hipEventDisableTiming));
+        if (n > 1) {
+            g_devs[d].px.assign(n, nullptr);
+            g_devs[d].pe.assign(n, nullptr);
+            for (int q = 0; q < n; q++) {
+                HIP_TRY(hipStreamCreateWithFlags(&g_devs[d].px[q], hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&g_devs[d].pe[q], hipEventDisableTiming));
+            }
+        }
     }
     HIP_TRY(hipSetDevice(device_ids[0]));
     return n;
@@ -214,12 +310,25 @@ extern "C" int smj_init(int n_gpus) {
 
 extern "C" int smj_device_count(void) { return (int)g_devs.size(); }
 
+// Diagnostic: rows (R + S, after the WHERE clause) each device of the last
+// sharded call received; returns the device count (at most `max` written).
+extern "C" int smj_debug_shard_rows(int64_t *out, int max) {
+    for (int d = 0; d < std::min(max, g_shard_n); d++) out[d] = g_shard_rows[d];
+    return g_shard_n;
+}
+
 extern "C" void smj_finalize(void) {
     for (auto &d : g_devs) {
         hipSetDevice(d.phys);
         for (int i = 0; i < B_N; i++) hipFree(d.b[i]);
         hipStreamDestroy(d.st);
         hipStreamDestroy(d.cp);
+        for (auto e : d.in_ev) hipEventDestroy(e);
+        for (auto q : d.px) hipStreamDestroy(q);
+        for (auto e : d.pe) hipEventDestroy(e);
+        for (auto q : d.ds) hipStreamDestroy(q);
+        for (auto e : d.de) hipEventDestroy(e);
+        for (auto p : d.dslot) hipHostFree(p);
     }
     g_devs.clear();
     api_free_all();
@@ -320,7 +429,7 @@ struct HTab {                 // one host table of a sharded call
 
 // N - 1 splitters: weighted quantiles of a key sample of every table (a
 // sample of table x stands for n_x / samples input rows; rows the WHERE
-// clause drops are not samples).  bucket(key) = #{splitters < key}.
+// clause drops are not samples).
 std::vector<int64_t> host_splitters(const HTab *t, int ntab, int ktype, int parts) {
     constexpr int64_t kSamples = 8192;
     std::vector<std::pair<int64_t, double>> kw;
@@ -349,6 +458,86 @@ std::vector<int64_t> host_splitters(const HTab *t, int ntab, int ktype, int part
     return spl;
 }
 
+// Partition boundaries for bucket(key) = #{bounds < key}: every splitter key
+// u gets the single-key bucket (u - 1, u] (single[b] = 1), so that a heavy key
+// can be cut between devices at an occurrence index (smj/dist.py
+// bucket_bounds).  Key-only bounds when they would not
+// fit the partition kernel's 64 buckets.
+void shard_bounds(const std::vector<int64_t> &spl, std::vector<int64_t> &bounds, std::vector<char> &single) {
+    bounds.clear();
+    for (int64_t u : spl) {
+        if (u > INT64_MIN && (bounds.empty() || bounds.back() < u - 1)) bounds.push_back(u - 1);
+        bounds.push_back(u);
+    }
+    if ((int)bounds.size() > kMaxSplitters) bounds = spl;
+    const int nb = (int)bounds.size() + 1;
+    single.assign(nb, 0);
+    for (int b = 0; b < nb; b++)
+        single[b] = (b == 0 && !bounds.empty() && bounds[0] == INT64_MIN) ||
+                    (b > 0 && b < nb - 1 && bounds[b] - bounds[b - 1] == 1);
+}
+
+// D - 1 cuts (bucket, occurrence) over the global bucket-ordered sequence,
+// balancing R + S rows per device (smj/dist.py choose_cuts): rows of buckets
+// < b go to the left, and of bucket b the occurrences < o; o != 0 only inside
+// a single-key bucket, and the same o cuts R and S, so occurrence i of R and
+// occurrence i of S -- a zip-join pair -- stay on one device.
+std::vector<std::pair<int, int64_t>> shard_cuts(const std::vector<int64_t> &GR, const std::vector<int64_t> &GS,
+                                                const std::vector<char> &single, int parts) {
+    const int nb = (int)GR.size();
+    std::vector<int64_t> tot(nb);
+    int64_t total = 0;
+    for (int b = 0; b < nb; b++) total += tot[b] = GR[b] + GS[b];
+    std::vector<std::pair<int, int64_t>> cuts;
+    std::pair<int, int64_t> prev{0, 0};
+    int64_t acc = 0;
+    int b = 0;
+    for (int d = 1; d < parts; d++) {
+        const double target = (double)total * d / parts;
+        while (b < nb && (double)(acc + tot[b]) <= target) acc += tot[b++];
+        std::pair<int, int64_t> cut;
+        if (b == nb) {
+            cut = {nb, 0};
+        } else if (single[b]) {
+            const double need = target - (double)acc;
+            auto left = [&](int64_t o) { return (double)(std::min(o, GR[b]) + std::min(o, GS[b])); };
+            int64_t lo = 0, hi = std::max(GR[b], GS[b]);
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if (left(mid) >= need) hi = mid; else lo = mid + 1;
+            }
+            if (lo > 0 && need - left(lo - 1) < left(lo) - need) lo--;
+            cut = {b, lo};
+        } else {  // a multi-key bucket moves whole: to the nearer side
+            cut = target - (double)acc <= (double)(acc + tot[b]) - target ? std::make_pair(b, (int64_t)0)
+                                                                        : std::make_pair(b + 1, (int64_t)0);
+        }
+        cut = std::max(cut, prev);
+        cuts.push_back(cut);
+        prev = cut;
+    }
+    return cuts;
+}
+
+// Row range [edge[d], edge[d + 1]) of one source's bucket-ordered slice goes
+// to device d: cut (b, o) sits after the slice's buckets < b and, of bucket b,
+// after its rows whose global occurrence (rows of bucket b on earlier sources
+// + the local offset) is below o.
+std::vector<int64_t> shard_edges(const std::vector<int64_t> &local, const std::vector<int64_t> &prefix,
+                                 const std::vector<std::pair<int, int64_t>> &cuts) {
+    const int nb = (int)local.size();
+    std::vector<int64_t> before(nb + 1, 0);
+    for (int b = 0; b < nb; b++) before[b + 1] = before[b] + local[b];
+    std::vector<int64_t> e{0};
+    for (const auto &c : cuts) {
+        int64_t p = before[c.first];
+        if (c.first < nb) p += std::min(std::max<int64_t>(c.second - prefix[c.first], 0), local[c.first]);
+        e.push_back(p);
+    }
+    e.push_back(before[nb]);
+    return e;
+}
+
 // ntab = 2: select -> sort -> zip join of R and S, *out / *out_rows the
 // joined rows.  ntab = 1: select-free stable sort of one table, written back
 // into sorted_back.  timing (may be NULL) in the reference's three buckets.
@@ -356,35 +545,43 @@ int sharded_run(int ktype, const HTab *tab, int ntab, int key2, T **out, int64_t
                 smj_timing_t *timing) {
     const int D = (int)g_devs.size();
     const double t0 = now_ms();
-    std::vector<int64_t> spl = host_splitters(tab, ntab, ktype, D);
-    const int nspl = (int)spl.size();
-    const int NB = nspl + 1;  // key ranges: range b goes to device b (b < D)
-    // counts[d][x][b]: rows of device d's slice of table x in range b
+    std::vector<int64_t> bounds;
+    std::vector<char> single;
+    shard_bounds(host_splitters(tab, ntab, ktype, D), bounds, single);
+    const int nspl = (int)bounds.size();
+    const int NB = nspl + 1;  // partition buckets; cuts (bucket, occurrence) split them over the devices
+    // counts[d][x][b]: rows of device d's slice of table x in bucket b
     std::vector<std::vector<std::vector<int64_t>>> counts(D, std::vector<std::vector<int64_t>>(2, std::vector<int64_t>(NB, 0)));
     std::vector<double> t_h2d(D, 0.0);
     auto slice = [&](int x, int d, int64_t &r0, int64_t &r1) {
         r0 = tab[x].n * d / D;
         r1 = tab[x].n * (d + 1) / D;
     };
-    // 2. H2D of the slices, key map, select + stable range partition
+    // 2. H2D of the slices on the copy stream; the key map, select and stable
+    //    bucket partition of table x start as soon as its slice has landed (so
+    //    R's partition overlaps S's copy)
     SMJ_TRY(on_devices([&](int d) -> int {
         HostDev &hd = g_devs[d];
         SMJ_TRY(hgrow(hd, B_SPL, 64 * sizeof(int64_t)));
-        if (nspl) HIP_TRY(hipMemcpyAsync(hd.b[B_SPL], spl.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, hd.st));
+        if (nspl) HIP_TRY(hipMemcpyAsync(hd.b[B_SPL], bounds.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, hd.st));
         for (int x = 0; x < ntab; x++) {
             int64_t r0, r1;
             slice(x, d, r0, r1);
             const size_t bytes = (size_t)(r1 - r0) * tab[x].cols * 8;
             SMJ_TRY(hgrow(hd, B_IN0 + x, bytes));
             SMJ_TRY(hgrow(hd, B_PART0 + x, bytes));
-            if (bytes) HIP_TRY(hipMemcpyAsync(hd.b[B_IN0 + x], tab[x].rows + r0 * tab[x].cols, bytes, hipMemcpyHostToDevice, hd.st));
+            if (bytes) HIP_TRY(hipMemcpyAsync(hd.b[B_IN0 + x], tab[x].rows + r0 * tab[x].cols, bytes, hipMemcpyHostToDevice, hd.cp));
+            HIP_TRY(hipEventRecord(hd.in_ev[x], hd.cp));
         }
-        HIP_TRY(hipStreamSynchronize(hd.st));
-        t_h2d[d] = now_ms();
         for (int x = 0; x < ntab; x++) {
             int64_t r0, r1;
             slice(x, d, r0, r1);
+            if (x == ntab - 1) {  // the CPU-GPU bucket ends when the last slice has landed
+                HIP_TRY(hipEventSynchronize(hd.in_ev[x]));
+                t_h2d[d] = now_ms();
+            }
             if (r1 == r0) continue;
+            HIP_TRY(hipStreamWaitEvent(hd.st, hd.in_ev[x], 0));
             if (ktype != SMJ_KEY_INT64)
                 HIP_TRY(launch_key_map((const int64_t *)hd.b[B_IN0 + x], (int64_t *)hd.b[B_IN0 + x], r1 - r0,
                                        tab[x].cols, map_mask(tab[x].key, tab[x].sel_col), ktype, 0, hd.st));
@@ -395,33 +592,56 @@ int sharded_run(int ktype, const HTab *tab, int ntab, int key2, T **out, int64_t
         return SMJ_OK;
     }));
     const double t_h2d_end = *std::max_element(t_h2d.begin(), t_h2d.end());
-    // 3 + 4. pull range d from every device (source order), then the pipeline
+    // 3. the cuts over the global counts; edges[s][x][d]: device d takes rows
+    //    [edges[d], edges[d + 1]) of source s's partitioned slice of table x
+    std::vector<int64_t> G[2] = {std::vector<int64_t>(NB, 0), std::vector<int64_t>(NB, 0)};
+    for (int d = 0; d < D; d++)
+        for (int x = 0; x < ntab; x++)
+            for (int b = 0; b < NB; b++) G[x][b] += counts[d][x][b];
+    const auto cuts = shard_cuts(G[0], G[1], single, D);
+    std::vector<std::vector<std::vector<int64_t>>> edges(D, std::vector<std::vector<int64_t>>(2));
+    for (int x = 0; x < ntab; x++) {
+        std::vector<int64_t> prefix(NB, 0);
+        for (int s = 0; s < D; s++) {
+            edges[s][x] = shard_edges(counts[s][x], prefix, cuts);
+            for (int b = 0; b < NB; b++) prefix[b] += counts[s][x][b];
+        }
+    }
+    // 4. device d pulls its range from every source at once (one stream per
+    //    source: the xGMI links run in parallel), placed in source order so
+    //    that equal keys keep their input order; then the pipeline
     std::vector<int64_t> J(D, 0), M(D, 0);
     const int tc = ntab > 1 ? tab[0].cols + tab[1].cols - 1 : 1;
+    g_shard_n = std::min(D, 64);
     SMJ_TRY(on_devices([&](int d) -> int {
         HostDev &hd = g_devs[d];
         int64_t rows[2] = {0, 0};
         for (int x = 0; x < ntab; x++) {
-            for (int s = 0; s < D; s++) rows[x] += d < NB ? counts[s][x][d] : 0;
+            for (int s = 0; s < D; s++) rows[x] += edges[s][x][d + 1] - edges[s][x][d];
             SMJ_TRY(hgrow(hd, B_RECV0 + x, (size_t)rows[x] * tab[x].cols * 8));
             SMJ_TRY(hgrow(hd, B_OUT0 + x, (size_t)rows[x] * tab[x].cols * 8));
-            int64_t at = 0;
-            for (int s = 0; s < D && d < NB; s++) {
-                int64_t off = 0;
-                for (int b = 0; b < d; b++) off += counts[s][x][b];
-                const int64_t c = counts[s][x][d];
+        }
+        if (d < 64) g_shard_rows[d] = rows[0] + (ntab > 1 ? rows[1] : 0);
+        int64_t at[2] = {0, 0};
+        for (int s = 0; s < D; s++) {
+            hipStream_t q = D > 1 ? hd.px[s] : hd.st;
+            for (int x = 0; x < ntab; x++) {
+                const int64_t c = edges[s][x][d + 1] - edges[s][x][d];
                 if (c == 0) continue;
                 const size_t W = (size_t)tab[x].cols * 8;
-                char *dst = (char *)hd.b[B_RECV0 + x] + at * W;
-                const char *src = (const char *)g_devs[s].b[B_PART0 + x] + off * W;
+                char *dst = (char *)hd.b[B_RECV0 + x] + at[x] * W;
+                const char *src = (const char *)g_devs[s].b[B_PART0 + x] + edges[s][x][d] * W;
                 if (g_devs[s].phys == hd.phys)
-                    HIP_TRY(hipMemcpyAsync(dst, src, c * W, hipMemcpyDeviceToDevice, hd.st));
+                    HIP_TRY(hipMemcpyAsync(dst, src, c * W, hipMemcpyDeviceToDevice, q));
                 else
-                    HIP_TRY(hipMemcpyPeerAsync(dst, hd.phys, src, g_devs[s].phys, c * W, hd.st));
-                at += c;
+                    HIP_TRY(hipMemcpyPeerAsync(dst, hd.phys, src, g_devs[s].phys, c * W, q));
+                at[x] += c;
+            }
+            if (D > 1) {
+                HIP_TRY(hipEventRecord(hd.pe[s], q));
+                HIP_TRY(hipStreamWaitEvent(hd.st, hd.pe[s], 0));
             }
         }
-        HIP_TRY(hipStreamSynchronize(hd.st));
         if (ntab == 1) {
             if (rows[0]) {
                 SMJ_TRY(smj_dev_select_sort((const T *)hd.b[B_RECV0], rows[0], tab[0].cols, 0, 0, 0, tab[0].key, 0,
@@ -430,6 +650,7 @@ int sharded_run(int ktype, const HTab *tab, int ntab, int key2, T **out, int64_t
                     HIP_TRY(launch_key_map((const int64_t *)hd.b[B_OUT0], (int64_t *)hd.b[B_OUT0], M[d], tab[0].cols,
                                            map_mask(tab[0].key, tab[0].key), ktype, 1, hd.st));
             }
+            HIP_TRY(hipStreamSynchronize(hd.st));
             return SMJ_OK;
         }
         SMJ_TRY(hgrow(hd, B_J, (size_t)std::max<int64_t>(1, std::min(rows[0], rows[1])) * tc * 8));
@@ -466,9 +687,7 @@ int sharded_run(int ktype, const HTab *tab, int ntab, int key2, T **out, int64_t
         if (n == 0) return SMJ_OK;
         const size_t W = (size_t)(ntab > 1 ? tc : tab[0].cols) * 8;
         void *dst = ntab > 1 ? (void *)((char *)res + at[d] * W) : (void *)((char *)sorted_back + at[d] * W);
-        HIP_TRY(hipMemcpyAsync(dst, hd.b[ntab > 1 ? B_J : B_OUT0], n * W, hipMemcpyDeviceToHost, hd.st));
-        HIP_TRY(hipStreamSynchronize(hd.st));
-        return SMJ_OK;
+        return d2h_result(hd, dst, hd.b[ntab > 1 ? B_J : B_OUT0], n * W);
     });
     if (rc != SMJ_OK) {
         free(res);
@@ -538,12 +757,12 @@ extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, con
     }
     HostDev &hd = g_devs[0];
     hipStream_t st = hd.st;
-    hipEvent_t ev[4];
+    hipEvent_t ev[3];
     for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
     struct EvFree {
         hipEvent_t *e;
         ~EvFree() {
-            for (int i = 0; i < 4; i++) hipEventDestroy(e[i]);
+            for (int i = 0; i < 3; i++) hipEventDestroy(e[i]);
         }
     } evf{ev};
     SMJ_TRY(hgrow(hd, B_IN0, (size_t)nr * c1 * 8));
@@ -575,17 +794,19 @@ extern "C" int smj_sort_merge_join_typed(int key_type, const dpu_block_t *r, con
     }
     const int64_t j = rows[2];
     HIP_TRY(hipEventRecord(ev[2], st));
+    HIP_TRY(hipEventSynchronize(ev[2]));
+    const double t2 = now_ms();
     T *res = (T *)result_alloc((size_t)j * tc * sizeof(T));
     if (!res) return SMJ_ERR_NOMEM;
-    if ((j && hipMemcpyAsync(res, hd.b[B_J], (size_t)j * tc * 8, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipEventRecord(ev[3], st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+    const int rc2 = d2h_result(hd, res, hd.b[B_J], (size_t)j * tc * 8);
+    if (rc2 != SMJ_OK) {
         free(res);
-        return SMJ_ERR_HIP;
+        return rc2;
     }
     if (timing) {
         timing->cpu_gpu_ms = ev_ms(ev[0], ev[1]);
         timing->gpu_ms = ev_ms(ev[1], ev[2]);
-        timing->gpu_cpu_ms = ev_ms(ev[2], ev[3]);
+        timing->gpu_cpu_ms = now_ms() - t2;
     }
     *out = res;
     *out_rows = j;

@@ -56,6 +56,9 @@ SIGNATURES = {
     "smj_dev_partition_count": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _PL, _PL, _P]),
     "smj_dev_partition_scatter": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _PL, _P, _P]),
     "smj_dev_partition": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _PL, _P]),
+    "smj_partition_plan_bytes": (ctypes.c_size_t, [_L, _I, _I]),
+    "smj_dev_partition_plan": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P]),
+    "smj_dev_partition_apply": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P]),
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),
@@ -63,6 +66,7 @@ SIGNATURES = {
     "smj_debug_msd_groups": (None, [_PL]),
     "smj_debug_msd_tiers": (None, [_PL]),
     "smj_debug_force_parts": (None, [_I]),
+    "smj_debug_shard_rows": (_I, [_PL, _I]),
     "smj_prof_enable": (None, [_I]),
     "smj_prof_report": (_I, [ctypes.c_char_p, ctypes.c_size_t]),
 }

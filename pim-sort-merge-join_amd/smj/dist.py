@@ -61,6 +61,8 @@ class HipOps:
     sort_merge_join = staticmethod(hip_ops.sort_merge_join)
     partition = staticmethod(hip_ops.partition)
     partition_count = staticmethod(hip_ops.partition_count)
+    partition_plan = staticmethod(hip_ops.partition_plan)    # asynchronous: counts stay on the device
+    partition_apply = staticmethod(hip_ops.partition_apply)
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
@@ -89,43 +91,44 @@ def _wire_device(t, group=None):
 
 
 def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None):
-    """parts - 1 (default W - 1) sorted key splitters, identical on every rank
-    (one all_gather)."""
+    """parts - 1 (default W - 1) sorted key splitters, identical on every rank,
+    as a host list: one all_gather of every rank's sample (a fixed-size buffer,
+    padded with INT64_MAX, plus its valid count), the sort and the order
+    statistics on the device, one device -> host copy of the result."""
     parts = parts or world
     local = torch.cat([_sample_keys(t, k, samples) for t, k in tables_and_keys])
-    home = local.device
     dev = _wire_device(local, group)
     local = local.to(dev)
-    # fixed-size exchange: pad with INT64_MAX and a count
-    cnt = torch.tensor([local.numel()], dtype=torch.int64, device=dev)
     cap = len(tables_and_keys) * samples
-    buf = torch.full((cap,), INT64_MAX, dtype=torch.int64, device=dev)
-    buf[: local.numel()] = local
-    all_cnt = [torch.empty_like(cnt) for _ in range(world)]
+    buf = torch.full((cap + 1,), INT64_MAX, dtype=torch.int64, device=dev)
+    buf[0] = local.numel()
+    buf[1: 1 + local.numel()] = local
     all_buf = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(all_cnt, cnt, group=group)
     dist.all_gather(all_buf, buf, group=group)
-    counts = torch.cat(all_cnt).tolist()  # one device -> host copy for all ranks' counts
-    keys = torch.cat([b[:c] for b, c in zip(all_buf, counts)])
-    if keys.numel() == 0:
-        return torch.zeros(parts - 1, dtype=torch.int64, device=home)
-    keys = torch.sort(keys).values
-    L = keys.numel()
-    pos = torch.tensor([max((i + 1) * L // parts - 1, 0) for i in range(parts - 1)], device=dev)
-    return keys[pos].contiguous().to(home)
+    allb = torch.stack(all_buf)
+    L = allb[:, 0].sum()
+    # the pads sort last (a real INT64_MAX key sorts among them: the same value)
+    keys = torch.sort(allb[:, 1:].reshape(-1)).values
+    pos = (torch.arange(1, parts, dtype=torch.int64, device=dev) * L // parts - 1).clamp(min=0)
+    got = torch.cat([keys[pos], L.view(1)]).tolist()
+    if got[-1] == 0:
+        return [0] * (parts - 1)
+    return got[:-1]
 
 
 def bucket_bounds(spl):
     """Boundaries s for the partition kernels' bucket(k) = #{s < k}: every
-    distinct splitter key u gets the single-key bucket (u-1, u].  Returns (s,
-    single) with single[b] true when bucket b holds exactly one key value."""
+    distinct splitter key u (spl: a host list) gets the single-key bucket
+    (u-1, u].  Returns (s, single) with single[b] true when bucket b holds
+    exactly one key value."""
+    spl = [int(x) for x in (spl.tolist() if isinstance(spl, torch.Tensor) else spl)]
     s = []
-    for u in sorted(set(int(x) for x in spl.tolist())):
+    for u in sorted(set(spl)):
         if u > INT64_MIN and (not s or s[-1] < u - 1):
             s.append(u - 1)
         s.append(u)
     if len(s) > MAX_BOUNDS:  # too many ranks for single-key buckets: key-only splitters
-        s = sorted(set(int(x) for x in spl.tolist()))
+        s = sorted(set(spl))
     single = [(b == 0 and bool(s) and s[0] == INT64_MIN) or (0 < b < len(s) and s[b] - s[b - 1] == 1)
               for b in range(len(s) + 1)]
     return s, single
@@ -185,11 +188,16 @@ def slice_counts(local, prefix, cuts, nb):
 
 
 def gather_counts(counts, world, group=None, device=None):
-    """all_gather of this rank's integer vector; returns a world x len list."""
-    t = torch.tensor(counts, dtype=torch.int64, device=device)
+    """all_gather of this rank's integer vector (a list, or a device tensor
+    that stays on the device until the one host copy of the gathered
+    result); returns a world x len list."""
+    if isinstance(counts, torch.Tensor):
+        t = counts.to(device if device is not None else counts.device)
+    else:
+        t = torch.tensor(counts, dtype=torch.int64, device=device)
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t, group=group)
-    return [[int(v) for v in o.tolist()] for o in out]
+    return torch.stack(out).tolist()
 
 
 def stage_count(world, stages):
@@ -283,18 +291,21 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
     nseg = world * K
 
-    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg)
+    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg)  # host sync 1
     bounds, single = bucket_bounds(spl)
-    bt = torch.tensor(bounds, dtype=torch.int64, device=R.device)
     nb = len(bounds) + 1
-    # exact S counts first (a read-only counting pass), so that R's stage-0
-    # rows can leave while S is being partitioned
-    cS, _ = ops.partition_count(S, bt, k2, sc2, sv2)
-    cR, rowsR = ops.partition(R, bt, k1, sc1, sv1)
+    # R: counted and scattered; S: counted only (its plan keeps the per-chunk
+    # starts), so that R's stage-0 rows can leave while S is being scattered.
+    # Nothing here waits for the device: the counts stay in `cnt`.
+    cnt = torch.empty(2 * nb, dtype=torch.int64, device=R.device)
+    planR = ops.partition_plan(R, bounds, cnt[:nb], k1, sc1, sv1)
+    rowsR = ops.partition_apply(R, bounds, planR, k1, sc1, sv1)
+    planS = ops.partition_plan(S, bounds, cnt[nb:], k2, sc2, sv2)
+    del planR
     wire = _wire_device(rowsR, group)
     sends = [rowsR.to(wire), None]
     del rowsR
-    allc = gather_counts(cR + cS, world, group, _wire_device(R, group))
+    allc = gather_counts(cnt, world, group, _wire_device(R, group))  # host sync 2
     G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
     cuts = choose_cuts(G[0], G[1], single, nseg)
     # every source rank's rows per segment, from the gathered counts
@@ -316,9 +327,8 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
     pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group, loopback)]  # R's stage 0
-    cS2, rowsS = ops.partition(S, bt, k2, sc2, sv2)  # overlaps R's stage-0 exchange
-    if list(cS2) != list(cS):
-        raise RuntimeError("smj.dist: partition counts disagree with the counting pass")
+    rowsS = ops.partition_apply(S, bounds, planS, k2, sc2, sv2)  # overlaps R's stage-0 exchange
+    del planS
     sends[1] = rowsS.to(wire)
     del rowsS
     pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group, loopback))
@@ -336,10 +346,11 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
             parts.append(ops.sort_merge_join(Rk, Sk, k1, k2, None, None)[2])
         del Rk, Sk
     del sends
-    if stats is not None:
-        loads = gather_counts([rows_in[0] + rows_in[1]], world, group, _wire_device(R, group))
-        mean = sum(l[0] for l in loads) / world
-        stats.update(rows_in=rows_in, load_max_over_mean=(max(l[0] for l in loads) / mean) if mean else 1.0,
+    if stats is not None:  # every rank's load, from the gathered counts (no communication)
+        loads = [sum(seg[t][r][d * K + k] for t in range(2) for r in range(world) for k in range(K))
+                 for d in range(world)]
+        mean = sum(loads) / world
+        stats.update(rows_in=rows_in, load_max_over_mean=(max(loads) / mean) if mean else 1.0,
                      cuts=cuts, buckets=nb, stages=K)
     if into:
         return J[:at]

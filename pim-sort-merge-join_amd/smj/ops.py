@@ -294,6 +294,51 @@ def partition(table, splitters, key_col=0, select_col=0, select_val=None, out=No
     return counts, out[: sum(counts)]
 
 
+def _host_splitters(bounds):
+    arr = (ctypes.c_int64 * max(len(bounds), 1))(*[int(b) for b in bounds])
+    return arr, len(bounds)
+
+
+def partition_plan(table, bounds, counts, key_col=0, select_col=0, select_val=None, stream=None):
+    """Asynchronous first half of the partition (smj_dev_partition_plan):
+    per-(chunk, bucket) counts of the selected rows turned into stable output
+    starts; the len(bounds) + 1 bucket counts are written into `counts` (a
+    1-D int64 CUDA tensor view) without a host synchronisation.  bounds: a
+    sorted host list.  Returns the plan (a device buffer) for
+    partition_apply."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    if not (counts.is_cuda and counts.dtype == torch.int64 and counts.is_contiguous()
+            and counts.numel() == len(bounds) + 1):
+        raise ValueError("counts must be a contiguous int64 CUDA tensor of len(bounds) + 1 entries")
+    plan = torch.empty(max(int(lib.smj_partition_plan_bytes(n, cols, len(bounds))), 4) // 4, dtype=torch.int32,
+                       device=table.device)
+    spl, ns = _host_splitters(bounds)
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition_plan(_ptr(table), n, cols, int(use), select_col, int(select_val) if use else 0,
+                                          key_col, spl, ns, _ptr(plan), ctypes.c_void_p(counts.data_ptr()),
+                                          _stream(stream)), "smj_dev_partition_plan")
+    return plan
+
+
+def partition_apply(table, bounds, plan, key_col=0, select_col=0, select_val=None, out=None, stream=None):
+    """Asynchronous second half: the selected rows in bucket-contiguous order,
+    written into `out` (n rows of room; the caller knows the selected count
+    from the plan's counts).  Returns out."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    out = torch.empty((max(n, 1), cols), dtype=torch.int64, device=table.device) if out is None else \
+        _out(out, "out", n, cols, table)
+    spl, ns = _host_splitters(bounds)
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition_apply(_ptr(table), n, cols, int(use), select_col,
+                                           int(select_val) if use else 0, key_col, spl, ns, _ptr(plan), _ptr(out),
+                                           _stream(stream)), "smj_dev_partition_apply")
+    return out
+
+
 def gen_uniform(rows, row0=0, seed=1, key_range=None, device="cuda", out=None, stream=None):
     """Synthetic (key, payload) table: keys iid uniform in [1, key_range],
     payload = global row index."""

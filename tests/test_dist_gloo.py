@@ -60,6 +60,17 @@ class OracleOps:
         return torch.from_numpy(keep[np.argsort(bucket, kind="stable")].copy())
 
     @staticmethod
+    def partition_plan(T, bounds, counts, key=0, sc=0, sv=None):
+        keep, bucket = OracleOps._keep(T, key, sc, sv, torch.tensor(bounds, dtype=torch.int64))
+        counts.copy_(torch.from_numpy(np.bincount(bucket, minlength=len(bounds) + 1).astype(np.int64)))
+        return keep, bucket
+
+    @staticmethod
+    def partition_apply(T, bounds, plan, key=0, sc=0, sv=None):
+        keep, bucket = plan
+        return torch.from_numpy(keep[np.argsort(bucket, kind="stable")].copy())
+
+    @staticmethod
     def partition(T, spl, key=0, sc=0, sv=None):
         counts, _ = OracleOps.partition_count(T, spl, key, sc, sv)
         return counts, OracleOps.partition_scatter(T, spl, counts, key, sc, sv)

@@ -106,6 +106,35 @@ def test_sharded_equals_oracle_for_every_device_count(lib, oracle_built, kind, n
         np.testing.assert_array_equal(got, ref.reshape(-1, R.shape[1] + S.shape[1] - 1), err_msg=f"{n} devices")
 
 
+def shard_rows(lib, n):
+    out = (ctypes.c_int64 * n)()
+    assert lib.smj_debug_shard_rows(out, n) == n
+    return list(out)
+
+
+@pytest.mark.parametrize("n_dev", [2, 4, 8])
+def test_heavy_key_is_cut_by_occurrence(lib, oracle_built, n_dev):
+    """A key holding 60 % of R and 50 % of S: the device set cuts it at an
+    occurrence index (the same for R and S, so zip pairs stay together) and
+    the devices' loads stay within 10 % of the mean (key-only splitters would
+    put the whole key on one device: max / mean ~ 0.55 n_dev); the result is
+    byte-identical to the oracle (smj/dist.py choose_cuts)."""
+    rng = np.random.default_rng(21)
+    nr, ns = 400_000, 300_000
+    R = np.stack([rng.integers(-10_000, 10_000, nr), np.arange(nr)], 1)
+    S = np.stack([rng.integers(-10_000, 10_000, ns), 10 ** 9 + np.arange(ns)], 1)
+    R[rng.random(nr) < 0.6, 0] = 4242
+    S[rng.random(ns) < 0.5, 0] = 4242
+    R, S = np.ascontiguousarray(R, dtype=np.int64), np.ascontiguousarray(S, dtype=np.int64)
+    sel = (1, -1, 0, -20_000)
+    ref = oracle.join(oracle.select_sort(R, 0, 1, -1), oracle.select_sort(S, 0, 0, -20_000), 0, 0)
+    init_virtual(lib, n_dev)
+    np.testing.assert_array_equal(run_smj(lib, R, S, sel, (0, 0)), ref)
+    rows = shard_rows(lib, n_dev)
+    assert sum(rows) == nr + ns
+    assert max(rows) / (sum(rows) / n_dev) <= 1.10, rows
+
+
 def test_sharded_sort(lib, oracle_built):
     from smj import _lib
     rng = np.random.default_rng(3)
