@@ -45,6 +45,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 namespace smj {
 
@@ -193,6 +195,17 @@ __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
     return (uint32_t)pos + (rep ? 1u : 0u);
 }
 
+// level-1 split of the partitioned mode: #{splitters < key} (the unused
+// splitters are INT64_MAX, never < key)
+__device__ __forceinline__ uint32_t bucket_range(const int64_t *s_spl, int64_t k) {
+    int pos = 0;
+#pragma unroll
+    for (int step = kBucketsA / 2; step >= 1; step >>= 1)
+        pos += (s_spl[pos + step - 1] < k) ? step : 0;
+    return (uint32_t)pos;
+}
+
+
 // ---------------------------------------------------------------------------
 // sample -> splitters
 // ---------------------------------------------------------------------------
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
                               ? jj
                               : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
                                                  jj % kSampleRun);
-        const int64_t *row = t.src + r * t.cols;
+        const int64_t *row = t.v.rows ? t.v.rows + virt_row(t.v, (uint32_t)r) * t.cols : t.src + r * t.cols;
         const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
         if (!t.use_sel || sv > t.sel_val) {
             k = kv;
@@ -319,10 +332,34 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     zero_counters<RADIX>(wc, lane);
     const int lrow0 = wave * ITEMS * 64 + lane;
     int64_t rows[ITEMS][COLS];
+    if (p.v.rows) {  // partitioned mode: this virtual tile's rows through its level-1 segments
+        const MsdVSeg &sg = p.v.seg[t];  // tile-uniform: scalar loads
+        const uint32_t ns = sg.n;
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++)
-        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
-        else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        for (int it = 0; it < ITEMS; it++) {
+            const uint32_t o = (uint32_t)min(lrow0 + it * 64, nrows - 1);
+            int64_t r;
+            if (ns <= (uint32_t)kVSegs) {
+                int64_t ph = sg.phys[0];
+                uint32_t b = 0;
+#pragma unroll
+                for (int k = 1; k < kVSegs; k++) {
+                    const bool in = (uint32_t)k < ns && sg.v0[k] <= o;
+                    ph = in ? sg.phys[k] : ph;
+                    b = in ? sg.v0[k] : b;
+                }
+                r = ph + (o - b);
+            } else {
+                r = virt_row(p.v, (uint32_t)row0 + o);
+            }
+            load_row<COLS>(p.v.rows + r * COLS, rows[it]);
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+            else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+    }
     __syncthreads();  // splitters
 
     uint32_t dig[ITEMS];
@@ -334,7 +371,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
         const bool pass = !p.use_sel | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
         const bool v = inb & pass;
         const int64_t k = pick<COLS>(rows[it], p.key_col);
-        dig[it] = v ? bucket_a(s_spl, k) : 0u;
+        dig[it] = v ? (p.range_parts ? bucket_range(s_spl, k) : bucket_a(s_spl, k)) : 0u;
         vmask |= v ? (1u << it) : 0u;
         mn = v ? min(mn, k) : mn;
         mx = v ? max(mx, k) : mx;
@@ -352,7 +389,11 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
     static_assert(RADIX < kMsdThreads && RADIX < kOffsARow, "one offsA entry per thread");
-    if (tid <= RADIX) p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
+    if (p.range_parts) {  // level-1 split: the part starts + the tile's selected rows
+        if (tid <= p.range_parts) p.offs[t * (p.range_parts + 1) + tid] = s_bin[tid];
+    } else if (tid <= RADIX) {
+        p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
+    }
     if (tid == 0) {
         p.tmm[2 * t] = mn;
         p.tmm[2 * t + 1] = mx;
@@ -2862,13 +2903,22 @@ constexpr int kBgIt = kGroupCap / kMsdThreads;  // chunk rows per thread
 #endif
 constexpr uint32_t kBgLarge = 8 * kGroupCap;  // groups over this many rows (either table) are dealt first
 static_assert(kBgSeg % kGroupCap == 0 && kStRange % (4 * kMsdThreads) == 0, "giant jobs: whole chunks, uint4 counts");
-struct BgSmem {                 // 48.5 KiB: three workgroups per CU
+constexpr int kBgIds = 256;     // compact residual ids of the parallel ranking (more distinct keys: the
+                                // wave-serial ranking)
+constexpr int kBgBlk = 2048;    // 64-row blocks of a row range a block table covers (131072 rows)
+struct BgSmem {                 // 69 KiB: two workgroups per CU
     uint32_t end[2][kStRange];   // per residual: row count, then the running start of its output rows
     union {
         uint2 list[2][kGroupCap];    // per table: {tempB row, group row} of each pass-B tile's run
         uint32_t jst[kStRange + 1];  // once the rows are placed: the exclusive prefix over residuals of
                                      // min(countR, countS) (join rows)
     };
+    uint8_t id[kStRange];        // residual -> compact id (the group's distinct residuals in order)
+    uint16_t rid[kBgIds];        // compact id -> residual
+    uint32_t wcnt[kMsdWaves][kBgIds];  // per wave and id: rows of the chunk, then their first output row
+    uint16_t blk[2][kBgBlk];     // per table: the run holding row bv0 + 64 b (bg_blocks)
+    uint32_t bv0[2], nblk[2];    // the rows the block table covers start at bv0 (nblk == 0: no table)
+    uint32_t nid;                // distinct residuals (> kBgIds: wave-serial ranking)
     uint32_t nl[2];              // runs per table
     uint32_t wsum[kMsdWaves];
     uint32_t ticket;
@@ -2923,6 +2973,39 @@ __device__ __forceinline__ uint32_t bg_src(const uint2 *lst, uint32_t nl, uint32
     return e.x + (v - e.y);
 }
 
+// O(1)-ish row -> run lookup for rows [v0, v1) of table X (after bg_lists):
+// blk[b] = the run holding row v0 + 64 b; a lookup walks on from there over
+// the runs starting inside the block (groups of Zipf tables: ~10-row runs)
+__device__ __forceinline__ void bg_blocks(BgSmem &sm, int X, uint32_t n, uint32_t v0, uint32_t v1) {
+    const int tid = threadIdx.x;
+    const uint32_t nb = (v1 - v0 + 63) >> 6, nl = sm.nl[X];
+    if (tid == 0) {
+        sm.bv0[X] = v0;
+        sm.nblk[X] = nb <= (uint32_t)kBgBlk ? nb : 0u;
+    }
+    if (nb <= (uint32_t)kBgBlk && v1 > v0) {
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t j = (uint32_t)tid * kBgIt + i;
+            if (j >= nl) continue;
+            const uint32_t y0 = max(sm.list[X][j].y, v0), y1 = min(j + 1 < nl ? sm.list[X][j + 1].y : n, v1);
+            if (y0 >= y1) continue;
+            for (uint32_t b = (y0 - v0 + 63) >> 6; b <= (y1 - 1 - v0) >> 6; b++) sm.blk[X][b] = (uint16_t)j;
+        }
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t bg_src_blk(const BgSmem &sm, int X, uint32_t v) {
+    const uint2 *lst = sm.list[X];
+    const uint32_t nl = sm.nl[X];
+    if (sm.nblk[X]) {
+        uint32_t j = sm.blk[X][(v - sm.bv0[X]) >> 6];
+        for (int k = 0; k < 8 && j + 1 < nl && lst[j + 1].y <= v; k++) j++;
+        if (!(j + 1 < nl && lst[j + 1].y <= v)) return lst[j].x + (v - lst[j].y);
+    }
+    return bg_src(lst, nl, v);
+}
+
 // the group's run list per table (one block scan each), then a barrier
 __device__ __forceinline__ void bg_lists(const MsdFinalParams &p, const MsdGroup &g, BgSmem &sm) {
     const int tid = threadIdx.x;
@@ -2971,7 +3054,7 @@ __device__ __forceinline__ void bg_count(const MsdFinalParams &p, const MsdGroup
             const uint32_t v = c0 + tid + i * kMsdThreads;
             k[i] = 0;
             if (v < v1) {
-                const i64x2 r = tB[bg_src(sm.list[X], sm.nl[X], v)];
+                const i64x2 r = tB[bg_src_blk(sm, X, v)];
                 k[i] = tb.key ? r.y : r.x;
             }
         }
@@ -2999,7 +3082,7 @@ __device__ __forceinline__ void bg_scatter(const MsdFinalParams &p, const MsdGro
             const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
             rows[i] = i64x2{0, 0};
             if (v < v1) {
-                rows[i] = tB[bg_src(sm.list[X], sm.nl[X], v)];
+                rows[i] = tB[bg_src_blk(sm, X, v)];
                 vm |= 1u << i;
             }
         }
@@ -3027,6 +3110,103 @@ __device__ __forceinline__ void bg_scatter(const MsdFinalParams &p, const MsdGro
 #pragma unroll
         for (int i = 0; i < kBgIt; i++) cur[i] = nxt[i];
         vmask = vnext;
+    }
+}
+
+// compact ids of the group's distinct residuals (sm.end = the residual
+// counts of both tables): id[r] = #{distinct residuals < r}, rid[id] = r,
+// nid = their number.  Ends with a barrier.
+__device__ __forceinline__ void bg_build_ids(BgSmem &sm) {
+    constexpr int RP = kStRange / kMsdThreads;
+    const int tid = threadIdx.x;
+    uint32_t f = 0, sum = 0;
+#pragma unroll
+    for (int j = 0; j < RP; j++) {
+        const int r = tid * RP + j;
+        const bool nz = (sm.end[0][r] | sm.end[1][r]) != 0u;
+        f |= nz ? (1u << j) : 0u;
+        sum += nz ? 1u : 0u;
+    }
+    uint32_t all;
+    uint32_t ex = block_excl_scan<kMsdWaves>(sum, sm.wsum, &all);
+    if (all <= (uint32_t)kBgIds) {
+#pragma unroll
+        for (int j = 0; j < RP; j++)
+            if ((f >> j) & 1u) {
+                const int r = tid * RP + j;
+                sm.id[r] = (uint8_t)ex;
+                sm.rid[ex] = (uint16_t)r;
+                ex++;
+            }
+    }
+    if (tid == 0) sm.nid = all;
+    __syncthreads();
+}
+
+// bg_scatter with the waves ranking in parallel (the group has <= kBgIds
+// distinct residuals): per chunk of kGroupCap rows (input order = wave,
+// item, lane) each wave ranks its rows by ballots on the 8-bit compact id and
+// counts them per id; one thread per id then turns the per-wave counts into
+// the waves' first output rows (running start end[r] + the earlier waves'
+// rows) and advances end[r].  Two barriers per chunk instead of eight waves
+// in turn.
+template <int X>
+__device__ __forceinline__ void bg_scatter_ids(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
+                                               BgSmem &sm) {
+    const MsdTab &tb = p.tab[X];
+    const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
+    i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (X ? g.outS : g.outR);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nid = sm.nid;
+    uint32_t *wc = sm.wcnt[wave];
+    auto load = [&](uint32_t c0, i64x2 (&rows)[kBgIt], uint32_t &vm) {
+        vm = 0;
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) {
+            const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
+            rows[i] = i64x2{0, 0};
+            if (v < v1) {
+                rows[i] = tB[bg_src_blk(sm, X, v)];
+                vm |= 1u << i;
+            }
+        }
+    };
+    i64x2 cur[kBgIt];
+    uint32_t vmask;
+    load(v0, cur, vmask);
+    for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
+        i64x2 nxt[kBgIt];
+        uint32_t vnext = 0;
+        if (c0 + kGroupCap < v1) load(c0 + kGroupCap, nxt, vnext);
+        for (int i = lane; i < kBgIds; i += 64) wc[i] = 0;  // this wave's counters (read by this wave only below)
+        uint32_t dig[kBgIt], pos[kBgIt];
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++)
+            dig[i] = ((vmask >> i) & 1u) ? (uint32_t)sm.id[(uint32_t)((uint64_t)(tb.key ? cur[i].y : cur[i].x) -
+                                                                     (uint64_t)g.base)]
+                                         : 0u;
+        bg_rank<kBgIt, 8>(dig, vmask, wc, lane, pos);  // pos = rank among the wave's rows of the id
+        __syncthreads();
+        if (tid < (int)nid) {  // id tid: the waves' first rows, then the running start advanced
+            const uint32_t r = sm.rid[tid];
+            uint32_t run = sm.end[X][r];
+#pragma unroll
+            for (int w = 0; w < kMsdWaves; w++) {
+                const uint32_t c = sm.wcnt[w][tid];
+                sm.wcnt[w][tid] = run;
+                run += c;
+            }
+            sm.end[X][r] = run;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++)
+            if ((vmask >> i) & 1u) dst[wc[dig[i]] + pos[i]] = cur[i];
+#pragma unroll
+        for (int i = 0; i < kBgIt; i++) cur[i] = nxt[i];
+        vmask = vnext;
+        // no barrier: a wave zeroes and reads only its own counter row, and the
+        // id threads of the next chunk write after its first barrier
     }
 }
 
@@ -3115,11 +3295,23 @@ __device__ __forceinline__ void bg_jst_from_ends(BgSmem &sm) {
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kMsdThreads, 3) void msd_big_stage_kernel(const MsdFinalParams p) {
+// SMJ_STAMPS builds, p.dbg bit 5: cycles per oversized group by size class
+// (log2 of its larger table's rows: [0..31]), groups per class, and cycles per
+// phase (lists, count, starts, scatter, join) -> smj_debug_big_times
+__device__ unsigned long long g_bg_cls[2][32], g_bg_ph[8];
+#define BG_STAMP(k)                                                              \
+    if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) {                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+        atomicAdd(&g_bg_ph[k], t_ - bg_t);                                       \
+        bg_t = t_;                                                               \
+    }
+
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
     const uint32_t nbig = p.plan->nbig;
     const int tid = threadIdx.x;
     const bool join = p.join && p.ntab > 1;
+    unsigned long long bg_t = 0, bg_g = 0;
     // dynamic tickets over the (unordered) list, twice: the groups over
     // kBgLarge rows first, so that the longest ones do not start last
     for (int round = 0; round < 2; round++)
@@ -3145,22 +3337,35 @@ __global__ __launch_bounds__(kMsdThreads, 3) void msd_big_stage_kernel(const Msd
         }
         if (!bg_ok(g, p.bg_max)) continue;  // block-uniform: a giant, or left to the host fallback
         if ((max(g.nR, g.nS) > kBgLarge) != (round == 0)) continue;
+        if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) bg_g = bg_t = __builtin_amdgcn_s_memtime();
         for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
         bg_lists(p, g, sm);
+        bg_blocks(sm, 0, g.nR, 0, g.nR);
+        if (p.ntab > 1) bg_blocks(sm, 1, g.nS, 0, g.nS);
+        BG_STAMP(0);
         if (!(SMJ_BG_ABL & 1)) {  // pass 1: residual counts of both tables
             bg_count<0>(p, g, 0, g.nR, sm, sm.end[0]);
             if (p.ntab > 1) bg_count<1>(p, g, 0, g.nS, sm, sm.end[1]);
         }
         __syncthreads();
+        BG_STAMP(1);
+        bg_build_ids(sm);
         const uint32_t J = bg_starts(sm, join, false);
         if (tid == 0) {
             p.counts[gi] = J;
             atomicAdd(&p.plan->nbigdev, 1u);
         }
+        BG_STAMP(2);
         if (!(SMJ_BG_ABL & 2)) {  // pass 2
-            bg_scatter<0>(p, g, 0, g.nR, sm);
-            if (p.ntab > 1) bg_scatter<1>(p, g, 0, g.nS, sm);
+            if (sm.nid <= (uint32_t)kBgIds) {
+                bg_scatter_ids<0>(p, g, 0, g.nR, sm);
+                if (p.ntab > 1) bg_scatter_ids<1>(p, g, 0, g.nS, sm);
+            } else {
+                bg_scatter<0>(p, g, 0, g.nR, sm);
+                if (p.ntab > 1) bg_scatter<1>(p, g, 0, g.nS, sm);
+            }
         }
+        BG_STAMP(3);
         if (join && !(SMJ_BG_ABL & 4)) {  // join rows from the sorted output ranges (written above by this workgroup)
             // workgroup scope is enough: only this workgroup's own rows are read
             // back, from the CU that wrote them.  (__threadfence()'s agent scope
@@ -3170,7 +3375,23 @@ __global__ __launch_bounds__(kMsdThreads, 3) void msd_big_stage_kernel(const Msd
             bg_jst_from_ends(sm);
             bg_join(p, g, 0, J, sm, true);
         }
+        BG_STAMP(4);
+        if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) {
+            const int c = 31 - __clz(max(max(g.nR, g.nS), 1u));
+            atomicAdd(&g_bg_cls[0][c], bg_t - bg_g);
+            atomicAdd(&g_bg_cls[1][c], 1ull);
+        }
     }
+}
+
+hipError_t read_big_times(unsigned long long *out72) {
+    hipError_t e = hipMemcpyFromSymbol(out72, HIP_SYMBOL(g_bg_cls), sizeof(g_bg_cls));
+    if (e != hipSuccess) return e;
+    e = hipMemcpyFromSymbol(out72 + 64, HIP_SYMBOL(g_bg_ph), sizeof(g_bg_ph));
+    if (e != hipSuccess) return e;
+    static const unsigned long long z[64] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_bg_cls), z, sizeof(g_bg_cls));
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bg_ph), z, sizeof(g_bg_ph));
 }
 
 // Groups over kBgMaxRows rows (the largest Zipf groups: up to ~1e6 rows, one
@@ -3197,6 +3418,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_count_kernel(const M
         for (int i = threadIdx.x; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
         bg_lists(p, g, sm);
         const uint32_t v0 = jb.s * p.bg_seg;
+        bg_blocks(sm, 0, g.nR, min(v0, g.nR), min(v0 + p.bg_seg, g.nR));
+        if (p.ntab > 1) bg_blocks(sm, 1, g.nS, min(v0, g.nS), min(v0 + p.bg_seg, g.nS));
         bg_count<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm, sm.end[0]);
         if (p.ntab > 1) bg_count<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm, sm.end[1]);
         __syncthreads();
@@ -3246,6 +3469,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const
         const MsdGroup g = p.groups[jb.gi];
         uint32_t pre[2][RP];
         giant_totals(p, jb, sm, pre);
+        bg_build_ids(sm);
         bg_starts(sm, join, false);
 #pragma unroll
         for (int x = 0; x < 2; x++)
@@ -3253,8 +3477,15 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const
             for (int j = 0; j < RP; j++) sm.end[x][threadIdx.x * RP + j] += pre[x][j];
         bg_lists(p, g, sm);  // (its barrier also orders the starts above)
         const uint32_t v0 = jb.s * p.bg_seg;
-        bg_scatter<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm);
-        if (p.ntab > 1) bg_scatter<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm);
+        bg_blocks(sm, 0, g.nR, min(v0, g.nR), min(v0 + p.bg_seg, g.nR));
+        if (p.ntab > 1) bg_blocks(sm, 1, g.nS, min(v0, g.nS), min(v0 + p.bg_seg, g.nS));
+        if (sm.nid <= (uint32_t)kBgIds) {
+            bg_scatter_ids<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm);
+            if (p.ntab > 1) bg_scatter_ids<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm);
+        } else {
+            bg_scatter<0>(p, g, min(v0, g.nR), min(v0 + p.bg_seg, g.nR), sm);
+            if (p.ntab > 1) bg_scatter<1>(p, g, min(v0, g.nS), min(v0 + p.bg_seg, g.nS), sm);
+        }
         __syncthreads();
     }
 }
@@ -3278,6 +3509,68 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_join_kernel(const Ms
         if (join && j0 < J) bg_join(p, g, j0, min(J, j0 + p.bg_seg), sm, false);
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// partitioned mode: the index of the virtual tables (MsdVirt)
+// ---------------------------------------------------------------------------
+// block p: pre[p][t] = rows of part p in level-1 tiles < t, t in [0, ntiles1]
+// (each thread sums a contiguous range of tiles, then a block scan)
+__global__ __launch_bounds__(1024) void msd_virt_pre_kernel(const uint32_t *__restrict__ offs, int64_t ntiles1,
+                                                            int width, uint32_t *__restrict__ pre) {
+    __shared__ uint32_t s_wsum[16];
+    const int part = blockIdx.x, tid = threadIdx.x;
+    const int64_t per = (ntiles1 + 1023) / 1024, t0 = min((int64_t)tid * per, ntiles1), t1 = min(t0 + per, ntiles1);
+    uint32_t sum = 0;
+    for (int64_t t = t0; t < t1; t++) sum += offs[t * width + part + 1] - offs[t * width + part];
+    uint32_t all;
+    uint32_t ex = block_excl_scan<16>(sum, s_wsum, &all);
+    uint32_t *out = pre + (int64_t)part * (ntiles1 + 1);
+    for (int64_t t = t0; t < t1; t++) {
+        out[t] = ex;
+        ex += offs[t * width + part + 1] - offs[t * width + part];
+    }
+    if (tid == 0) out[ntiles1] = all;
+}
+
+// seg[p][j]: the level-1 segments of virtual tile j of part p (rows
+// [j vt, j vt + vt) of the part): the tile holding its first row (a search
+// over pre), then the following non-empty tiles up to the tile's end
+__global__ __launch_bounds__(256) void msd_virt_seg_kernel(const uint32_t *__restrict__ offs, int width,
+                                                           const uint32_t *__restrict__ pre, int64_t ntiles1,
+                                                           MsdVSeg *__restrict__ seg, int64_t vcap, int vt, int T1) {
+    const int part = blockIdx.y;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t *pp = pre + (int64_t)part * (ntiles1 + 1);
+    const uint32_t rows = pp[ntiles1];
+    if (j >= vcap || (uint64_t)j * vt >= rows) return;
+    const uint32_t v0 = (uint32_t)(j * vt), v1 = (uint32_t)min((int64_t)v0 + vt, (int64_t)rows);
+    uint32_t lo = 0, hi = (uint32_t)ntiles1 - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pp[mid] <= v0) lo = mid; else hi = mid - 1;
+    }
+    MsdVSeg &g = seg[(int64_t)part * vcap + j];
+    uint32_t n = 0;
+    for (int64_t t = lo; t < ntiles1 && pp[t] < v1; t++) {
+        if (pp[t + 1] == pp[t]) continue;  // no rows of this part in tile t
+        if (n < (uint32_t)kVSegs) {
+            const uint32_t s0 = max(pp[t], v0);
+            g.phys[n] = t * T1 + offs[t * width + part] + (s0 - pp[t]);
+            g.v0[n] = s0 - v0;
+        }
+        n++;
+    }
+    g.n = n;
+}
+
+hipError_t launch_msd_virt_index(const uint32_t *offs, int64_t ntiles1, int width, int nparts, uint32_t *pre,
+                                 MsdVSeg *seg, int64_t vcap, int vt_rows, int T1, hipStream_t s) {
+    if (ntiles1 <= 0 || nparts <= 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_virt_pre_kernel, dim3(nparts), dim3(1024), 0, s, offs, ntiles1, width, pre);
+    hipLaunchKernelGGL(msd_virt_seg_kernel, dim3((unsigned)((vcap + 255) / 256), nparts), dim3(256), 0, s, offs,
+                       width, pre, ntiles1, seg, vcap, vt_rows, T1);
+    return hipGetLastError();
 }
 
 static const unsigned long long zero8_pb[8] = {0};
@@ -3650,10 +3943,14 @@ hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s) {
 
 // resident workgroups of a `threads`-thread kernel on the current device
 // (occupancy x CUs), cached per kernel and LDS pad
+// resident workgroups of `kernel` on the whole device, cached per kernel and
+// LDS pad (kernels of one signature share K: the cache is keyed by address)
 template <class K>
 static int64_t resident_blocks(K kernel, int threads, size_t dyn_lds) {
-    static int cached[2] = {0, 0};
-    int &c = cached[dyn_lds ? 1 : 0];
+    static std::mutex mu;
+    static std::map<std::pair<const void *, size_t>, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    int &c = cache[{reinterpret_cast<const void *>(kernel), dyn_lds}];
     if (!c) {
         int dev = 0, per = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -3694,8 +3991,11 @@ hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s) {
 
 // oversized multi-key groups of a small key span (2-column tables; the
 // rest: host fallback), launched by the host once the plan shows some
-hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s) {
+hipError_t launch_msd_big(const MsdFinalParams &p_in, hipStream_t s) {
     static const unsigned bg_grid = (unsigned)resident_blocks(msd_big_stage_kernel, kMsdThreads, 0);
+    static const int dbg = getenv("SMJ_DEBUG_BIG") ? 32 : 0;
+    MsdFinalParams p = p_in;
+    p.dbg |= dbg;
     hipLaunchKernelGGL(msd_big_stage_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
     // the groups over the one-workgroup limit it registered, as jobs (no-ops without)
     hipLaunchKernelGGL(msd_giant_count_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);

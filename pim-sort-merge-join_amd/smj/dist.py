@@ -66,19 +66,30 @@ class HipOps:
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
+_SAMPLE_IDX = {}
+
+
 def sample_index(n, samples, device=None):
     """min(samples, n) row indices spread evenly over [0, n - 1], in exact
     int64 arithmetic (a float32 linspace rounds n - 1 up to n above 2^24 rows
-    and would read past the table)."""
-    k = min(samples, n)
-    return torch.arange(k, dtype=torch.int64, device=device) * (n - 1) // max(k - 1, 1)
+    and would read past the table).  Cached per (n, samples, device): the
+    same slices come back every step."""
+    key = (n, samples, str(device))
+    idx = _SAMPLE_IDX.get(key)
+    if idx is None:
+        k = min(samples, n)
+        idx = torch.arange(k, dtype=torch.int64, device=device) * (n - 1) // max(k - 1, 1)
+        if len(_SAMPLE_IDX) > 64:
+            _SAMPLE_IDX.clear()
+        _SAMPLE_IDX[key] = idx
+    return idx
 
 
 def _sample_keys(table, key_col, samples):
     n = table.shape[0]
     if n == 0:
         return table.new_empty((0,))
-    return table[sample_index(n, samples, table.device), key_col].contiguous()
+    return table[:, key_col].index_select(0, sample_index(n, samples, table.device))
 
 
 def _wire_device(t, group=None):
@@ -288,6 +299,37 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     loopback = (LOOPBACK if loopback is None else loopback) and dist.is_initialized()
     if world == 1 and not loopback:
         return ops.sort_merge_join(R, S, k1, k2, (sc1, sv1), (sc2, sv2))[2]
+    if not R.is_cuda:
+        return _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback,
+                                world, rank)
+    # The local work runs on a high-priority stream of its own.  RCCL's
+    # point-to-point kernels run on the process group's stream; HIP multiplexes
+    # streams onto GPU_MAX_HW_QUEUES hardware queues, and a trace of the
+    # one-GPU loopback (profiles/r03c_loopback_trace.txt) found RCCL's stream
+    # and torch's default stream on the SAME queue: every exchange kernel then
+    # ran between two pipeline kernels instead of beside them.
+    caller = torch.cuda.current_stream(R.device)
+    cs = _compute_stream(R.device)
+    cs.wait_stream(caller)
+    with torch.cuda.stream(cs):
+        J = _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback,
+                             world, rank)
+    caller.wait_stream(cs)
+    J.record_stream(caller)
+    return J
+
+
+_STREAMS = {}
+
+
+def _compute_stream(device):
+    s = _STREAMS.get(device)
+    if s is None:
+        s = _STREAMS[device] = torch.cuda.Stream(device=device, priority=-1)
+    return s
+
+
+def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
     nseg = world * K
 

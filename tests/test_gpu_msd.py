@@ -238,6 +238,40 @@ def test_small_span_oversized_groups_on_device(gpu, oracle_built, monkeypatch, k
     np.testing.assert_array_equal(host(gS1), Ss.reshape(-1, 2))
 
 
+@pytest.mark.parametrize("giant", [False, True])
+def test_oversized_groups_many_distinct_keys(gpu, oracle_built, monkeypatch, giant):
+    """Oversized groups of a small key span but with more distinct keys than
+    the parallel ranking's 256 compact ids (dense clusters: ~3,000 rows over
+    ~2,000 consecutive key values inside a sparse 2^31 key range) take the
+    wave-serial ranking; clusters of < 256 distinct keys take the compact-id
+    one -- both in one call, bit-exact against the oracle."""
+    from smj import ops
+    if giant:
+        monkeypatch.setenv("SMJ_BG_MAX_ROWS", "2048")
+        monkeypatch.setenv("SMJ_BG_SEG", "2048")
+    rng = np.random.default_rng(5)
+    centers = rng.choice(1 << 20, 60, replace=False).astype(np.int64) * 2048
+
+    def make(n, pay0):
+        keys = [rng.integers(0, 1 << 31, n)]
+        for i, c in enumerate(centers):
+            width = 2200 if i % 2 == 0 else 150  # > 256 distinct keys / a narrow one
+            keys.append(c + rng.integers(0, width, 3000 + 40 * i))
+        k = rng.permutation(np.concatenate(keys))
+        t = np.empty((len(k), 2), dtype=np.int64)
+        t[:, 0] = k
+        t[:, 1] = pay0 + np.arange(len(k))
+        return t
+
+    R, S = make(2_000_000, 0), make(1_700_000, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, None, None)
+    assert ops.msd_bigdev() > 0, (ops.msd_stats(), ops.msd_bigdev())
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
 @pytest.mark.parametrize("n,cols,kind", [(100_000, 2, "uniform"), (70_000, 3, "dups"), (4097, 2, "wide")])
 def test_lsd_select_sort_matches_oracle(gpu, oracle_built, n, cols, kind):
     from smj import ops
