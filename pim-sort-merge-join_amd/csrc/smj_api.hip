@@ -484,13 +484,6 @@ struct MsdScratch {
     int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
     void *giant = nullptr, *gmap = nullptr, *gh = nullptr;  // msd_giant_*: groups, job map, job counts
     size_t c_giant = 0, c_gmap = 0, c_gh = 0;
-    // partitioned mode, per table: the level-1 split (rows, part starts per
-    // tile, min / max per tile), the parts' tile prefixes, virtual tile starts
-    // and part sizes (MsdVirt)
-    enum { L_ROWS, L_OFFS, L_TMM, L_PRE, L_VSTART, L_TOT, L_N };
-    void *L[2][L_N] = {};
-    size_t cL[2][L_N] = {};
-    uint32_t *h_tot = nullptr;  // pinned: part sizes of both tables
 };
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
@@ -533,10 +526,9 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.radix_list, sizeof(uint32_t) * kSlots));
         HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
         HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
-        HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 256));
+        HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 64));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc(&m.h_tot, sizeof(uint32_t) * 2 * 64, hipHostMallocDefault));
         m.dev = dev;  // only once every buffer exists (a failed call retries the allocation)
     }
     *out = &m;
@@ -555,11 +547,8 @@ void msd_free_all() {
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                         (void *)m.lspl, m.giant, m.gmap, m.gh})
             hipFree(p);
-        for (auto &tl : m.L)
-            for (void *p : tl) hipFree(p);
         hipHostFree(m.h_plan);
         hipHostFree(m.h_samp);
-        hipHostFree(m.h_tot);
     }
     g_msd.clear();
 }
@@ -570,7 +559,6 @@ struct MsdIn {            // one input table of the pipeline
     int cols, use_sel, sel_col, key;
     T sel_val;
     T *out;               // sorted selected rows
-    MsdVirt v;            // partitioned mode: the table is part v.part of a level-1 split (src unused)
 };
 
 // Records the index of the last profiling record (to patch its byte count
@@ -843,8 +831,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     {
         MsdSampleParams sp{};
         for (int x = 0; x < ntab; x++)
-            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val,
-                                 in[x].v};
+            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val};
         sp.ntab = ntab;
         sp.spl = ms->spl;
         sp.samp = ms->samp;
@@ -869,7 +856,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     MsdPartAParams pp[2];
     for (int x = 0; x < ntab; x++)
         pp[x] = MsdPartAParams{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
-                               (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm, in[x].v, 0};
+                               (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
     // both tables in one launch when nothing is staged and the widths agree (no tail between them)
     const bool pa_fused = !stg && ntab == 2 && in[0].cols == in[1].cols;
     if (pa_fused) {
@@ -978,7 +965,8 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     MsdFinalParams fp{};
     for (int x = 0; x < ntab; x++)
         fp.tab[x] = MsdTab{(const int64_t *)ms->t[x].tempB, (const uint16_t *)ms->t[x].offsB,
-                           (const MsdBucket *)ms->t[x].bk, in[x].out, TB_[x], in[x].cols, in[x].key, x};
+                           (const MsdBucket *)ms->t[x].bk, in[x].out, TB_[x], in[x].cols, in[x].key, x,
+                           maxB[x] * TB_[x]};
     fp.groups = ms->groups;
     fp.slots = (int64_t *)ms->slots;
     fp.counts = ms->counts;
@@ -1022,7 +1010,11 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (ms->h_plan->err) return SMJ_ERR_TIMEOUT;
+    if (ms->h_plan->err) {
+        fprintf(stderr, "smj: pipeline %s\n", (ms->h_plan->err & 1u) ? "look-back wait timed out"
+                                                                  : "run metadata inconsistent (SMJ_BOUNDS check)");
+        return (ms->h_plan->err & 1u) ? SMJ_ERR_TIMEOUT : SMJ_ERR_HIP;
+    }
     if (t_slot < 0) {
         g_msd_stats[0] = ms->h_plan->nsingle;
         g_msd_stats[1] = ms->h_plan->nbig;
@@ -1136,86 +1128,34 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         for (int64_t p = 1; p < P && !kw.empty(); p++) {
             const double target = W * (double)p / (double)P;
             while (i + 1 < kw.size() && acc + kw[i].second < target) acc += kw[i++].second;
-            const int64_t k = kw[i].first;  // part(key) = #{splitters < key}: key k closes part p - 1
+            const int64_t k = kw[i].first;  // bucket(key) = #{splitters < key}: key k closes part p - 1
             if (spl.empty() || spl.back() < k) spl.push_back(k);
         }
     }
-    const int nspl = (int)spl.size(), parts = nspl + 1;
-    {  // the level-1 digit searches 255 splitters: the unused ones never compare below a key
-        std::vector<int64_t> pad(256, INT64_MAX);
-        std::copy(spl.begin(), spl.end(), pad.begin());
-        HIP_TRY(hipMemcpyAsync(ms->lspl, pad.data(), sizeof(int64_t) * 256, hipMemcpyHostToDevice, s));
-    }
-    // 3. level-1 split (select + stable tile-local partition by part: part_a in
-    // range mode, one read and one write), then each part's index: the rows of
-    // part p in earlier tiles, and the level-1 tile of every virtual tile
-    int64_t tiles1[2] = {0, 0}, vcap[2] = {0, 0};
-    MsdPartAParams lp[2];
-    for (int x = 0; x < ntab; x++) {
-        const int T1 = msd_tile(in[x].cols);
-        tiles1[x] = std::max<int64_t>(1, (in[x].n + T1 - 1) / T1);
-        vcap[x] = in[x].n / T1 + 2;
-        void **L = ms->L[x];
-        size_t *cL = ms->cL[x];
-        SMJ_TRY(grow(&L[MsdScratch::L_ROWS], &cL[MsdScratch::L_ROWS], std::max<size_t>(1, in[x].n) * in[x].cols * 8));
-        SMJ_TRY(grow(&L[MsdScratch::L_OFFS], &cL[MsdScratch::L_OFFS], (size_t)tiles1[x] * (parts + 1) * 4));
-        SMJ_TRY(grow(&L[MsdScratch::L_TMM], &cL[MsdScratch::L_TMM], (size_t)tiles1[x] * 16));
-        SMJ_TRY(grow(&L[MsdScratch::L_PRE], &cL[MsdScratch::L_PRE], (size_t)parts * (tiles1[x] + 1) * 4));
-        SMJ_TRY(grow(&L[MsdScratch::L_VSTART], &cL[MsdScratch::L_VSTART], (size_t)parts * vcap[x] * sizeof(MsdVSeg)));
-        lp[x] = MsdPartAParams{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val,
-                               ms->lspl, (int64_t *)L[MsdScratch::L_ROWS], (uint32_t *)L[MsdScratch::L_OFFS],
-                               (int64_t *)L[MsdScratch::L_TMM], MsdVirt{}, parts};
-        if (in[x].n == 0) HIP_TRY(hipMemsetAsync(L[MsdScratch::L_OFFS], 0, (size_t)(parts + 1) * 4, s));
-    }
-    {
-        ProfScope ps("msd_part_split", 0, s);
-        if (ntab == 2 && in[0].cols == in[1].cols) {
-            HIP_TRY(launch_msd_part_a2(lp[0], lp[1], in[0].cols, s));
-        } else {
-            for (int x = 0; x < ntab; x++) HIP_TRY(launch_msd_part_a(lp[x], in[x].cols, s));
-        }
-    }
-    const size_t psplit = prof_last();
-    for (int x = 0; x < ntab; x++) {
-        void **L = ms->L[x];
-        uint32_t *pre = (uint32_t *)L[MsdScratch::L_PRE];
-        HIP_TRY(launch_msd_virt_index((const uint32_t *)L[MsdScratch::L_OFFS], tiles1[x], parts + 1, parts, pre,
-                                      (MsdVSeg *)L[MsdScratch::L_VSTART], vcap[x], msd_tile(in[x].cols),
-                                      msd_tile(in[x].cols), s));
-        for (int p = 0; p < parts; p++)  // the part sizes: pre[p][tiles1]
-            HIP_TRY(hipMemcpyAsync(ms->h_tot + x * 64 + p, pre + (int64_t)p * (tiles1[x] + 1) + tiles1[x], 4,
-                                   hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
+    const int nspl = (int)spl.size();
+    if (nspl) HIP_TRY(hipMemcpyAsync(ms->lspl, spl.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, s));
+    // 3. select + stable partition of every table straight into its output
+    // buffer (the parts are then sorted in place)
     std::vector<int64_t> cnt[2], off[2];
-    double split_bytes = 0;
     for (int x = 0; x < ntab; x++) {
-        cnt[x].assign(parts, 0);
-        off[x].assign(parts + 1, 0);
-        for (int p = 0; p < parts; p++) {
-            cnt[x][p] = ms->h_tot[x * 64 + p];
-            off[x][p + 1] = off[x][p] + cnt[x][p];
-        }
-        h_rows[x] = off[x][parts];
-        split_bytes += 8.0 * in[x].cols * ((double)in[x].n + (double)h_rows[x]);
+        cnt[x].assign(nspl + 1, 0);
+        if (in[x].n)
+            SMJ_TRY(smj_dev_partition(in[x].src, in[x].n, in[x].cols, in[x].use_sel, in[x].sel_col, in[x].sel_val,
+                                      in[x].key, ms->lspl, nspl, in[x].out, cnt[x].data(), s));
+        off[x].assign(nspl + 2, 0);
+        for (int p = 0; p <= nspl; p++) off[x][p + 1] = off[x][p] + cnt[x][p];
+        h_rows[x] = off[x][nspl + 1];
     }
-    prof_set_bytes(psplit, split_bytes);
-    // 4. the pipeline per part: part_a reads the part's rows through the
-    // index; parts ascend in key order, so part p's sorted rows start at the
-    // exclusive prefix of the part sizes and its joined rows follow part p - 1's
+    // 4. the pipeline per part, in place
     int64_t J = 0;
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
-    for (int p = 0; p < parts; p++) {
+    for (int p = 0; p <= nspl; p++) {
         MsdIn part[2];
         int np = 0;
         for (int x = 0; x < ntab; x++) {
             if (cnt[x][p] == 0) continue;
-            void **L = ms->L[x];
-            MsdVirt v{(const int64_t *)L[MsdScratch::L_ROWS], (const uint32_t *)L[MsdScratch::L_OFFS],
-                      (const uint32_t *)L[MsdScratch::L_PRE] + (int64_t)p * (tiles1[x] + 1),
-                      (const MsdVSeg *)L[MsdScratch::L_VSTART] + (int64_t)p * vcap[x], tiles1[x], parts + 1, p,
-                      msd_tile(in[x].cols)};
-            part[np++] = MsdIn{nullptr, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, in[x].out + off[x][p] * in[x].cols, v};
+            T *base = in[x].out + off[x][p] * in[x].cols;
+            part[np++] = MsdIn{base, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
         }
         int64_t rows[3] = {0, 0, 0};
         if (np == 2 && join) {

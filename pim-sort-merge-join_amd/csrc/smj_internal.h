@@ -209,46 +209,11 @@ constexpr int kMsdSegs = SMJ_MSD_SEGS;     // segments of the run scans (x 4 wav
 constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
 
-// Partitioned mode (smj_api.hip msd_large): part p of a table is a VIRTUAL
-// table -- its rows sit in the level-1 split's tiles (msd_part_a in range
-// mode: every level-1 tile holds its rows in part order), at
-// rows[t * T1 + offs[t * width + p] + i] for the i-th row of part p in tile t.
-// pre[t] = rows of part p in tiles < t (pre[ntiles1] = the part's size).
-// seg[j]: the level-1 segments of virtual tile j (msd_tile(cols) rows): its
-// k-th segment starts at tile row v0[k] and physical row phys[k]; part_a reads
-// it through scalar loads, so a tile costs one extra round trip, not a search.
-constexpr int kVSegs = 16;
-struct MsdVSeg {
-    int64_t phys[kVSegs];
-    uint32_t v0[kVSegs];
-    uint32_t n;              // segments (> kVSegs: part_a searches pre instead)
-    uint32_t pad[15];
-};
-struct MsdVirt {
-    const int64_t *rows;     // nullptr: a plain table (src)
-    const uint32_t *offs;
-    const uint32_t *pre;
-    const MsdVSeg *seg;
-    int64_t ntiles1;
-    int width, part, T1;
-};
-// virtual row v -> its physical row (a linear search from tile t, which must
-// not be past v's tile): the level-1 tiles between are few
-__device__ __forceinline__ int64_t virt_row(const MsdVirt &vt, uint32_t v) {
-    uint32_t lo = 0, hi = (uint32_t)vt.ntiles1 - 1;  // last tile with pre[t] <= v
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (vt.pre[mid] <= v) lo = mid; else hi = mid - 1;
-    }
-    return (int64_t)lo * vt.T1 + vt.offs[(int64_t)lo * vt.width + vt.part] + (v - vt.pre[lo]);
-}
-
 struct MsdTable {        // an input table as the sampler and part_a see it
     const int64_t *src;
     int64_t n;
     int cols, key_col, use_sel, sel_col;
     int64_t sel_val;
-    MsdVirt v;           // partitioned mode: src is part v.part of a level-1 split
 };
 struct MsdSampleParams {
     MsdTable tab[2];
@@ -265,10 +230,6 @@ struct MsdPartAParams {
     int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
     uint32_t *offs;      // [tiles][kOffsARow]
     int64_t *tmm;        // [tiles][2] min / max selected key
-    MsdVirt v;           // partitioned mode: the input is part v.part of a level-1 split
-    int range_parts;     // > 0: level-1 split of the partitioned mode -- digit = #{splitters < key}
-                         // (< range_parts), offs rows of range_parts + 1 entries (part starts + the
-                         // tile's selected rows)
 };
 struct MsdPartA2 {       // one part_a launch over up to two tables
     MsdPartAParams t[2];
@@ -301,7 +262,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t bgticket[2];// msd_big_stage_kernel's group tickets (large groups first, then the rest)
     uint32_t ngiant;     // groups over kBgMaxRows rows registered as jobs
     uint32_t njobs;      // their jobs
-    uint32_t err;        // != 0: a cross-workgroup wait gave up (msd_group_kernel) -> SMJ_ERR_TIMEOUT
+    uint32_t err;        // bit 0: a cross-workgroup wait gave up (msd_group_kernel) -> SMJ_ERR_TIMEOUT;
+                         // bit 1: inconsistent run metadata (SMJ_BOUNDS builds) -> SMJ_ERR_HIP
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)
@@ -353,6 +315,7 @@ struct MsdTab {          // a table as the final kernels see it
     const MsdBucket *bk;
     int64_t *out;        // sorted rows
     int tile, cols, key, x;
+    int64_t capB;        // rows tempB holds (SMJ_BOUNDS builds check gathers against it)
 };
 struct MsdFinalParams {
     MsdTab tab[2];
@@ -390,11 +353,6 @@ hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s);
 constexpr int kSampleGatherBlocksH = 2 * kSampleMax / 256;
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s);
-// partitioned mode: pre[p * (ntiles1 + 1) + t] per part from the level-1 offs
-// rows (width = nparts + 1), then seg[p * vcap + j] for the virtual tiles of
-// every part (vt_rows = msd_tile(cols), vcap >= rows / vt_rows + 2)
-hipError_t launch_msd_virt_index(const uint32_t *offs, int64_t ntiles1, int width, int nparts, uint32_t *pre,
-                                 MsdVSeg *seg, int64_t vcap, int vt_rows, int T1, hipStream_t s);
 // both tables (the same column count) in one launch: no tail between them
 hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, int cols, hipStream_t s);
 // tiles [t0, t1) only (their rows must be resident: the staged host path)

@@ -38,6 +38,9 @@
 
 // Phase stamps (tools/msd_phases.py) are compiled in only with -DSMJ_STAMPS=1
 // (they hold registers); at run time they also need SMJ_DEBUG_MSD=1.
+#ifndef SMJ_BOUNDS
+#define SMJ_BOUNDS 0  // debug builds: run metadata checked before the gathers it drives (plan->err bit 1)
+#endif
 #ifndef SMJ_STAMPS
 #define SMJ_STAMPS 0
 #endif
@@ -195,16 +198,6 @@ __device__ __forceinline__ uint32_t bucket_a(const int64_t *s_spl, int64_t k) {
     return (uint32_t)pos + (rep ? 1u : 0u);
 }
 
-// level-1 split of the partitioned mode: #{splitters < key} (the unused
-// splitters are INT64_MAX, never < key)
-__device__ __forceinline__ uint32_t bucket_range(const int64_t *s_spl, int64_t k) {
-    int pos = 0;
-#pragma unroll
-    for (int step = kBucketsA / 2; step >= 1; step >>= 1)
-        pos += (s_spl[pos + step - 1] < k) ? step : 0;
-    return (uint32_t)pos;
-}
-
 
 // ---------------------------------------------------------------------------
 // sample -> splitters
@@ -229,7 +222,7 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
                               ? jj
                               : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
                                                  jj % kSampleRun);
-        const int64_t *row = t.v.rows ? t.v.rows + virt_row(t.v, (uint32_t)r) * t.cols : t.src + r * t.cols;
+        const int64_t *row = t.src + r * t.cols;
         const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
         if (!t.use_sel || sv > t.sel_val) {
             k = kv;
@@ -332,34 +325,10 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     zero_counters<RADIX>(wc, lane);
     const int lrow0 = wave * ITEMS * 64 + lane;
     int64_t rows[ITEMS][COLS];
-    if (p.v.rows) {  // partitioned mode: this virtual tile's rows through its level-1 segments
-        const MsdVSeg &sg = p.v.seg[t];  // tile-uniform: scalar loads
-        const uint32_t ns = sg.n;
 #pragma unroll
-        for (int it = 0; it < ITEMS; it++) {
-            const uint32_t o = (uint32_t)min(lrow0 + it * 64, nrows - 1);
-            int64_t r;
-            if (ns <= (uint32_t)kVSegs) {
-                int64_t ph = sg.phys[0];
-                uint32_t b = 0;
-#pragma unroll
-                for (int k = 1; k < kVSegs; k++) {
-                    const bool in = (uint32_t)k < ns && sg.v0[k] <= o;
-                    ph = in ? sg.phys[k] : ph;
-                    b = in ? sg.v0[k] : b;
-                }
-                r = ph + (o - b);
-            } else {
-                r = virt_row(p.v, (uint32_t)row0 + o);
-            }
-            load_row<COLS>(p.v.rows + r * COLS, rows[it]);
-        }
-    } else {
-#pragma unroll
-        for (int it = 0; it < ITEMS; it++)
-            if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
-            else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
-    }
+    for (int it = 0; it < ITEMS; it++)
+        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
     __syncthreads();  // splitters
 
     uint32_t dig[ITEMS];
@@ -371,7 +340,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
         const bool pass = !p.use_sel | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
         const bool v = inb & pass;
         const int64_t k = pick<COLS>(rows[it], p.key_col);
-        dig[it] = v ? (p.range_parts ? bucket_range(s_spl, k) : bucket_a(s_spl, k)) : 0u;
+        dig[it] = v ? bucket_a(s_spl, k) : 0u;
         vmask |= v ? (1u << it) : 0u;
         mn = v ? min(mn, k) : mn;
         mx = v ? max(mx, k) : mx;
@@ -389,11 +358,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
     static_assert(RADIX < kMsdThreads && RADIX < kOffsARow, "one offsA entry per thread");
-    if (p.range_parts) {  // level-1 split: the part starts + the tile's selected rows
-        if (tid <= p.range_parts) p.offs[t * (p.range_parts + 1) + tid] = s_bin[tid];
-    } else if (tid <= RADIX) {
-        p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
-    }
+    if (tid <= RADIX) p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
     if (tid == 0) {
         p.tmm[2 * t] = mn;
         p.tmm[2 * t + 1] = mx;
@@ -2438,6 +2403,11 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
     for (int x = 0; x < 2; x++) {
         if (tid < g.kt[x] && x < p.ntab) {
             const uint32_t vs = x ? (ex >> 16) : (ex & 0xffffu);
+            if (SMJ_BOUNDS) {  // a run inside its pass-B tile, and the runs adding up to the group's rows
+                const uint32_t nx = x ? g.nS : g.nR;
+                if (o1[x] < o0[x] || o1[x] > (uint32_t)p.tab[x].tile || (tid + 1 == g.kt[x] && vs + len[x] != nx))
+                    atomicOr(&p.plan->err, 2u);
+            }
             sm.L.list[x][tid] = make_uint2((g.tb[x] + tid) * (uint32_t)p.tab[x].tile + o0[x], vs);
             if (len[x]) {
                 sm.L.at[x][vs] = (uint16_t)tid;
@@ -2464,7 +2434,12 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
                     const int64_t k = g.base + (int64_t)((v * 3u) % max(g.span, 1u));
                     r = {p.tab[x].key ? (int64_t)v : k, p.tab[x].key ? k : (int64_t)v};
                 } else {
-                    r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[e.x + (v - e.y)];
+                    int64_t ix = (int64_t)e.x + (v - e.y);
+                    if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
+                        atomicOr(&p.plan->err, 2u);
+                        ix = 0;
+                    }
+                    r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[ix];
                 }
             }
             rows[x][k] = r;
@@ -3023,6 +2998,10 @@ __device__ __forceinline__ void bg_lists(const MsdFinalParams &p, const MsdGroup
                 const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
                 src[i] = (uint32_t)id * (uint32_t)tb.tile + lo;
                 len[i] = hi - lo;
+                if (SMJ_BOUNDS && (hi < lo || hi > (uint32_t)tb.tile)) {
+                    atomicOr(&p.plan->err, 2u);
+                    len[i] = 0;
+                }
             }
             sum += len[i];
         }
@@ -3509,68 +3488,6 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_join_kernel(const Ms
         if (join && j0 < J) bg_join(p, g, j0, min(J, j0 + p.bg_seg), sm, false);
         __syncthreads();
     }
-}
-
-// ---------------------------------------------------------------------------
-// partitioned mode: the index of the virtual tables (MsdVirt)
-// ---------------------------------------------------------------------------
-// block p: pre[p][t] = rows of part p in level-1 tiles < t, t in [0, ntiles1]
-// (each thread sums a contiguous range of tiles, then a block scan)
-__global__ __launch_bounds__(1024) void msd_virt_pre_kernel(const uint32_t *__restrict__ offs, int64_t ntiles1,
-                                                            int width, uint32_t *__restrict__ pre) {
-    __shared__ uint32_t s_wsum[16];
-    const int part = blockIdx.x, tid = threadIdx.x;
-    const int64_t per = (ntiles1 + 1023) / 1024, t0 = min((int64_t)tid * per, ntiles1), t1 = min(t0 + per, ntiles1);
-    uint32_t sum = 0;
-    for (int64_t t = t0; t < t1; t++) sum += offs[t * width + part + 1] - offs[t * width + part];
-    uint32_t all;
-    uint32_t ex = block_excl_scan<16>(sum, s_wsum, &all);
-    uint32_t *out = pre + (int64_t)part * (ntiles1 + 1);
-    for (int64_t t = t0; t < t1; t++) {
-        out[t] = ex;
-        ex += offs[t * width + part + 1] - offs[t * width + part];
-    }
-    if (tid == 0) out[ntiles1] = all;
-}
-
-// seg[p][j]: the level-1 segments of virtual tile j of part p (rows
-// [j vt, j vt + vt) of the part): the tile holding its first row (a search
-// over pre), then the following non-empty tiles up to the tile's end
-__global__ __launch_bounds__(256) void msd_virt_seg_kernel(const uint32_t *__restrict__ offs, int width,
-                                                           const uint32_t *__restrict__ pre, int64_t ntiles1,
-                                                           MsdVSeg *__restrict__ seg, int64_t vcap, int vt, int T1) {
-    const int part = blockIdx.y;
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t *pp = pre + (int64_t)part * (ntiles1 + 1);
-    const uint32_t rows = pp[ntiles1];
-    if (j >= vcap || (uint64_t)j * vt >= rows) return;
-    const uint32_t v0 = (uint32_t)(j * vt), v1 = (uint32_t)min((int64_t)v0 + vt, (int64_t)rows);
-    uint32_t lo = 0, hi = (uint32_t)ntiles1 - 1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (pp[mid] <= v0) lo = mid; else hi = mid - 1;
-    }
-    MsdVSeg &g = seg[(int64_t)part * vcap + j];
-    uint32_t n = 0;
-    for (int64_t t = lo; t < ntiles1 && pp[t] < v1; t++) {
-        if (pp[t + 1] == pp[t]) continue;  // no rows of this part in tile t
-        if (n < (uint32_t)kVSegs) {
-            const uint32_t s0 = max(pp[t], v0);
-            g.phys[n] = t * T1 + offs[t * width + part] + (s0 - pp[t]);
-            g.v0[n] = s0 - v0;
-        }
-        n++;
-    }
-    g.n = n;
-}
-
-hipError_t launch_msd_virt_index(const uint32_t *offs, int64_t ntiles1, int width, int nparts, uint32_t *pre,
-                                 MsdVSeg *seg, int64_t vcap, int vt_rows, int T1, hipStream_t s) {
-    if (ntiles1 <= 0 || nparts <= 0) return hipSuccess;
-    hipLaunchKernelGGL(msd_virt_pre_kernel, dim3(nparts), dim3(1024), 0, s, offs, ntiles1, width, pre);
-    hipLaunchKernelGGL(msd_virt_seg_kernel, dim3((unsigned)((vcap + 255) / 256), nparts), dim3(256), 0, s, offs,
-                       width, pre, ntiles1, seg, vcap, vt_rows, T1);
-    return hipGetLastError();
 }
 
 static const unsigned long long zero8_pb[8] = {0};

@@ -107,16 +107,23 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
     padded with INT64_MAX, plus its valid count), the sort and the order
     statistics on the device, one device -> host copy of the result."""
     parts = parts or world
-    local = torch.cat([_sample_keys(t, k, samples) for t, k in tables_and_keys])
-    dev = _wire_device(local, group)
-    local = local.to(dev)
+    home = tables_and_keys[0][0].device
+    dev = _wire_device(tables_and_keys[0][0], group)
     cap = len(tables_and_keys) * samples
-    buf = torch.full((cap + 1,), INT64_MAX, dtype=torch.int64, device=dev)
-    buf[0] = local.numel()
-    buf[1: 1 + local.numel()] = local
-    all_buf = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(all_buf, buf, group=group)
-    allb = torch.stack(all_buf)
+    # [count, keys..., INT64_MAX pads]: the sampled keys are gathered straight
+    # into their slice (on the wire device when the transport is gloo)
+    buf = torch.full((cap + 1,), INT64_MAX, dtype=torch.int64, device=home)
+    at = 1
+    for t, k in tables_and_keys:
+        n = t.shape[0]
+        if n:
+            idx = sample_index(n, samples, t.device)
+            torch.index_select(t[:, k], 0, idx, out=buf[at: at + idx.numel()])
+            at += idx.numel()
+    buf[0] = at - 1
+    buf = buf.to(dev)
+    allb = torch.empty((world, cap + 1), dtype=torch.int64, device=dev)
+    dist.all_gather(list(allb.unbind(0)), buf, group=group)  # rows of allb (gloo has no all_gather_into_tensor)
     L = allb[:, 0].sum()
     # the pads sort last (a real INT64_MAX key sorts among them: the same value)
     keys = torch.sort(allb[:, 1:].reshape(-1)).values

@@ -12,3 +12,5 @@ SMJ_LIB=pim-sort-merge-join_amd/lib/variants/stamps/libsmj_hip.so SMJ_DEBUG_BIG=
 python3 -c "import json; d=json.load(open('$O/big_times.json')); print(d['msd_big_dev_ms'], d['phases'], {k: v['cycles_per_group'] for k, v in d['classes'].items()})"
 timeout -k 10 300 python bench.py --cpu-sample 0 --cpu-mt 0 > $O/c3.json 2> $O/c3.err || { echo "c3 rc=$?"; tail -20 $O/c3.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/c3.json')); print('c3', d['ms_per_step'])"
+SMJ_LIB=pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_msd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/bounds_tests.out 2>&1 || { echo "bounds tests rc=$?"; tail -40 $O/bounds_tests.out; exit 1; }
+tail -1 $O/bounds_tests.out
