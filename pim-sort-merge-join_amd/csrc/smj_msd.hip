@@ -1287,6 +1287,9 @@ __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams
         const uint32_t k0 = (uint32_t)(((uint64_t)K * sl) / kGroupSlices), k1 = (uint32_t)(((uint64_t)K * (sl + 1)) / kGroupSlices);
         const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
         static_assert(SB == 8 && kOffsB % 8 == 0, "one 16-B load of 8 starts per row (rows 16-B aligned)");
+        if (bk.one_key) {  // a heavy key's bucket: every row is in sub-bucket 0 (C5: thousands of tiles)
+            if (sl == 0 && t == 0) tot[0] = bk.L;
+        } else
 #pragma unroll 4
         for (uint32_t k = k0; k < k1; k++) {
             const uint16_t *r = o + (int64_t)k * kOffsB;
@@ -1317,6 +1320,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     __shared__ uint16_t s_nz[kRadB + 1];            // positions of the non-empty sub-buckets, in order
     __shared__ uint16_t s_cnz[kRadB + 1];           // non-empty sub-buckets before position q
     __shared__ uint32_t s_base;
+    __shared__ uint32_t s_nl[2], s_lb[2];  // this bucket's single / oversized groups: count, then list base
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];   // groups: sub-buckets [b0, b1)
     __shared__ int s_ng;
@@ -1460,7 +1464,16 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         __syncthreads();
     }
     const uint32_t base = s_base;
-    for (int j = t; j < s_ng; j += kGroupThreads) {
+    // the streamed / oversized lists: slots counted in LDS, one global
+    // reservation per list and bucket (C5: ~10^4 flagged groups per call --
+    // one global atomic each serialised on one L2 address, 0.13 ms per launch)
+    if (t < 2) s_nl[t] = 0;
+    __syncthreads();
+    constexpr int GPT = kRadB / kGroupThreads;  // groups per thread (j = t + i * kGroupThreads)
+    uint32_t lslot[GPT], lgi[GPT], lkind[GPT];
+#pragma unroll
+    for (int i = 0; i < GPT; i++) lkind[i] = 0;
+    for (int j = t, i = 0; j < s_ng; j += kGroupThreads, i++) {
         const uint32_t b0 = s_g0[j], b1 = s_g1[j];
         MsdGroup gr{};
         gr.a = (uint16_t)a;
@@ -1501,11 +1514,23 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         uint32_t cnt = 0;
         if (gr.flags == kGroupSingle) {
             cnt = min(gr.nR, gr.nS);
-            p.single_list[atomicAdd(&p.plan->nsingle, 1u)] = gi;
+            lkind[i] = 1;
+            lslot[i] = atomicAdd(&s_nl[0], 1u);
+            lgi[i] = gi;
         } else if (gr.flags == kGroupBig) {
-            p.big_list[atomicAdd(&p.plan->nbig, 1u)] = gi;
+            lkind[i] = 2;
+            lslot[i] = atomicAdd(&s_nl[1], 1u);
+            lgi[i] = gi;
         }
         p.counts[gi] = cnt;
+    }
+    __syncthreads();
+    if (t < 2) s_lb[t] = s_nl[t] ? atomicAdd(t ? &p.plan->nbig : &p.plan->nsingle, s_nl[t]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < GPT; i++) {
+        if (lkind[i] == 1) p.single_list[s_lb[0] + lslot[i]] = lgi[i];
+        if (lkind[i] == 2) p.big_list[s_lb[1] + lslot[i]] = lgi[i];
     }
 }
 
@@ -3129,63 +3154,83 @@ __device__ __forceinline__ void bg_build_ids(BgSmem &sm) {
 // the waves' first output rows (running start end[r] + the earlier waves'
 // rows) and advances end[r].  Two barriers per chunk instead of eight waves
 // in turn.
+// one chunk of kGroupCap rows of table X (rows in input order = wave, item,
+// lane; vmask: valid items) to their places by the parallel ranking
 template <int X>
-__device__ __forceinline__ void bg_scatter_ids(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
-                                               BgSmem &sm) {
+__device__ __forceinline__ void bg_place_ids(const MsdFinalParams &p, const MsdGroup &g, const i64x2 (&cur)[kBgIt],
+                                             uint32_t vmask, BgSmem &sm) {
     const MsdTab &tb = p.tab[X];
-    const i64x2 *tB = reinterpret_cast<const i64x2 *>(tb.tempB);
     i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (X ? g.outS : g.outR);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nid = sm.nid;
     uint32_t *wc = sm.wcnt[wave];
-    auto load = [&](uint32_t c0, i64x2 (&rows)[kBgIt], uint32_t &vm) {
-        vm = 0;
+    for (int i = lane; i < kBgIds; i += 64) wc[i] = 0;  // this wave's counters (read by this wave only below)
+    uint32_t dig[kBgIt], pos[kBgIt];
 #pragma unroll
-        for (int i = 0; i < kBgIt; i++) {
-            const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
-            rows[i] = i64x2{0, 0};
-            if (v < v1) {
-                rows[i] = tB[bg_src_blk(sm, X, v)];
-                vm |= 1u << i;
-            }
+    for (int i = 0; i < kBgIt; i++)
+        dig[i] = ((vmask >> i) & 1u)
+                     ? (uint32_t)sm.id[(uint32_t)((uint64_t)(tb.key ? cur[i].y : cur[i].x) - (uint64_t)g.base)]
+                     : 0u;
+    bg_rank<kBgIt, 8>(dig, vmask, wc, lane, pos);  // pos = rank among the wave's rows of the id
+    __syncthreads();
+    if (tid < (int)nid) {  // id tid: the waves' first rows, then the running start advanced
+        const uint32_t r = sm.rid[tid];
+        uint32_t run = sm.end[X][r];
+#pragma unroll
+        for (int w = 0; w < kMsdWaves; w++) {
+            const uint32_t c = sm.wcnt[w][tid];
+            sm.wcnt[w][tid] = run;
+            run += c;
         }
-    };
+        sm.end[X][r] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBgIt; i++)
+        if ((vmask >> i) & 1u) dst[wc[dig[i]] + pos[i]] = cur[i];
+    // no barrier: a wave zeroes and reads only its own counter row, and the id
+    // threads of the next chunk write after its first barrier
+}
+
+// row v of table X's group sequence, input-order mapping of chunk c0
+template <int X>
+__device__ __forceinline__ void bg_load_chunk(const MsdFinalParams &p, const BgSmem &sm, uint32_t c0, uint32_t v1,
+                                              i64x2 (&rows)[kBgIt], uint32_t &vm) {
+    const i64x2 *tB = reinterpret_cast<const i64x2 *>(p.tab[X].tempB);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    vm = 0;
+#pragma unroll
+    for (int i = 0; i < kBgIt; i++) {
+        const uint32_t v = c0 + (uint32_t)(wave * kBgIt + i) * 64u + (uint32_t)lane;
+        rows[i] = i64x2{0, 0};
+        if (v < v1) {
+            rows[i] = tB[bg_src_blk(sm, X, v)];
+            vm |= 1u << i;
+        }
+    }
+}
+
+// bg_scatter with the waves ranking in parallel (the group has <= kBgIds
+// distinct residuals): per chunk of kGroupCap rows (input order = wave,
+// item, lane) each wave ranks its rows by ballots on the 8-bit compact id and
+// counts them per id; one thread per id then turns the per-wave counts into
+// the waves' first output rows (running start end[r] + the earlier waves'
+// rows) and advances end[r].  Two barriers per chunk instead of eight waves
+// in turn.
+template <int X>
+__device__ __forceinline__ void bg_scatter_ids(const MsdFinalParams &p, const MsdGroup &g, uint32_t v0, uint32_t v1,
+                                               BgSmem &sm) {
     i64x2 cur[kBgIt];
     uint32_t vmask;
-    load(v0, cur, vmask);
+    bg_load_chunk<X>(p, sm, v0, v1, cur, vmask);
     for (uint32_t c0 = v0; c0 < v1; c0 += kGroupCap) {
-        i64x2 nxt[kBgIt];
+        i64x2 nxt[kBgIt];  // the next chunk's rows are in flight while this one is ranked and stored
         uint32_t vnext = 0;
-        if (c0 + kGroupCap < v1) load(c0 + kGroupCap, nxt, vnext);
-        for (int i = lane; i < kBgIds; i += 64) wc[i] = 0;  // this wave's counters (read by this wave only below)
-        uint32_t dig[kBgIt], pos[kBgIt];
-#pragma unroll
-        for (int i = 0; i < kBgIt; i++)
-            dig[i] = ((vmask >> i) & 1u) ? (uint32_t)sm.id[(uint32_t)((uint64_t)(tb.key ? cur[i].y : cur[i].x) -
-                                                                     (uint64_t)g.base)]
-                                         : 0u;
-        bg_rank<kBgIt, 8>(dig, vmask, wc, lane, pos);  // pos = rank among the wave's rows of the id
-        __syncthreads();
-        if (tid < (int)nid) {  // id tid: the waves' first rows, then the running start advanced
-            const uint32_t r = sm.rid[tid];
-            uint32_t run = sm.end[X][r];
-#pragma unroll
-            for (int w = 0; w < kMsdWaves; w++) {
-                const uint32_t c = sm.wcnt[w][tid];
-                sm.wcnt[w][tid] = run;
-                run += c;
-            }
-            sm.end[X][r] = run;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kBgIt; i++)
-            if ((vmask >> i) & 1u) dst[wc[dig[i]] + pos[i]] = cur[i];
+        if (c0 + kGroupCap < v1) bg_load_chunk<X>(p, sm, c0 + kGroupCap, v1, nxt, vnext);
+        bg_place_ids<X>(p, g, cur, vmask, sm);
 #pragma unroll
         for (int i = 0; i < kBgIt; i++) cur[i] = nxt[i];
         vmask = vnext;
-        // no barrier: a wave zeroes and reads only its own counter row, and the
-        // id threads of the next chunk write after its first barrier
     }
 }
 

@@ -1,0 +1,19 @@
+# after dropping the virtual mode: MSD + large + multidev + staged suites; C3/C4/C5 bench lines; C5 and C3 rocprof stats; C3 PMC (FETCH_SIZE, WRITE_SIZE passes)
+set -o pipefail
+O=gpurun_out/r03h; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_msd.py tests/test_gpu_large.py tests/test_gpu_multidev.py tests/test_gpu_staged.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.out 2>&1 || { echo "tests rc=$?"; tail -40 $O/tests.out; exit 1; }
+tail -1 $O/tests.out
+for w in c3 c4 c5; do
+timeout -k 10 400 python bench.py --workload $w --steps 5 --warmup 2 --cpu-sample 0 --cpu-mt 0 > $O/$w.json 2> $O/$w.err || { echo "$w rc=$?"; tail -20 $O/$w.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/$w.json')); print('$w', d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], {k: v['ms_per_step'] for k, v in d['kernels'].items() if v['ms_per_step'] > 0.1})"
+done
+SMJ_LIB=pim-sort-merge-join_amd/lib/variants/stamps/libsmj_hip.so SMJ_DEBUG_BIG=1 timeout -k 10 300 python tools/big_times.py > $O/big_times.json 2> $O/big_times.err || { echo "big rc=$?"; tail -5 $O/big_times.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/big_times.json')); print(d['msd_big_dev_ms'], d['phases'], {k: v['cycles_per_group'] for k, v in d['classes'].items()})"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --workload c5 --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 > $O/c5_prof.json 2> $O/c5_prof.err || { echo "prof c5 rc=$?"; tail -5 $O/c5_prof.err; exit 1; }
+rm -f $O/prof_c5/c5_kernel_trace.csv
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --cpu-mt 0 > $O/c3_prof.json 2> $O/c3_prof.err || { echo "prof c3 rc=$?"; tail -5 $O/c3_prof.err; exit 1; }
+rm -f $O/prof_c3/c3_kernel_trace.csv
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 > $O/pmcf.json 2> $O/pmcf.err || { echo "pmcf rc=$?"; tail -5 $O/pmcf.err; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 > $O/pmcw.json 2> $O/pmcw.err || { echo "pmcw rc=$?"; tail -5 $O/pmcw.err; exit 1; }
+ls $O/pmc_fetch $O/pmc_write | head
