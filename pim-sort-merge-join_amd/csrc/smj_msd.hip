@@ -2481,23 +2481,24 @@ __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key 
 // sm.key[x].
 // A pass ranks each (item, wave) group of 64 rows by wave ballots on the
 // digit, prefixes the 16 groups' counts per digit (v order = item, wave,
-// lane) and scatters; pass 2 reads pass 1's order back the same way.
+// lane) and scatters; pass 2 reads pass 1's order back the same way.  Both
+// tables go through a pass together (round 3: half the barriers, and the
+// two per-digit prefixes run on two waves at once).
 // Counters: 2 x 16 x 64 words in the list region (idle during the sort).
 __device__ __forceinline__ void st_lsd(uint32_t (&cur)[2][kStIt], const int (&n)[2], StSmem &sm) {
     constexpr int G = kStIt * kStWaves, DB = 6, D = 1 << DB;
-    static_assert(G * D * 4 <= (int)sizeof(sm.L.list) + (int)sizeof(sm.L.at), "LSD counters fit the list region");
+    static_assert(2 * G * D * 4 <= (int)sizeof(sm.L), "LSD counters of both tables fit the list region");
     static_assert(kStRange <= (1 << (2 * DB)), "two digits cover the residual");
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(&sm.L.list[0][0]);  // [g][d]
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(&sm.L);  // [table][g][d]
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int x = 0; x < 2; x++) {  // one table at a time (register pressure)
-        if (n[x] == 0) continue;
+    for (int pass = 0; pass < 2; pass++) {
+        const int sh = kFinIdxBits + DB * pass;
+        for (int i = tid; i < 2 * G * D; i += kStThreads) cnt[i] = 0;
+        __syncthreads();
+        uint32_t rk[2][kStIt];
 #pragma unroll
-        for (int pass = 0; pass < 2; pass++) {
-            const int sh = kFinIdxBits + DB * pass;
-            for (int i = tid; i < G * D; i += kStThreads) cnt[i] = 0;
-            __syncthreads();
-            uint32_t rk[kStIt];
+        for (int x = 0; x < 2; x++)
 #pragma unroll
             for (int k = 0; k < kStIt; k++) {
                 const bool v = cur[x][k] != ~0u;
@@ -2511,36 +2512,42 @@ __device__ __forceinline__ void st_lsd(uint32_t (&cur)[2][kStIt], const int (&n)
                     plo = peer_fold(plo, (uint32_t)bb, sb);
                     phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
                 }
-                rk[k] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+                rk[x][k] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
                 const uint64_t peers = ((uint64_t)phi << 32) | plo;
-                if (v && (peers >> lane) == 1ull) cnt[(k * kStWaves + wave) * D + d] = (uint32_t)__popcll(peers);
+                if (v && (peers >> lane) == 1ull) cnt[(x * G + k * kStWaves + wave) * D + d] = (uint32_t)__popcll(peers);
             }
-            __syncthreads();
-            if (tid < D) {  // lane d: prefix over the groups in v order, then over the digits
-                uint32_t t = 0;
+        __syncthreads();
+        if (tid < 2 * D && n[tid >> DB] > 0) {  // wave x, lane d: prefix over the groups in v order, then the digits
+            uint32_t *c = cnt + (tid >> DB) * G * D;
+            const int d = tid & (D - 1);
+            uint32_t t = 0;
 #pragma unroll 4
-                for (int g = 0; g < G; g++) t += cnt[g * D + tid];
-                uint32_t run = wave_incl_scan(t, lane) - t;
+            for (int g = 0; g < G; g++) t += c[g * D + d];
+            uint32_t run = wave_incl_scan(t, lane) - t;
 #pragma unroll 4
-                for (int g = 0; g < G; g++) {
-                    const uint32_t c = cnt[g * D + tid];
-                    cnt[g * D + tid] = run;
-                    run += c;
-                }
+            for (int g = 0; g < G; g++) {
+                const uint32_t q = c[g * D + d];
+                c[g * D + d] = run;
+                run += q;
             }
-            __syncthreads();
+        }
+        __syncthreads();
+#pragma unroll
+        for (int x = 0; x < 2; x++)
 #pragma unroll
             for (int k = 0; k < kStIt; k++)
                 if (cur[x][k] != ~0u)
-                    sm.key[x][cnt[(k * kStWaves + wave) * D + ((cur[x][k] >> sh) & (D - 1))] + rk[k]] = cur[x][k];
-            __syncthreads();
-            if (pass == 0) {
+                    sm.key[x][cnt[(x * G + k * kStWaves + wave) * D + ((cur[x][k] >> sh) & (D - 1))] + rk[x][k]] =
+                        cur[x][k];
+        __syncthreads();
+        if (pass == 0) {
+#pragma unroll
+            for (int x = 0; x < 2; x++)
 #pragma unroll
                 for (int k = 0; k < kStIt; k++) {
                     const int o = tid + k * kStThreads;
                     cur[x][k] = o < n[x] ? sm.key[x][o] : ~0u;
                 }
-            }
         }
     }
 }
@@ -2590,7 +2597,9 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     }
     if (mrun > 1u) atomicMax(&sm.flag[wsb], mrun);  // longest equal-key run
     // one barrier for two block scans: this group's bin totals and the next
-    // group's run lengths (len R | len S << 16); publishes flag[wsb]
+    // group's run lengths (len R | len S << 16); publishes flag[wsb].
+    // (Scanning the lengths in st_issue instead, after the sort: C5 final
+    // 11.75 -> 12.27 ms, C3 neutral; profiles/r03/r03k_ab.txt)
     const uint32_t lens = (no1[0] - no0[0]) | ((no1[1] - no0[1]) << 16);
     const uint32_t i1 = wave_incl_scan(tot, lane), i2 = wave_incl_scan(lens, lane);
     if (lane == 63) {

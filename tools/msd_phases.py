@@ -15,9 +15,13 @@ from smj import _lib, ops  # noqa: E402
 
 lib = _lib.load()
 n = int(float(os.environ.get("ROWS", "1e8")))
-R = ops.gen_uniform(n, seed=1, key_range=3 * n)
-S = ops.gen_uniform(n, seed=2, key_range=3 * n)
-bufs = [torch.empty_like(R), torch.empty_like(S), torch.empty((n, 3), dtype=torch.int64, device=R.device)]
+if os.environ.get("WORKLOAD") == "c5":  # C5's Zipf(0.9) tables, 1e8 x 1e9 (partitioned mode)
+    R = ops.gen_zipf(100_000_000, seed=3, domain=100_000_000, theta=0.9)
+    S = ops.gen_zipf(1_000_000_000, seed=4, domain=100_000_000, theta=0.9)
+else:
+    R = ops.gen_uniform(n, seed=1, key_range=3 * n)
+    S = ops.gen_uniform(n, seed=2, key_range=3 * n)
+bufs = [torch.empty_like(R), torch.empty_like(S), torch.empty((R.shape[0], 3), dtype=torch.int64, device=R.device)]
 ops.sort_merge_join(R, S, 0, 0, (0, 5000), (0, 5000), *bufs)
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 24)()
@@ -48,3 +52,8 @@ tot = sum(buf[16 + k] for k in range(6))
 for k in range(6):
     print(f"  {pb[k]:18s} {buf[16 + k] / max(tiles, 1):10.0f}  {100 * buf[16 + k] / max(tot, 1):5.1f}%")
 print(f"  total              {tot / max(tiles, 1):10.0f}")
+sub = ["stage + count", "bin scan", "place (scatter / LSD)", "equal-key rounds", "next lists", "next gathers"]
+stot = sum(buf[10 + k] for k in range(6))
+print("staged sort sub-phases (cycles/group):")
+for k in range(6):
+    print(f"  {sub[k]:22s} {buf[10 + k] / max(groups, 1):10.0f}  {100 * buf[10 + k] / max(stot, 1):5.1f}%")
