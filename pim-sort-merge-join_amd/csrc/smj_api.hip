@@ -804,7 +804,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     for (int x = 0; x < ntab; x++) {
         const MsdIn &t = in[x];
         MsdTabScratch &ts = ms->t[x];
-        T_[x] = msd_tile(t.cols);
+        T_[x] = msd_tile_a(t.cols);
         TB_[x] = msd_tile_b(t.cols);
         tilesA[x] = (t.n + T_[x] - 1) / T_[x];
         maxB[x] = (t.n + TB_[x] - 1) / TB_[x] + kBucketsA;  // every bucket adds <= 1 partial pass-B tile

@@ -155,6 +155,14 @@ __host__ __device__ constexpr int msd_items(int cols) {
     return cols == 1 ? 16 : cols == 2 ? 8 : cols == 3 ? 5 : cols == 4 ? 4 : cols == 5 ? 3 : 2;
 }
 __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_items(cols); }
+// pass-A tiles: 2-column tables take 8192-row tiles (1024 threads, 128 KiB of
+// staged rows, one workgroup per CU) with SMJ_PA_BIG=1, so that the bucket
+// runs part_b gathers are ~32 rows long instead of ~16
+#ifndef SMJ_PA_BIG
+#define SMJ_PA_BIG 0
+#endif
+__host__ __device__ constexpr int pa_threads(int cols) { return (SMJ_PA_BIG && cols == 2) ? 1024 : kMsdThreads; }
+__host__ __device__ constexpr int msd_tile_a(int cols) { return pa_threads(cols) * msd_items(cols); }
 // pass-B tiles (rows); part_b runs 1024 threads x 4 rows for 2-column tables
 // (64 VGPRs, 2 x 16 waves per CU: part_b is latency-bound)
 __host__ __device__ constexpr int msd_tile_b(int cols) { return msd_tile(cols); }

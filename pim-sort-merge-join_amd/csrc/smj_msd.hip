@@ -106,10 +106,15 @@ __device__ __forceinline__ void block_minmax(int64_t &mn, int64_t &mx, int64_t *
         s_mm[NW + wave] = mx;
     }
     __syncthreads();
+    // the NW wave partials through lanes [0, NW) and one more wave reduction
+    // (reading all of them per thread kept 4 NW VGPRs live: spills at NW = 16)
+    static_assert(NW <= 64, "one partial per lane");
+    mn = lane < NW ? s_mm[lane] : INT64_MAX;
+    mx = lane < NW ? s_mm[NW + lane] : INT64_MIN;
 #pragma unroll
-    for (int w = 0; w < NW; w++) {
-        mn = min(mn, s_mm[w]);
-        mx = max(mx, s_mm[NW + w]);
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
+        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
     }
     __syncthreads();
 }
@@ -145,13 +150,39 @@ __device__ __forceinline__ void wave_rank(uint32_t (&dig)[ITEMS], uint32_t vmask
     }
 }
 
+// wave_rank over u16 counters (a wave ranks at most 64 * ITEMS rows)
+template <int ITEMS, int DBITS>
+__device__ __forceinline__ void wave_rank16(uint32_t (&dig)[ITEMS], uint32_t vmask, uint16_t *wc, int lane) {
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const bool v = (vmask >> it) & 1u;
+        const uint64_t act = __ballot(v);
+        uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
+        const uint32_t dd = dig[it];
+#pragma unroll
+        for (int b = 0; b < DBITS; b++) {
+            const uint32_t sb = (uint32_t)((int32_t)(dd << (31 - b)) >> 31);
+            const uint64_t bb = __ballot(sb != 0u);
+            plo = peer_fold(plo, (uint32_t)bb, sb);
+            phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
+        }
+        if (v) {
+            const uint32_t base = wc[dd];
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, base));
+            const uint64_t peers = ((uint64_t)phi << 32) | plo;
+            if ((peers >> lane) == 1ull) wc[dd] = (uint16_t)(base + (uint32_t)__popcll(peers));
+            dig[it] = dd | (rank << 16);
+        }
+    }
+}
+
 // Per-digit cross-wave exclusive prefixes (in place in s_wcnt[wave][digit])
 // and tile-local exclusive digit starts s_bin[0..RADIX] (s_bin[RADIX] = the
 // tile's row count).  Thread t owns digits [t * DPT, t * DPT + DPT).  Ends
 // with a barrier.
-template <int RADIX>
+template <int RADIX, int NT = kMsdThreads>
 __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t *s_bin, uint32_t *s_wsum) {
-    constexpr int DPT = RADIX > kMsdThreads ? RADIX / kMsdThreads : 1;
+    constexpr int DPT = RADIX > NT ? RADIX / NT : 1, NW = NT / 64;
     const int tid = threadIdx.x;
     uint32_t tot[DPT], sum = 0;
 #pragma unroll
@@ -160,7 +191,7 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
         uint32_t t = 0;
         if (d < RADIX) {
 #pragma unroll
-            for (int w = 0; w < kMsdWaves; w++) {
+            for (int w = 0; w < NW; w++) {
                 const uint32_t c = s_wcnt[w * RADIX + d];
                 s_wcnt[w * RADIX + d] = t;
                 t += c;
@@ -170,7 +201,7 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
         sum += t;
     }
     uint32_t all;
-    uint32_t ex = block_excl_scan<kMsdWaves>(sum, s_wsum, &all);
+    uint32_t ex = block_excl_scan<NW>(sum, s_wsum, &all);
 #pragma unroll
     for (int j = 0; j < DPT; j++) {
         const int d = tid * DPT + j;
@@ -300,20 +331,22 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 #define SMJ_PB_NTLOAD 0  // A/B switch: the pipelined part_b's gathers through nontemporal loads
 #endif
 template <int COLS>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPartA2 q) {
+__global__ __launch_bounds__(pa_threads(COLS), pa_threads(COLS) == kMsdThreads ? 2 : 1) void msd_part_a_kernel(
+    const MsdPartA2 q) {
     // one launch may cover both tables (the same column count): blocks past
     // q.tiles0 take table 1's tiles
     const bool second = blockIdx.x >= q.tiles0;
     const MsdPartAParams &p = second ? q.t[1] : q.t[0];
     const unsigned bx = blockIdx.x - (second ? q.tiles0 : 0u);
-    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = kBucketsA;
-    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
+    constexpr int ITEMS = msd_items(COLS), T = msd_tile_a(COLS), RADIX = kBucketsA;
+    constexpr int NT = pa_threads(COLS), NW = NT / 64;
+    constexpr int ROWB = T * COLS * 8, CNTB = NW * RADIX * 4;
     constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
     __shared__ int64_t s_spl[kSplA + 1];
     __shared__ uint32_t s_bin[RADIX + 1];
-    __shared__ uint32_t s_wsum[kMsdWaves];
-    __shared__ int64_t s_mm[2 * kMsdWaves];
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ int64_t s_mm[2 * NW];
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
     uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
 
@@ -347,17 +380,17 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
     }
     wave_rank<ITEMS, kBitsA>(dig, vmask, wc, lane);
     __syncthreads();
-    const uint32_t total = tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
+    const uint32_t total = tile_digit_starts<RADIX, NT>(s_wcnt, s_bin, s_wsum);
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
         const uint32_t d = dig[it] & 0xffffu;
         dig[it] = s_bin[d] + wc[d] + (dig[it] >> 16);
     }
-    block_minmax<kMsdWaves>(mn, mx, s_mm);  // its barriers also retire the counters
+    block_minmax<NW>(mn, mx, s_mm);  // its barriers also retire the counters
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    static_assert(RADIX < kMsdThreads && RADIX < kOffsARow, "one offsA entry per thread");
+    static_assert(RADIX < NT && RADIX < kOffsARow, "one offsA entry per thread");
     if (tid <= RADIX) p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
     if (tid == 0) {
         p.tmm[2 * t] = mn;
@@ -368,7 +401,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part_a_kernel(const MsdPar
         int64_t *dst = p.out + row0 * COLS;
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
-            const uint32_t s = min((uint32_t)(tid + it * kMsdThreads), total - 1u);
+            const uint32_t s = min((uint32_t)(tid + it * NT), total - 1u);
             int64_t r[COLS];
             load_row<COLS>(s_rows + (size_t)s * COLS, r);
             store_row<COLS>(dst + (size_t)s * COLS, r);
@@ -990,6 +1023,9 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 #ifndef SMJ_PB_ONEKEY
 #define SMJ_PB_ONEKEY 1  // heavy-key buckets skip the tile's counting and ranking
 #endif
+#ifndef SMJ_PB_SLOWPAR
+#define SMJ_PB_SLOWPAR 1  // the ballot path ranks on per-wave counters in parallel (0: waves in turn)
+#endif
 
 // row -> run lookups of a tile (run list lst, start bitmap bm, 64-row block
 // table bt) and the row gathers into registers
@@ -1202,6 +1238,45 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                         for (uint32_t j = st; j < en; j++) rank += (uint32_t)s_perm[j] < r;
                     dig[it] = st + rank;
                 }
+        } else if (SMJ_PB_SLOWPAR) {
+            // a sub-bucket run over SMJ_PB_FASTMAX rows (Zipf tiles): every wave
+            // ranks its rows on a u16 counter row of its own (NW x RADIX x 2 B =
+            // the whole 64 KiB region), then one cross-wave prefix per digit.
+            // The tile's sub-bucket starts (quad 0's first rows) wait in the
+            // next tile's list region, idle until the staging barrier.
+            static_assert(NW * RADIX * 2 <= UB && RADIX * 2 <= (int)sizeof(s_nl) && RADIX == 2 * NT,
+                          "per-wave u16 counters fit the region; one packed counter pair per thread");
+            uint16_t *s_st = reinterpret_cast<uint16_t *>(s_nl);
+            uint16_t *cw = reinterpret_cast<uint16_t *>(s_u);
+            for (int d = tid; d < RADIX; d += NT) s_st[d] = (uint16_t)(s_q[d] & 0xffffu);
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) dig[it] &= 0xffffu;
+            __syncthreads();  // s_q read out: the region becomes the counters
+            {
+                uint4 *z = reinterpret_cast<uint4 *>(cw + wave * RADIX);
+#pragma unroll
+                for (int i = 0; i < RADIX * 2 / 16 / 64; i++) z[lane + i * 64] = make_uint4(0, 0, 0, 0);
+            }
+            __syncthreads();
+            wave_rank16<ITEMS, kBitsB>(dig, vmask, cw + wave * RADIX, lane);
+            __syncthreads();
+            {  // digits 2 tid, 2 tid + 1: exclusive prefix over the waves (u16 pairs, no carry: <= T rows)
+                uint32_t *c32 = reinterpret_cast<uint32_t *>(s_u);
+                uint32_t run = 0;
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    const uint32_t c = c32[w * (RADIX / 2) + tid];
+                    c32[w * (RADIX / 2) + tid] = run;
+                    run += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) {
+                    const uint32_t d = dig[it] & 0xffffu;
+                    dig[it] = (uint32_t)s_st[d] + (uint32_t)cw[wave * RADIX + d] + (dig[it] >> 16);
+                }
         } else {
 #pragma unroll
             for (int k = 0; k < RADIX / NT; k++) s_cnt[tid + k * NT] = 0;
@@ -1220,6 +1295,10 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                 }
         }
         __syncthreads();  // permutation / counters dead: the region becomes the staging tile
+        // (storing the ranked rows straight from registers instead, scattered
+        // 16-B stores into the tile's region: part_b 1.58 -> 1.93 ms at C3,
+        // profiles/r03/r03l_ab_c3.txt)
+        int64_t *dst = p.out + g * T * COLS;
 #pragma unroll
         for (int it = 0; it < ITEMS; it++)
             if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
@@ -1235,7 +1314,6 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // the stores are unconditional (a run-time ablation bit around them
         // made hipcc's wait for the next tile's rows a vmcnt(0) that also
         // retired these stores); SMJ_PB_NOSTORE=1 builds the no-store ablation
-        int64_t *dst = p.out + g * T * COLS;
         if (!SMJ_PB_NOSTORE) {
 #pragma unroll
             for (int it = 0; it < ITEMS; it++) {
@@ -3852,7 +3930,7 @@ hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
 
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
-    return launch_msd_part_a_tiles(p, cols, 0, blocks_for(p.n, msd_tile(cols)), s);
+    return launch_msd_part_a_tiles(p, cols, 0, blocks_for(p.n, msd_tile_a(cols)), s);
 }
 
 hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t t0, int64_t t1, hipStream_t s) {
@@ -3861,8 +3939,8 @@ hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t
     q.t[0] = p_in;
     q.t[0].tile0 = (int)t0;
     q.tiles0 = (unsigned)(t1 - t0);
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3((unsigned)(t1 - t0)), dim3(kMsdThreads), 0,
-                                             s, q));
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3((unsigned)(t1 - t0)), dim3(pa_threads(C)),
+                                             0, s, q));
     return hipGetLastError();
 }
 
@@ -3871,11 +3949,11 @@ hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, 
     q.t[0] = a;
     q.t[1] = b;
     q.t[0].tile0 = q.t[1].tile0 = 0;
-    q.tiles0 = a.n > 0 ? blocks_for(a.n, msd_tile(cols)) : 0u;
-    const unsigned tiles1 = b.n > 0 ? blocks_for(b.n, msd_tile(cols)) : 0u;
+    q.tiles0 = a.n > 0 ? blocks_for(a.n, msd_tile_a(cols)) : 0u;
+    const unsigned tiles1 = b.n > 0 ? blocks_for(b.n, msd_tile_a(cols)) : 0u;
     if (q.tiles0 + tiles1 == 0) return hipSuccess;
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(q.tiles0 + tiles1), dim3(kMsdThreads), 0, s,
-                                             q));
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(q.tiles0 + tiles1), dim3(pa_threads(C)), 0,
+                                             s, q));
     return hipGetLastError();
 }
 
