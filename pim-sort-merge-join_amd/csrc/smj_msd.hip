@@ -755,12 +755,14 @@ __device__ __forceinline__ int opaque_tid() {
 }
 
 constexpr int kPbFastMax = 16;  // longest sub-bucket run of a tile the atomic-rank path orders
-// the same limit in msd_part_b_pipe_kernel (per quad of waves): runs up to
-// 128 rows are still cheaper ranked by the scan than by the wave-by-wave
-// ballot path (C5's Zipf tiles: part_b 13.8 -> 12.9 ms at 128, 13.9 at 256,
-// 22.5 at 1024; C3 unchanged -- profiles/r02bu, r02bv)
+// the same limit in msd_part_b_pipe_kernel (per quad of waves).  With the
+// waves taking turns on the ballot path, runs up to 128 rows were cheaper
+// ranked by the scan (C5's Zipf tiles: part_b 13.8 -> 12.9 ms at 128, 13.9
+// at 256, 22.5 at 1024 -- profiles/r02bu, r02bv); with the parallel ballot
+// path (SMJ_PB_SLOWPAR) 16 is best again: C5 part_b 11.3 -> 9.6 ms, 32 gives
+// 9.7 (profiles/r03/r03m_ab_c5.txt); C3's tiles never take it
 #ifndef SMJ_PB_FASTMAX
-#define SMJ_PB_FASTMAX 128
+#define SMJ_PB_FASTMAX 16
 #endif
 
 template <int COLS>
