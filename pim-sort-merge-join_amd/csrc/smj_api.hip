@@ -484,7 +484,14 @@ struct MsdScratch {
     int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
     void *giant = nullptr, *gmap = nullptr, *gh = nullptr;  // msd_giant_*: groups, job map, job counts
     size_t c_giant = 0, c_gmap = 0, c_gh = 0;
+    void *pst[2] = {nullptr, nullptr};  // partitioned mode: the one-pass partition's part regions per table
+    size_t c_pst[2] = {0, 0};
+    void *p1st = nullptr;               // its look-back words
+    size_t c_p1st = 0;
+    int64_t *p1d = nullptr;             // device [2][kP1Words]: oc[128], tot[64], flags[4] (u32 x 8) per table
+    int64_t *p1h = nullptr;             // pinned twin
 };
+constexpr int kP1Words = 128 + 64 + 4;
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
 int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
@@ -527,6 +534,8 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
         HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
         HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 64));
+        HIP_TRY(hipMalloc(&m.p1d, sizeof(int64_t) * 2 * kP1Words));
+        HIP_TRY(hipHostMalloc(&m.p1h, sizeof(int64_t) * 2 * kP1Words, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
         m.dev = dev;  // only once every buffer exists (a failed call retries the allocation)
@@ -545,8 +554,9 @@ void msd_free_all() {
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
-                        (void *)m.lspl, m.giant, m.gmap, m.gh})
+                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d})
             hipFree(p);
+        hipHostFree(m.p1h);
         hipHostFree(m.h_plan);
         hipHostFree(m.h_samp);
     }
@@ -1087,6 +1097,100 @@ int64_t msd_large_parts(const MsdIn *in, int ntab) {
     return std::min<int64_t>(64, (mx + kMsdPartRows - 1) / kMsdPartRows);
 }
 
+// The one-pass partition (msd_part1_kernel) for tables of up to 8 columns;
+// SMJ_PART1=0 keeps the counting partition (A/B runs).
+bool msd_part1_on(const MsdIn *in, int ntab) {
+    static const bool on = [] {
+        const char *e = getenv("SMJ_PART1");
+        return !(e && e[0] == '0');
+    }();
+    for (int x = 0; x < ntab; x++)
+        if (in[x].cols > kDirectCols) return false;
+    return on;
+}
+
+// Region capacities from the key sample (ms->h_samp: table x's sampled keys at
+// [x * kSampleMax, + min(n, kSampleMax)), INT64_MAX for a row the select
+// drops): part b's estimated rows plus 8 binomial standard deviations plus a
+// tile, capped at the table's rows.  *staged = false when a region overflowed
+// (the caller then runs the counting partition instead); cnt / roff: rows per
+// part and region starts.
+int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64_t> &spl, std::vector<int64_t> *cnt,
+              std::vector<int64_t> *roff, bool *staged, hipStream_t s) {
+    const int nspl = (int)spl.size(), nb = nspl + 1;
+    *staged = false;
+    int64_t nt[2] = {0, 0};
+    for (int x = 0; x < ntab; x++) {
+        cnt[x].assign(nb, 0);
+        roff[x].assign(nb + 1, 0);
+        if (in[x].n == 0) continue;
+        const int64_t m = std::min<int64_t>(in[x].n, kSampleMax);
+        std::vector<int64_t> sc(nb, 0);
+        for (int64_t j = 0; j < m; j++) {
+            const int64_t k = ms->h_samp[x * kSampleMax + j];
+            if (k == INT64_MAX) continue;
+            sc[std::lower_bound(spl.begin(), spl.end(), k) - spl.begin()]++;
+        }
+        const double w = (double)in[x].n / (double)m;
+        const int64_t tile = msd_tile(in[x].cols);
+        const char *cs = getenv("SMJ_PART1_CAP");  // tests: scaled-down regions force the fallback
+        const double scale = cs ? atof(cs) : 1.0;
+        int64_t *oc = ms->p1h + x * kP1Words;
+        for (int b = 0; b < nb; b++) {
+            const double f = (double)sc[b] / (double)m;
+            const double sd = w * std::sqrt((double)m * f * (1.0 - f) + 1.0);
+            const int64_t cap =
+                std::min<int64_t>(in[x].n, (int64_t)(((double)sc[b] * w + 8.0 * sd) * scale) + (scale < 1.0 ? 0 : tile));
+            oc[b] = roff[x][b];
+            oc[64 + b] = cap;
+            roff[x][b + 1] = roff[x][b] + cap;
+        }
+        SMJ_TRY(grow(&ms->pst[x], &ms->c_pst[x], (size_t)roff[x][nb] * in[x].cols * sizeof(T)));
+        nt[x] = (in[x].n + tile - 1) / tile;
+    }
+    SMJ_TRY(grow(&ms->p1st, &ms->c_p1st, (size_t)std::max(nt[0], nt[1]) * nb * 8));
+    for (int x = 0; x < ntab; x++) {
+        if (in[x].n == 0) continue;
+        int64_t *d = ms->p1d + x * kP1Words;
+        // oc from the pinned twin; tot and flags zeroed (one copy: the twin's zeros)
+        int64_t *h = ms->p1h + x * kP1Words;
+        for (int i = 128; i < kP1Words; i++) h[i] = 0;
+        HIP_TRY(hipMemcpyAsync(d, h, sizeof(int64_t) * kP1Words, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ms->p1st, 0, (size_t)nt[x] * nb * 8, s));
+        MsdPart1Params p{};
+        p.src = in[x].src;
+        p.n = in[x].n;
+        p.use_sel = in[x].use_sel;
+        p.sel_col = in[x].sel_col;
+        p.key_col = in[x].key;
+        p.nspl = nspl;
+        p.sel_val = in[x].sel_val;
+        p.spl = ms->lspl;
+        p.oc = d;
+        p.dst = (int64_t *)ms->pst[x];
+        p.status = (unsigned long long *)ms->p1st;
+        p.tot = (long long *)(d + 128);
+        p.flags = (uint32_t *)(d + 192);
+        p.ntiles = nt[x];
+        ProfScope ps("partition_1pass", 16.0 * in[x].cols * in[x].n, s);
+        HIP_TRY(launch_msd_part1(p, in[x].cols, s));
+    }
+    HIP_TRY(hipMemcpyAsync(ms->p1h, ms->p1d, sizeof(int64_t) * 2 * kP1Words, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    bool over = false;
+    for (int x = 0; x < ntab; x++) {
+        if (in[x].n == 0) continue;
+        const int64_t *h = ms->p1h + x * kP1Words;
+        const uint32_t *fl = (const uint32_t *)(h + 192);
+        if (fl[2]) return SMJ_ERR_TIMEOUT;
+        over |= fl[1] != 0;
+        for (int b = 0; b < nb; b++) cnt[x][b] = h[128 + b];
+    }
+    if (over && getenv("SMJ_DEBUG_PART1")) fprintf(stderr, "smj: one-pass partition overflowed a region\n");
+    *staged = !over;
+    return SMJ_OK;
+}
+
 int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
@@ -1134,14 +1238,21 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     }
     const int nspl = (int)spl.size();
     if (nspl) HIP_TRY(hipMemcpyAsync(ms->lspl, spl.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, s));
-    // 3. select + stable partition of every table straight into its output
-    // buffer (the parts are then sorted in place)
-    std::vector<int64_t> cnt[2], off[2];
+    // 3. select + stable partition of every table: in one pass into part
+    // regions sized from the sample (msd_part1_kernel; each part is then sorted
+    // from its region to its place in the output), or -- when a region would
+    // overflow, or SMJ_PART1=0 -- counted, then scattered straight into the
+    // output buffer (smj_dev_partition; the parts are then sorted in place)
+    std::vector<int64_t> cnt[2], off[2], roff[2];
+    bool staged = false;
+    if (msd_part1_on(in, ntab)) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
     for (int x = 0; x < ntab; x++) {
-        cnt[x].assign(nspl + 1, 0);
-        if (in[x].n)
-            SMJ_TRY(smj_dev_partition(in[x].src, in[x].n, in[x].cols, in[x].use_sel, in[x].sel_col, in[x].sel_val,
-                                      in[x].key, ms->lspl, nspl, in[x].out, cnt[x].data(), s));
+        if (!staged) {
+            cnt[x].assign(nspl + 1, 0);
+            if (in[x].n)
+                SMJ_TRY(smj_dev_partition(in[x].src, in[x].n, in[x].cols, in[x].use_sel, in[x].sel_col,
+                                          in[x].sel_val, in[x].key, ms->lspl, nspl, in[x].out, cnt[x].data(), s));
+        }
         off[x].assign(nspl + 2, 0);
         for (int p = 0; p <= nspl; p++) off[x][p + 1] = off[x][p] + cnt[x][p];
         h_rows[x] = off[x][nspl + 1];
@@ -1155,7 +1266,8 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         for (int x = 0; x < ntab; x++) {
             if (cnt[x][p] == 0) continue;
             T *base = in[x].out + off[x][p] * in[x].cols;
-            part[np++] = MsdIn{base, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
+            const T *src = staged ? (const T *)ms->pst[x] + roff[x][p] * in[x].cols : base;
+            part[np++] = MsdIn{src, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
         }
         int64_t rows[3] = {0, 0, 0};
         if (np == 2 && join) {

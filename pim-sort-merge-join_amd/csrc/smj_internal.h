@@ -354,6 +354,21 @@ int msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int sc1, i
                                int64_t *dS, int64_t *dRs, int64_t *dSs, int64_t *dJ, int64_t *h_rows, hipStream_t s,
                                hipStream_t copy, hipEvent_t landed);
 
+// the partitioned mode's one-pass range partition (msd_part1_kernel)
+struct MsdPart1Params {
+    const int64_t *src;
+    int64_t n;
+    int use_sel, sel_col, key_col, nspl;
+    int64_t sel_val;
+    const int64_t *spl;          // device: nspl part splitters (part of a key = #{splitters < key})
+    const int64_t *oc;           // device [128]: region start of part b (rows), then its capacity
+    int64_t *dst;                // staging buffer of the regions
+    unsigned long long *status;  // [ntiles][nspl + 1] look-back words, zeroed
+    long long *tot;              // [nspl + 1]: rows per part (written by the last tile)
+    uint32_t *flags;             // [0] tile ticket, [1] a region overflowed, [2] look-back timeout; zeroed
+    int64_t ntiles;
+};
+hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s);
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 // the sample gather alone: samp[x * kSampleMax + j] = sampled key j of table x
 // (INT64_MAX for a row the select drops or a missing row), samp[2 kSampleMax

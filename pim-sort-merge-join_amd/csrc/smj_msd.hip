@@ -410,6 +410,154 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_threads(COLS) == kMsdThreads ?
 }
 
 // ---------------------------------------------------------------------------
+// part1: the partitioned mode's range partition in ONE pass (no counting pass)
+// ---------------------------------------------------------------------------
+// Every tile (T rows, taken in ticket order) is select-filtered, ranked by its
+// part (#{splitters < key}, <= 64 parts) and staged in LDS like part_a; its
+// part counts go out as an aggregate status word per part, and wave 0 looks
+// back over the predecessors' words (64 lanes = up to 64 / nb predecessors x
+// nb parts per round trip) until each part meets an inclusive prefix: the
+// decoupled look-back, with ~T / nb rows per part per tile and <= 64 parts it
+// costs one status word per (tile, part).  Part b's rows go to its own region
+// [oc[b], oc[b] + oc[64 + b]) of the staging buffer, at the exclusive prefix:
+// stable (tile order = input order) and contiguous.  The region capacities
+// come from the key sample (smj_api.hip msd_large); a part whose rows exceed
+// its region sets flags[1] and the host falls back to the counting partition.
+// Status word: bits 63..62 = 1 aggregate, 2 inclusive prefix; 61..0 the value.
+// The look-back never waits on a later ticket, so the grid always drains; a
+// wait over 2^24 polls (a bug) sets flags[2].
+constexpr uint64_t kP1Agg = 1ull << 62, kP1Inc = 2ull << 62, kP1Val = (1ull << 62) - 1;
+template <int COLS>
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart1Params p) {
+    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = 64;
+    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
+    constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
+    __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
+    __shared__ uint8_t s_pd[T];        // part of each staged row
+    __shared__ int64_t s_spl[RADIX];
+    __shared__ uint32_t s_bin[RADIX + 1];
+    __shared__ uint32_t s_wsum[kMsdWaves];
+    __shared__ unsigned long long s_acc[RADIX];
+    __shared__ int64_t s_gb[RADIX];    // global row of part b's first row in this tile, minus its tile-local start
+    __shared__ uint32_t s_ok[RADIX];   // part b's rows fit its region
+    __shared__ uint32_t s_t;
+    int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
+    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nb = p.nspl + 1;
+    if (tid == 0) s_t = atomicAdd(&p.flags[0], 1u);
+    if (tid < RADIX) {
+        s_spl[tid] = tid < p.nspl ? p.spl[tid] : INT64_MAX;
+        s_acc[tid] = 0;
+    }
+    uint32_t *wc = s_wcnt + wave * RADIX;
+    zero_counters<RADIX>(wc, lane);
+    __syncthreads();
+    const int64_t t = s_t;
+    const int64_t row0 = t * T;
+    const int nrows = (int)min((int64_t)T, p.n - row0);
+    const int lrow0 = wave * ITEMS * 64 + lane;
+    int64_t rows[ITEMS][COLS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+    uint32_t dig[ITEMS];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const bool inb = lrow0 + it * 64 < nrows;
+        const bool pass = !p.use_sel | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+        const bool v = inb & pass;
+        const int64_t k = pick<COLS>(rows[it], p.key_col);
+        uint32_t b = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) b += s_spl[b + step - 1] < k ? step : 0u;
+        dig[it] = v ? b : 0u;
+        vmask |= v ? (1u << it) : 0u;
+    }
+    wave_rank<ITEMS, 6>(dig, vmask, wc, lane);
+    __syncthreads();
+    const uint32_t total = tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t d = dig[it] & 0xffffu;
+        dig[it] = (d << 16) | (s_bin[d] + wc[d] + (dig[it] >> 16));  // part << 16 | staging slot
+    }
+    if (wave == 0) {
+        const uint32_t cnt = lane < nb ? s_bin[lane + 1] - s_bin[lane] : 0u;
+        unsigned long long *st = p.status + t * nb;
+        if (t > 0) {
+            if (lane < nb) atomicExch(&st[lane], kP1Agg | cnt);
+            const int J = max(1, 64 / nb);  // predecessors per round
+            const int j = lane / nb, b = lane - j * nb;
+            const bool lv = lane < J * nb;
+            bool done = false;
+            uint32_t spins = 0;
+            for (int64_t tt = t - 1;; tt -= J) {
+                const bool act = lv && !done;
+                uint64_t s = 0;
+                if (act) {
+                    const int64_t tj = tt - j;
+                    if (tj < 0) {
+                        s = kP1Inc;  // before the first tile: prefix 0
+                    } else {
+                        for (;;) {
+                            s = __hip_atomic_load(&p.status[tj * nb + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (s >> 62) break;
+                            if (++spins > (1u << 24)) {
+                                atomicOr(&p.flags[2], 1u);
+                                s = kP1Inc;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                }
+                const uint64_t im = __ballot(act && (s >> 62) == 2u);
+                int jinc = J;  // this part's nearest predecessor with an inclusive prefix
+                for (int q = 0; q < J; q++)
+                    if ((im >> (q * nb + b)) & 1ull) {
+                        jinc = q;
+                        break;
+                    }
+                if (act && j <= jinc) atomicAdd(&s_acc[b], (unsigned long long)(s & kP1Val));
+                done = done || jinc < J;
+                if (__ballot(lv && !done) == 0ull) break;
+            }
+        }
+        if (lane < nb) {
+            const uint64_t ex = s_acc[lane];
+            atomicExch(&st[lane], kP1Inc | (ex + cnt));
+            const bool ok = ex + cnt <= (uint64_t)p.oc[64 + lane];
+            if (!ok) atomicOr(&p.flags[1], 1u);
+            s_ok[lane] = ok ? 1u : 0u;
+            s_gb[lane] = p.oc[lane] + (int64_t)ex - (int64_t)s_bin[lane];
+            if (t == p.ntiles - 1) p.tot[lane] = (long long)(ex + cnt);
+        }
+    }
+    __syncthreads();  // counters read out: the region becomes the staging tile
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++)
+        if ((vmask >> it) & 1u) {
+            const uint32_t slot = dig[it] & 0xffffu;
+            store_row<COLS>(s_rows + (size_t)slot * COLS, rows[it]);
+            s_pd[slot] = (uint8_t)(dig[it] >> 16);
+        }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t slot = (uint32_t)(tid + it * kMsdThreads);
+        if (slot < total) {
+            const uint32_t b = s_pd[slot];
+            if (s_ok[b]) {
+                int64_t r[COLS];
+                load_row<COLS>(s_rows + (size_t)slot * COLS, r);
+                store_row<COLS>(p.dst + (s_gb[b] + (int64_t)slot) * COLS, r);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // runs: per-bucket run lists over the tile-local partitions
 // ---------------------------------------------------------------------------
 // rows [c0, c1) of a table of ntiles rows for this wave of this segment
@@ -2987,6 +3135,9 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const Ms
 // occurrence i in S, cpu_app.c:204-266) into the group's slot range, and
 // counts[g] = their number, as the staged kernel does.
 constexpr int kBgIt = kGroupCap / kMsdThreads;  // chunk rows per thread
+#ifndef SMJ_BG_AGG
+#define SMJ_BG_AGG 1  // bg_count: the wave's rows of its first residual counted by one atomic
+#endif
 #ifndef SMJ_BG_ABL
 #define SMJ_BG_ABL 0  // timing ablation (output invalid): 1 = no counting pass, 2 = no row pass, 4 = no join rows
 #endif
@@ -3151,9 +3302,24 @@ __device__ __forceinline__ void bg_count(const MsdFinalParams &p, const MsdGroup
                 k[i] = tb.key ? r.y : r.x;
             }
         }
+        // the rows of the wave's first active residual (Zipf groups: usually
+        // the heavy key's) are counted by one atomic instead of colliding on
+        // one LDS word, lane by lane
 #pragma unroll
-        for (int i = 0; i < U; i++)
-            if (c0 + tid + i * kMsdThreads < v1) atomicAdd(&cnt[(uint32_t)((uint64_t)k[i] - (uint64_t)g.base)], 1u);
+        for (int i = 0; i < U; i++) {
+            const bool v = c0 + tid + i * kMsdThreads < v1;
+            const uint32_t r = (uint32_t)((uint64_t)k[i] - (uint64_t)g.base);
+            const uint64_t act = __ballot(v);
+            if (act == 0) continue;
+            const int lead = __ffsll((unsigned long long)act) - 1;
+            const uint32_t r0 = (uint32_t)__shfl((int)r, lead, 64);
+            const uint64_t same = __ballot(v && r == r0);
+            if (SMJ_BG_AGG && v && r == r0) {
+                if ((threadIdx.x & 63) == lead) atomicAdd(&cnt[r0], (uint32_t)__popcll(same));
+            } else if (v) {
+                atomicAdd(&cnt[r], 1u);
+            }
+        }
     }
 }
 
@@ -3927,6 +4093,12 @@ hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s) {
 
 hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
     hipLaunchKernelGGL(msd_sample_gather_kernel, dim3(kSampleGatherBlocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s) {
+    if (p.ntiles <= 0) return hipSuccess;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part1_kernel<C>), dim3((unsigned)p.ntiles), dim3(kMsdThreads), 0, s, p));
     return hipGetLastError();
 }
 

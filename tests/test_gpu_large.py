@@ -68,6 +68,44 @@ def test_partitioned_mode_matches_oracle(gpu, oracle_built, parts, nr, ns, c1, c
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
 
 
+@pytest.mark.parametrize("kind,p", [("uniform", 5), ("zipf", 7), ("sorted", 4)])
+def test_partition_fallback_when_a_region_overflows(gpu, oracle_built, parts, monkeypatch, kind, p):
+    """The one-pass partition's part regions are sized from the key sample; a
+    part over its region sends the call to the counting partition.  Regions
+    scaled down to 30 % force that, and the result stays bit-exact."""
+    from smj import ops
+    parts(p)
+    monkeypatch.setenv("SMJ_PART1_CAP", "0.3")
+    rng = np.random.default_rng(p)
+    base = "uniform" if kind == "sorted" else kind
+    R = table(rng, 200_000, 2, base, 0, 0)
+    S = table(rng, 150_000, 2, base, 0, 10 ** 9)
+    if kind == "sorted":
+        R = np.ascontiguousarray(R[np.argsort(R[:, 0], kind="stable")])
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, (0, SEL), (0, SEL))
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, (0, SEL), (0, SEL))
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
+def test_partitioned_sorted_input_matches_oracle(gpu, oracle_built, parts):
+    """Input already in key order (each sampled cluster of 16 rows falls in one
+    part): the one-pass partition's regions, or its fallback, stay exact."""
+    from smj import ops
+    parts(6)
+    rng = np.random.default_rng(11)
+    R = table(rng, 300_000, 2, "dups", 0, 0)
+    S = table(rng, 250_000, 2, "dups", 0, 10 ** 9)
+    R = np.ascontiguousarray(R[np.argsort(R[:, 0], kind="stable")])
+    S = np.ascontiguousarray(S[np.argsort(-S[:, 0], kind="stable")])  # descending: the sort reverses it stably
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, (0, -10), None)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, (0, -10), None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
 def test_partitioned_select_sort_matches_oracle(gpu, oracle_built, parts):
     from smj import ops
     parts(5)
