@@ -198,6 +198,19 @@ int scratch_key(int *dev) {
     return t_slot >= 0 ? (1 << 16) + t_slot : *dev;
 }
 
+// pinned host twin of grow() (staging of small device <-> host lists: a
+// pageable copy runs through the runtime's bounce buffer and blocks)
+int grow_host(void **p, size_t *cap, size_t need) {
+    if (need <= *cap) return SMJ_OK;
+    if (*p) HIP_TRY(hipHostFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    size_t n = std::max(need, (size_t)1 << 20);
+    HIP_TRY(hipHostMalloc(p, n, hipHostMallocDefault));
+    *cap = n;
+    return SMJ_OK;
+}
+
 int grow(void **p, size_t *cap, size_t need) {
     if (need <= *cap) return SMJ_OK;
     if (*p) HIP_TRY(hipFree(*p));
@@ -484,6 +497,10 @@ struct MsdScratch {
     int64_t *h_samp = nullptr;  // partitioned mode: the sampled keys (pinned)
     void *giant = nullptr, *gmap = nullptr, *gh = nullptr;  // msd_giant_*: groups, job map, job counts
     size_t c_giant = 0, c_gmap = 0, c_gh = 0;
+    void *pick = nullptr, *h_pick = nullptr;  // msd_fallback: the listed groups (device, pinned host)
+    size_t c_pick = 0, c_hpick = 0;
+    void *h_work = nullptr;                   // msd_fallback: pinned work lists
+    size_t c_hwork = 0;
     void *pst[2] = {nullptr, nullptr};  // partitioned mode: the one-pass partition's part regions per table
     size_t c_pst[2] = {0, 0};
     void *p1st = nullptr;               // its look-back words
@@ -554,9 +571,11 @@ void msd_free_all() {
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
-                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d})
+                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick})
             hipFree(p);
         hipHostFree(m.p1h);
+        hipHostFree(m.h_pick);
+        hipHostFree(m.h_work);
         hipHostFree(m.h_plan);
         hipHostFree(m.h_samp);
     }
@@ -592,22 +611,56 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
     const MsdPlan &pl = *ms->h_plan;
     *redo_compact = false;
     if (pl.nsingle == 0 && pl.nbig == 0) return SMJ_OK;
-    std::vector<MsdGroup> groups(std::max<uint32_t>(pl.ngroups, 1));
-    HIP_TRY(hipMemcpyAsync(groups.data(), ms->groups, sizeof(MsdGroup) * pl.ngroups, hipMemcpyDeviceToHost, s));
-    std::vector<uint32_t> singles(pl.nsingle), bigs(pl.nbig);
-    if (pl.nsingle)
-        HIP_TRY(hipMemcpyAsync(singles.data(), ms->single_list, 4 * pl.nsingle, hipMemcpyDeviceToHost, s));
-    if (pl.nbig) HIP_TRY(hipMemcpyAsync(bigs.data(), ms->big_list, 4 * pl.nbig, hipMemcpyDeviceToHost, s));
+    // only the listed groups come to the host (picked on the device, pinned
+    // staging): the dense group array is ~10 MB per 1.5e8-row part
+    const uint32_t nl = pl.nsingle + pl.nbig;
+    SMJ_TRY(grow(&ms->pick, &ms->c_pick, (size_t)nl * sizeof(MsdGroup)));
+    SMJ_TRY(grow_host(&ms->h_pick, &ms->c_hpick, (size_t)nl * (sizeof(MsdGroup) + 4)));
+    HIP_TRY(launch_msd_pick_groups(ms->groups, ms->single_list, ms->big_list, pl.nsingle, pl.nbig,
+                                   (MsdGroup *)ms->pick, s));
+    MsdGroup *picked = (MsdGroup *)ms->h_pick;
+    uint32_t *slots_h = (uint32_t *)(picked + nl);
+    HIP_TRY(hipMemcpyAsync(picked, ms->pick, sizeof(MsdGroup) * nl, hipMemcpyDeviceToHost, s));
+    if (pl.nsingle) HIP_TRY(hipMemcpyAsync(slots_h, ms->single_list, 4 * pl.nsingle, hipMemcpyDeviceToHost, s));
+    if (pl.nbig) HIP_TRY(hipMemcpyAsync(slots_h + pl.nsingle, ms->big_list, 4 * pl.nbig, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    std::map<uint32_t, uint32_t> where;  // dense slot -> its picked record
+    for (uint32_t i = 0; i < nl; i++) where[slots_h[i]] = i;
+    struct PickedGroups {
+        const MsdGroup *rec;
+        const std::map<uint32_t, uint32_t> *at;
+        const MsdGroup &operator[](uint32_t slot) const { return rec[at->find(slot)->second]; }
+    } groups{picked, &where};
+    std::vector<uint32_t> singles(slots_h, slots_h + pl.nsingle), bigs(slots_h + pl.nsingle, slots_h + nl);
+    // pinned work lists, packed back to back (their H2D copies need no sync)
+    size_t hw_at = 0;
+    auto hw_take = [&](size_t bytes) -> int {
+        hw_at = (hw_at + 15) & ~(size_t)15;
+        const size_t need = hw_at + bytes;
+        if (need > ms->c_hwork) return SMJ_ERR_HIP;  // sized above: never
+        return SMJ_OK;
+    };
+    {
+        size_t bound = 0;  // every list below, with its alignment
+        for (uint32_t i = 0; i < nl; i++) {
+            const MsdGroup &g = picked[i];
+            const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
+            bound += (rows / kGroupCap + 2) * sizeof(uint2) + (rows / kCompactChunk + 2) * sizeof(uint2);
+        }
+        SMJ_TRY(grow_host(&ms->h_work, &ms->c_hwork, bound + 64));
+    }
     if (pl.nsingle) {
-        std::vector<uint2> work;
+        SMJ_TRY(hw_take(0));
+        uint2 *work = (uint2 *)((char *)ms->h_work + hw_at);
+        size_t nw = 0;
         for (uint32_t slot : singles) {
             const MsdGroup &g = groups[slot];
             const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
-            for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work.push_back(make_uint2(slot, c));
+            for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work[nw++] = make_uint2(slot, c);
         }
-        SMJ_TRY(grow(&ms->work, &ms->c_work, work.size() * sizeof(uint2)));
-        HIP_TRY(hipMemcpyAsync(ms->work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+        hw_at += nw * sizeof(uint2);
+        SMJ_TRY(grow(&ms->work, &ms->c_work, nw * sizeof(uint2)));
+        HIP_TRY(hipMemcpyAsync(ms->work, work, nw * sizeof(uint2), hipMemcpyHostToDevice, s));
         double b = 0;  // rows read + written once, join rows min(nR, nS) (single key: all pair up)
         for (uint32_t slot : singles) {
             const MsdGroup &g = groups[slot];
@@ -615,8 +668,7 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
             if (join) b += 8.0 * (in[0].cols + in[1].cols - 1) * (double)std::min(g.nR, g.nS);
         }
         ProfScope ps("msd_single", b, s);
-        HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)work.size(), s));
-        HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
+        HIP_TRY(launch_msd_single(fp, (const uint2 *)ms->work, (int64_t)nw, s));
     }
     // oversized multi-key groups of a small key span are sorted (and joined)
     // on the device (msd_big_stage_kernel, msd_giant_*; 2-column tables),
@@ -749,18 +801,20 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         HIP_TRY(hipStreamSynchronize(s));  // the work list is host-owned
     }
     if (join) {  // the oversized groups' join rows are packed in chunks (msd_compact_big_kernel)
-        std::vector<uint2> cw;
+        SMJ_TRY(hw_take(0));
+        uint2 *cw = (uint2 *)((char *)ms->h_work + hw_at);
+        size_t nc = 0;
         for (const std::vector<uint32_t> *l : {&singles, &bigs})
             for (uint32_t slot : *l) {
                 const uint32_t m = std::min(groups[slot].nR, groups[slot].nS);
                 if (m > (uint32_t)kGroupCap)
-                    for (uint32_t c = 0; c * kCompactChunk < m; c++) cw.push_back(make_uint2(slot, c));
+                    for (uint32_t c = 0; c * kCompactChunk < m; c++) cw[nc++] = make_uint2(slot, c);
             }
-        ms->n_cwork = (int64_t)cw.size();
-        if (!cw.empty()) {
-            SMJ_TRY(grow(&ms->cwork, &ms->c_cwork, cw.size() * sizeof(uint2)));
-            HIP_TRY(hipMemcpyAsync(ms->cwork, cw.data(), cw.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
-            HIP_TRY(hipStreamSynchronize(s));  // host-owned
+        hw_at += nc * sizeof(uint2);
+        ms->n_cwork = (int64_t)nc;
+        if (nc) {
+            SMJ_TRY(grow(&ms->cwork, &ms->c_cwork, nc * sizeof(uint2)));
+            HIP_TRY(hipMemcpyAsync(ms->cwork, cw, nc * sizeof(uint2), hipMemcpyHostToDevice, s));
         }
     }
     (void)out_j;

@@ -404,6 +404,9 @@ hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
+// out[i] = groups[list[i]] over the single-key then oversized list entries
+hipError_t launch_msd_pick_groups(const MsdGroup *groups, const uint32_t *single_list, const uint32_t *big_list,
+                                  uint32_t nsingle, uint32_t nbig, MsdGroup *out, hipStream_t s);
 // batched fallback (oversized multi-key groups): see smj_msd.hip
 hipError_t launch_msd_gather_list(const MsdTab &tb, const MsdGroup *groups, const uint4 *work, int64_t nwork,
                                   int64_t *dst, hipStream_t s);

@@ -150,6 +150,15 @@ __device__ __forceinline__ void wave_rank(uint32_t (&dig)[ITEMS], uint32_t vmask
     }
 }
 
+// threadIdx.x as a value the compiler may not hoist out of the group loop:
+// per-lane addresses are recomputed where used instead of living (spilled)
+// across the whole loop
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // wave_rank over u16 counters (a wave ranks at most 64 * ITEMS rows)
 template <int ITEMS, int DBITS>
 __device__ __forceinline__ void wave_rank16(uint32_t (&dig)[ITEMS], uint32_t vmask, uint16_t *wc, int lane) {
@@ -893,14 +902,6 @@ __device__ unsigned long long g_pb_phase[8];
         pb_t = t_;                                                  \
     }
 
-// threadIdx.x as a value the compiler may not hoist out of the group loop:
-// per-lane addresses are recomputed where used instead of living (spilled)
-// across the whole loop
-__device__ __forceinline__ int opaque_tid() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
 
 constexpr int kPbFastMax = 16;  // longest sub-bucket run of a tile the atomic-rank path orders
 // the same limit in msd_part_b_pipe_kernel (per quad of waves).  With the
@@ -3875,6 +3876,29 @@ __global__ __launch_bounds__(kMsdThreads) void msd_gather_list_kernel(const MsdT
     });
 }
 
+// the host fallback's view of the oversized groups: out[i] = groups[list[i]]
+// for the nsingle single-key then nbig oversized list entries (copied to the
+// host instead of every dense group record)
+__global__ __launch_bounds__(256) void msd_pick_groups_kernel(const MsdGroup *__restrict__ groups,
+                                                              const uint32_t *__restrict__ single_list,
+                                                              const uint32_t *__restrict__ big_list, uint32_t nsingle,
+                                                              uint32_t nbig, MsdGroup *__restrict__ out) {
+    constexpr int W = sizeof(MsdGroup) / 8;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 8-B word of one record
+    const int64_t r = i / W;
+    if (r >= (int64_t)nsingle + nbig) return;
+    const uint32_t slot = r < nsingle ? single_list[r] : big_list[r - nsingle];
+    reinterpret_cast<int64_t *>(out)[i] = reinterpret_cast<const int64_t *>(groups + slot)[i % W];
+}
+hipError_t launch_msd_pick_groups(const MsdGroup *groups, const uint32_t *single_list, const uint32_t *big_list,
+                                  uint32_t nsingle, uint32_t nbig, MsdGroup *out, hipStream_t s) {
+    const int64_t words = ((int64_t)nsingle + nbig) * (int64_t)(sizeof(MsdGroup) / 8);
+    if (words == 0) return hipSuccess;
+    hipLaunchKernelGGL(msd_pick_groups_kernel, dim3(blocks_for(words, 256)), dim3(256), 0, s, groups, single_list,
+                       big_list, nsingle, nbig, out);
+    return hipGetLastError();
+}
+
 // work item = {source row, destination row, rows, -}: contiguous row runs
 __global__ __launch_bounds__(256) void msd_seg_copy_kernel(const int64_t *__restrict__ src, int64_t *__restrict__ dst,
                                                            const uint4 *work, int cols) {
@@ -4098,6 +4122,10 @@ hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
 
 hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s) {
     if (p.ntiles <= 0) return hipSuccess;
+    // one tile per workgroup: a persistent form that took its next ticket
+    // ahead (its rows in flight during the look-back) ran 17.7 vs 14.4 ms at
+    // C4 -- the taken-ahead tiles publish late and every successor's look-back
+    // waits on them (profiles/r03/r03o_ab_c4.txt)
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part1_kernel<C>), dim3((unsigned)p.ntiles), dim3(kMsdThreads), 0, s, p));
     return hipGetLastError();
 }
