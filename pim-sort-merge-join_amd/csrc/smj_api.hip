@@ -624,14 +624,13 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
     if (pl.nsingle) HIP_TRY(hipMemcpyAsync(slots_h, ms->single_list, 4 * pl.nsingle, hipMemcpyDeviceToHost, s));
     if (pl.nbig) HIP_TRY(hipMemcpyAsync(slots_h + pl.nsingle, ms->big_list, 4 * pl.nbig, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    std::map<uint32_t, uint32_t> where;  // dense slot -> its picked record
-    for (uint32_t i = 0; i < nl; i++) where[slots_h[i]] = i;
-    struct PickedGroups {
-        const MsdGroup *rec;
-        const std::map<uint32_t, uint32_t> *at;
-        const MsdGroup &operator[](uint32_t slot) const { return rec[at->find(slot)->second]; }
-    } groups{picked, &where};
-    std::vector<uint32_t> singles(slots_h, slots_h + pl.nsingle), bigs(slots_h + pl.nsingle, slots_h + nl);
+    // list entry i: dense slot slots_h[i], record picked[i] (singles first, then the oversized groups)
+    struct Listed {
+        uint32_t slot;
+        const MsdGroup *g;
+    };
+    std::vector<Listed> singles(pl.nsingle), bigs(pl.nbig);
+    for (uint32_t i = 0; i < nl; i++) (i < pl.nsingle ? singles[i] : bigs[i - pl.nsingle]) = Listed{slots_h[i], picked + i};
     // pinned work lists, packed back to back (their H2D copies need no sync)
     size_t hw_at = 0;
     auto hw_take = [&](size_t bytes) -> int {
@@ -653,17 +652,17 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         SMJ_TRY(hw_take(0));
         uint2 *work = (uint2 *)((char *)ms->h_work + hw_at);
         size_t nw = 0;
-        for (uint32_t slot : singles) {
-            const MsdGroup &g = groups[slot];
+        for (const Listed &e : singles) {
+            const MsdGroup &g = *e.g;
             const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
-            for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work[nw++] = make_uint2(slot, c);
+            for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work[nw++] = make_uint2(e.slot, c);
         }
         hw_at += nw * sizeof(uint2);
         SMJ_TRY(grow(&ms->work, &ms->c_work, nw * sizeof(uint2)));
         HIP_TRY(hipMemcpyAsync(ms->work, work, nw * sizeof(uint2), hipMemcpyHostToDevice, s));
         double b = 0;  // rows read + written once, join rows min(nR, nS) (single key: all pair up)
-        for (uint32_t slot : singles) {
-            const MsdGroup &g = groups[slot];
+        for (const Listed &e : singles) {
+            const MsdGroup &g = *e.g;
             b += 2.0 * 8.0 * ((double)g.nR * in[0].cols + (ntab > 1 ? (double)g.nS * in[1].cols : 0.0));
             if (join) b += 8.0 * (in[0].cols + in[1].cols - 1) * (double)std::min(g.nR, g.nS);
         }
@@ -680,8 +679,8 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         // ceil(rows / seg) jobs with 2 x kStageRange residual counts each
         const MsdBgLimits bl = msd_bg_limits();
         int64_t ngiant = 0, njobs = 0;
-        for (uint32_t slot : bigs) {
-            const MsdGroup &g = groups[slot];
+        for (const Listed &e : bigs) {
+            const MsdGroup &g = *e.g;
             const uint32_t m = std::max(g.nR, ntab > 1 ? g.nS : 0u);
             if (std::max(g.nR, g.nS) > bl.max_rows) {
                 ngiant++;
@@ -709,24 +708,24 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
             HIP_TRY(hipStreamSynchronize(s));
             const int tcb = join ? in[0].cols + in[1].cols - 1 : 0;
             double b = 0;
-            for (uint32_t slot : bigs) {
-                const MsdGroup &g = groups[slot];
+            for (const Listed &e : bigs) {
+                const MsdGroup &g = *e.g;
                 if (!msd_big_on_device(g.span, g.kt[0], g.kt[1])) continue;
                 b += 2.0 * 8.0 * ((double)g.nR * in[0].cols + (ntab > 1 ? (double)g.nS * in[1].cols : 0.0));
-                b += 8.0 * tcb * (double)cnt[slot];
+                b += 8.0 * tcb * (double)cnt[e.slot];
             }
             prof_set_bytes(pi, b);
         }
     }
-    std::vector<uint32_t> host_bigs;
-    for (uint32_t slot : bigs) {
-        const MsdGroup &g = groups[slot];
-        if (!(two && msd_big_on_device(g.span, g.kt[0], g.kt[1]))) host_bigs.push_back(slot);
+    std::vector<Listed> host_bigs;
+    for (const Listed &e : bigs) {
+        const MsdGroup &g = *e.g;
+        if (!(two && msd_big_on_device(g.span, g.kt[0], g.kt[1]))) host_bigs.push_back(e);
     }
     if (getenv("SMJ_DEBUG_BIG")) {  // size distribution of the oversized multi-key groups (rows, log2 bins)
         int64_t hist[2][33] = {}, rows[2][33] = {};
-        for (uint32_t slot : bigs) {
-            const MsdGroup &g = groups[slot];
+        for (const Listed &e : bigs) {
+            const MsdGroup &g = *e.g;
             const uint32_t m = std::max(g.nR, g.nS);
             const int b = 31 - __builtin_clz(std::max(m, 1u)), d = g.span <= (uint32_t)kStageRange ? 0 : 1;
             hist[d][b]++;
@@ -744,11 +743,12 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         // output rows; with join, one zip join of the two sorted buffers split
         // per group
         constexpr uint32_t kSeg = 4096;  // rows per copy-back work item
-        std::sort(host_bigs.begin(), host_bigs.end());  // dense group index = key order (the list is filled by atomics)
+        std::sort(host_bigs.begin(), host_bigs.end(), [](const Listed &a, const Listed &b) { return a.slot < b.slot; });  // dense group index = key order (the list is filled by atomics)
         std::vector<uint4> gw[2], cw[2], bw;
         int64_t tot[2] = {0, 0};
-        for (uint32_t slot : host_bigs) {
-            const MsdGroup &g = groups[slot];
+        for (const Listed &e : host_bigs) {
+            const uint32_t slot = e.slot;
+            const MsdGroup &g = *e.g;
             const uint32_t nx[2] = {g.nR, ntab > 1 ? g.nS : 0u};
             const uint32_t ox[2] = {g.outR, g.outS};
             bw.push_back(make_uint4(slot, (uint32_t)tot[0], nx[0], nx[1]));
@@ -804,11 +804,11 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         SMJ_TRY(hw_take(0));
         uint2 *cw = (uint2 *)((char *)ms->h_work + hw_at);
         size_t nc = 0;
-        for (const std::vector<uint32_t> *l : {&singles, &bigs})
-            for (uint32_t slot : *l) {
-                const uint32_t m = std::min(groups[slot].nR, groups[slot].nS);
+        for (const std::vector<Listed> *l : {&singles, &bigs})
+            for (const Listed &e : *l) {
+                const uint32_t m = std::min(e.g->nR, e.g->nS);
                 if (m > (uint32_t)kGroupCap)
-                    for (uint32_t c = 0; c * kCompactChunk < m; c++) cw[nc++] = make_uint2(slot, c);
+                    for (uint32_t c = 0; c * kCompactChunk < m; c++) cw[nc++] = make_uint2(e.slot, c);
             }
         hw_at += nc * sizeof(uint2);
         ms->n_cwork = (int64_t)nc;
