@@ -856,6 +856,25 @@ void host_sample(const MsdIn *in, const MsdStage &stg, int ntab, int64_t *samp) 
         }
 }
 
+// Combined final groups (<= kStRows rows of both tables together, the staged
+// final kernel) for 2-column tables of skewed sizes (or one table): a group
+// then fills with the larger table's rows instead of stopping at kGroupCap of
+// them.  Balanced tables keep <= kGroupCap rows per table (the staged kernel's
+// per-table layout: C3 msd_final 1.59 vs 1.70 ms combined; C5 11.6 -> 9.1 ms
+// combined, profiles/r03/r03s).  SMJ_ST_COMBINED=0 / 1 forces either (A/B).
+int msd_combined(const MsdIn *in, int ntab) {
+    static const int force = [] {
+        const char *e = getenv("SMJ_ST_COMBINED");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    for (int x = 0; x < ntab; x++)
+        if (in[x].cols != 2) return 0;
+    if (force >= 0) return force;
+    if (ntab < 2) return 1;
+    const int64_t lo = std::min(in[0].n, in[1].n), hi = std::max(in[0].n, in[1].n);
+    return 2 * hi > 3 * lo ? 1 : 0;  // over 1.5 : 1
+}
+
 int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s,
             const MsdStage *stg = nullptr) {
     for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
@@ -988,6 +1007,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         }
         bp.ntab = ntab;
         bp.full_radix = getenv("SMJ_PASSB_FULL") && atoi(getenv("SMJ_PASSB_FULL")) == 1;
+        bp.combined = msd_combined(in, ntab);
         bp.spl = ms->spl;
         bp.plan = ms->plan;
         HIP_TRY(launch_msd_bases(bp, s));
@@ -1016,6 +1036,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
             gp.tile[x] = TB_[x];
         }
         gp.ntab = ntab;
+        gp.combined = msd_combined(in, ntab);
         gp.part = ms->gpart;
         gp.ngrp = ms->ngrp;
         gp.groups = ms->groups;
@@ -1046,6 +1067,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.bg_seg = bl.seg;
     fp.ntab = ntab;
     fp.join = join;
+    fp.combined = msd_combined(in, ntab);
     fp.key2 = key2;
     if (t_slot < 0) g_fin_last = fp;
     size_t pf;
@@ -1148,7 +1170,12 @@ int64_t msd_large_parts(const MsdIn *in, int ntab) {
     if (g_force_parts > 0) return std::min(64, g_force_parts);
     int64_t mx = 0;
     for (int x = 0; x < ntab; x++) mx = std::max(mx, in[x].n);
-    return std::min<int64_t>(64, (mx + kMsdPartRows - 1) / kMsdPartRows);
+    static const int64_t rows = [] {  // SMJ_PART_ROWS: A/B of the part size
+        const char *e = getenv("SMJ_PART_ROWS");
+        const int64_t v = e ? (int64_t)atof(e) : 0;
+        return v >= 1000000 && v <= kMsdSingleMax ? v : kMsdPartRows;
+    }();
+    return std::min<int64_t>(64, (mx + rows - 1) / rows);
 }
 
 // The one-pass partition (msd_part1_kernel) for tables of up to 8 columns;

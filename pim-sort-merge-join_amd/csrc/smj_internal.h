@@ -184,6 +184,11 @@ constexpr int kBitsB = 11;
 constexpr int kRadB = 1 << kBitsB;         // 2048 pass-B sub-buckets per bucket
 constexpr int kOffsB = kRadB + 8;          // offsB row (u16): 2048 starts + the tile's row count, padded to 16 B
 constexpr int kGroupCap = 1024;            // rows per table in one final group (LDS)
+constexpr int kStRows = 2 * kGroupCap;     // rows of both tables in one group of the staged final kernel
+#ifndef SMJ_ST_LIST
+#define SMJ_ST_LIST 256
+#endif
+constexpr int kStList = SMJ_ST_LIST;       // pass-B tiles per bucket and table a staged group may span
 constexpr int kStageRange = 4096;          // key range of the staged final path's counting sort
 #ifndef SMJ_BG_MAX_ROWS
 #define SMJ_BG_MAX_ROWS 131072
@@ -271,7 +276,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t ngiant;     // groups over kBgMaxRows rows registered as jobs
     uint32_t njobs;      // their jobs
     uint32_t err;        // bit 0: a cross-workgroup wait gave up (msd_group_kernel) -> SMJ_ERR_TIMEOUT;
-                         // bit 1: inconsistent run metadata (SMJ_BOUNDS builds) -> SMJ_ERR_HIP
+                         // bit 1: inconsistent run metadata (SMJ_BOUNDS builds) -> SMJ_ERR_HIP;
+                         // bit 2: a combined group missed the staged kernel (a bug) -> SMJ_ERR_HIP
 };
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)
@@ -281,6 +287,7 @@ struct MsdBasesParams {
     int tile[2];
     int ntab;
     int full_radix;            // ablation (SMJ_PASSB_FULL=1): D = kRadB pass-B sub-buckets in every bucket
+    int combined;              // 2-column tables: final groups of <= 2 kGroupCap rows of both tables together
     const int64_t *spl;
     MsdBucket *bk[2];
     MsdPlan *plan;
@@ -316,6 +323,7 @@ struct MsdGroupParams {
     uint32_t *counts;       // dense: join rows per group (single-key groups: known here)
     MsdPlan *plan;
     uint32_t *single_list, *big_list;  // dense group indices
+    int combined;           // as MsdBasesParams::combined
 };
 struct MsdTab {          // a table as the final kernels see it
     const int64_t *tempB;
@@ -339,6 +347,7 @@ struct MsdFinalParams {
     uint32_t *gh;        // [job][2][kStageRange] residual counts of each job's rows
     uint32_t bg_max, bg_seg;  // msd_bg_limits()
     int ntab, join, key2, dbg;
+    int combined;        // the group kernel packed combined groups (staged kernel: R rows then S rows in one sort)
 };
 
 // ---- C-ABI internals shared by smj_api.hip and smj_host.hip -------------------

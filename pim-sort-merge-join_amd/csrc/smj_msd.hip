@@ -726,7 +726,8 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             // (uniform keys) below the cap: a multi-key sub-bucket over the cap
             // would leave the LDS path for the (slow) LSD fallback
             constexpr uint64_t kFill = (uint64_t)kGroupCap * 15 / 16, kOne = (uint64_t)kGroupCap * 13 / 16;
-            const uint64_t Lm = max(Lt[0], Lt[1]);
+            // (combined packing: groups of ~2 kFill rows of both tables)
+            const uint64_t Lm = p.combined ? ((uint64_t)Lt[0] + Lt[1] + 1u) / 2u : (uint64_t)max(Lt[0], Lt[1]);
             uint64_t D = kRadB;
             if (Lm > 0 && !p.full_radix) {
                 const uint64_t k = (uint64_t)kRadB * kFill / Lm;
@@ -1600,6 +1601,21 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
+    // Combined packing (2-column tables, round 3): a group holds up to
+    // kStRows rows of both tables together when every group of the bucket is
+    // sure to fit the staged final kernel -- sub-buckets of <= kStageRange keys
+    // (then maxspan keeps a group's span within the counting range) and <=
+    // kStList pass-B tiles per table; elsewhere <= kGroupCap rows per table.
+    bool comb = p.combined != 0;
+    {
+        const MsdBucket &b0 = p.bk[0][a];
+        const uint64_t w = b0.scale == 0 ? 1ull
+                           : b0.s32      ? ((1ull << 32) + b0.s32 - 1u) / b0.s32 + 1u
+                                         : (uint64_t)((((unsigned __int128)1 << 64) + b0.scale - 1u) / b0.scale) + 1u;
+        comb = comb && w <= (uint64_t)kStageRange;
+        for (int x = 0; x < p.ntab; x++)
+            comb = comb && (p.bk[x][a].L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x] <= (uint32_t)kStList;
+    }
     // The greedy packing (a group takes consecutive non-empty sub-buckets while
     // both tables stay <= kGroupCap rows and the sub-bucket span < maxspan; a
     // sub-bucket over the cap is a group of its own), computed in parallel:
@@ -1612,16 +1628,27 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         int f = kRadB;
         if (i < kRadB) {
             int lim = min(kRadB, i + maxspan);
-#pragma unroll
-            for (int x = 0; x < 2; x++) {  // first m in [i + 2, kRadB] with P[m] - P[i] > cap: j = m - 1
-                const uint32_t cap = s_P[x][i] + (uint32_t)kGroupCap;
-                int lo = i + 2, hi = kRadB + 1;  // answer in [lo, hi); hi = none
+            if (comb) {  // first m in [i + 2, kRadB] with the rows of both tables in [i, m) over kStRows
+                const uint32_t cap = s_P[0][i] + s_P[1][i] + (uint32_t)kStRows;
+                int lo = i + 2, hi = kRadB + 1;
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
-                    if (s_P[x][mid] > cap) hi = mid; else lo = mid + 1;
+                    if (s_P[0][mid] + s_P[1][mid] > cap) hi = mid; else lo = mid + 1;
                 }
                 if (lo <= kRadB) lim = min(lim, lo - 1);
-                else if (i + 1 <= kRadB && s_P[x][i + 1] > cap) lim = min(lim, i + 1);
+                else if (i + 1 <= kRadB && s_P[0][i + 1] + s_P[1][i + 1] > cap) lim = min(lim, i + 1);
+            } else {
+#pragma unroll
+                for (int x = 0; x < 2; x++) {  // first m in [i + 2, kRadB] with P[m] - P[i] > cap: j = m - 1
+                    const uint32_t cap = s_P[x][i] + (uint32_t)kGroupCap;
+                    int lo = i + 2, hi = kRadB + 1;  // answer in [lo, hi); hi = none
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_P[x][mid] > cap) hi = mid; else lo = mid + 1;
+                    }
+                    if (lo <= kRadB) lim = min(lim, lo - 1);
+                    else if (i + 1 <= kRadB && s_P[x][i + 1] > cap) lim = min(lim, i + 1);
+                }
             }
             f = next_nz(max(lim, i + 1));
         }
@@ -1713,7 +1740,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.outR = p.bk[0][a].row_start + s_P[0][b0];
         gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_P[1][b0] : 0u;
         gr.flags = 0;
-        if (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap)
+        if (comb ? gr.nR + gr.nS > (uint32_t)kStRows : (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap))
             gr.flags = single_sub ? kGroupSingle : kGroupBig;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
@@ -2538,28 +2565,48 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
 // ---- 2-column staged path --------------------------------------------------------
 // The common case, (key, payload) tables: every row of a group is gathered
 // ONCE (16 B, lanes on consecutive rows of a pass-B tile range); its payload
-// column is staged in LDS; the 32-bit sort words (key - base) << 10 | row are counting-sorted
+// column is staged in LDS; the 32-bit sort words (key - base) << 11 | row are counting-sorted
 // (base and key span come from the group record, no reduction); the zip
 // join reads its run starts straight from the histogram; sorted rows and
 // join rows leave through LDS as coalesced stores.  The next group's rows
 // are gathered into registers while this one is sorted and written.  Groups
-// outside its limits (key span > kStageRange, an equal-key run >
-// kMaxDupRun, > kStList pass-B tiles) go to the radix list.
+// outside its limits (key span > kStageRange, > kStList pass-B tiles) go to
+// the radix list.
+// Round 3: a group holds up to kStRows = 2048 rows of BOTH tables together
+// (group rows [0, nR) are R's, [nR, nR + nS) S's; the group kernel packs
+// nR + nS <= kStRows where the bucket allows it), so a skewed pair (C5: S
+// has ten times R's rows) fills a group as well as a balanced one does.
 constexpr int kStThreads = 512, kStWaves = kStThreads / 64;  // 3 per CU (1024-thread workgroups: slower, r01z)
 #ifndef SMJ_ST_GRID
 #define SMJ_ST_GRID 768
 #endif
-#ifndef SMJ_ST_LIST
-#define SMJ_ST_LIST 256
-#endif
 #ifndef SMJ_ST_RECS
 #define SMJ_ST_RECS 16
 #endif
-constexpr int kStList = SMJ_ST_LIST;           // pass-B tiles per bucket and table a staged group may span
-constexpr int kStIt = kGroupCap / kStThreads;  // rows per table per thread
+constexpr int kStIt = kStRows / kStThreads;    // group rows per thread: tid + k * kStThreads
+constexpr int kStIdx = 11;                     // sort word = residual << 11 | group row
+constexpr uint32_t kStIdxMask = (1u << kStIdx) - 1u;
+static_assert(kStRows == (1 << kStIdx) && kStList * 2 <= 65536, "group rows / list entries fit their fields");
 constexpr int kStRange = kStageRange;
 constexpr int kStRecs = SMJ_ST_RECS;           // group records per LDS chunk (two chunks in flight)
-static_assert(kFinIdxBits == 10, "sort word = residual << 10 | group row");
+
+// Group-row layout of the staged kernel: R's rows are group rows [0, nR),
+// S's [sp, sp + nS).  COMB (combined groups, <= kStRows rows of both tables):
+// sp = nR.  Per-table groups (<= kGroupCap rows each): sp = kGroupCap, so
+// items k < kStIt / 2 of a thread (group rows tid + k * kStThreads) are R's
+// and the others S's -- a compile-time table per item, as the balanced
+// tables (C3, C4) want it.
+template <bool COMB>
+struct StSplit {
+    uint32_t nR, nS, sp;
+    __device__ __forceinline__ StSplit(const MsdFinalParams &p, const MsdGroup &g)
+        : nR(g.nR), nS(p.ntab > 1 ? g.nS : 0u), sp(COMB ? g.nR : (uint32_t)kGroupCap) {}
+    __device__ __forceinline__ bool is_s(int k, uint32_t v) const { return COMB ? v >= nR : k >= kStIt / 2; }
+    __device__ __forceinline__ bool valid(int k, uint32_t v) const {
+        return COMB ? v < nR + nS : (k < kStIt / 2 ? v < nR : v - sp < nS);
+    }
+    __device__ __forceinline__ bool valid_pos(uint32_t q) const { return q < nR || q - sp < nS; }
+};
 
 // LDS: 50.4 KiB and 80 VGPRs (launch bounds: 6 waves per SIMD), so three
 // workgroups share a CU (24 waves).  Only the payload column is staged: a
@@ -2569,17 +2616,18 @@ static_assert(kFinIdxBits == 10, "sort word = residual << 10 | group row");
 // per CU is slower (2.03 ms), and without opaque_tid (below) it spills 100 B
 // per lane at 80 VGPRs and runs at 2.74 ms.
 struct StSmem {
-    int64_t pay[2][kGroupCap];        // payload (non-key) column, gather order
-    uint32_t key[2][kGroupCap];       // sort words, sorted
-    uint32_t hist[2][kStRange / 2];   // packed u16 bins (zeroed for the next group during the emit)
+    int64_t pay[kStRows];             // payload (non-key) column, group-row order
+    uint32_t key[kStRows];            // sort words, sorted: R's at [0, nR), S's at [nR, nR + nS)
+    uint32_t hist[2][kStRange / 2];   // per table, packed u16 bins (zeroed for the next group during the emit)
     union {
         struct {
-            uint2 list[2][kStList];                // run lists of the next group: {tempB row, group row}
-            uint16_t at[2][kGroupCap];             // list entry of the non-empty range starting at row v
-            uint32_t starts[2][kGroupCap / 32];    // bitmap: a non-empty range starts at row v
-            uint16_t btab[2][kGroupCap / 64];      // list entry holding row 64 * b
+            uint2 list[2][kStList];          // run lists of the next group: {tempB row, table row}
+            uint16_t at[kStRows];            // entry (x * kStList + j) of the non-empty range starting at group row v
+            uint32_t starts[kStRows / 32];   // bitmap: a non-empty range starts at group row v
+            uint16_t btab[kStRows / 64];     // entry holding group row 64 * b
         } L;
-        uint32_t match[kGroupCap];       // join rows: R position << 10 | S position
+        uint32_t match[kGroupCap];           // join rows (<= min(nR, nS)): R position << 11 | S position
+        uint16_t lsd[kStIt * kStWaves][128]; // in-LDS LSD: per 64-row group and digit, counts then starts
     };
     MsdGroup recs[2 * kStRecs];       // ring of this workgroup's group records
     uint32_t wsum[2][kStWaves];
@@ -2597,9 +2645,12 @@ struct StSmem {
 #endif
 #define ST_ABL(bit) (SMJ_ABLATE && (p.dbg & (bit)))
 
+template <bool COMB>
 __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g) {
+    const uint32_t nS = p.ntab > 1 ? g.nS : 0u;
     return !g.flags && g.span <= (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStList &&
-           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList);
+           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList) &&
+           (COMB ? g.nR + nS <= (uint32_t)kStRows : g.nR <= (uint32_t)kGroupCap && nS <= (uint32_t)kGroupCap);
 }
 
 __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
@@ -2624,35 +2675,39 @@ __device__ unsigned long long g_st_sub[8];
         st_t = t_;                                                  \
     }
 
+template <bool COMB>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
-                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[2][kStIt],
+                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
                                                StSmem &sm);
 
 // run lists from the offsB values (union region), then the row gathers of
-// group g into registers (row v = tid + k * kStThreads).  Row v's range is
-// found in O(1): the range holding the wave's first row (btab) and the last
+// group g into registers (group row v = tid + k * kStThreads).  Row v's range
+// is found in O(1): the range holding the wave's first row (btab) and the last
 // non-empty range starting in (64b, v] (bitmap word + at[]; the list also
 // holds the group's empty ranges, so a popcount of the bitmap would not
-// index it).
+// index it).  S's ranges start at group row nR + their table row.
+template <bool COMB>
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
-                                         const uint32_t (&o1)[2], i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb) {
+                                         const uint32_t (&o1)[2], i64x2 (&rows)[kStIt], StSmem &sm, int &wsb) {
     const uint32_t tid = opaque_tid();
-    for (uint32_t i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
+    for (uint32_t i = tid; i < kStRows / 32; i += kStThreads) sm.L.starts[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
     const uint32_t ex = block_excl_scan_nb<kStWaves>(len[0] | (len[1] << 16), sm.wsum[wsb], &tot);  // + barrier
     wsb ^= 1;
-    st_issue_lists(p, g, o0, o1, ex, rows, sm);
+    st_issue_lists<COMB>(p, g, o0, o1, ex, rows, sm);
 }
 
 // st_issue after the run-length scan: ex = this thread's exclusive prefix of
 // (len R | len S << 16), the start bitmap zeroed and ordered by a barrier
+template <bool COMB>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
-                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[2][kStIt],
+                                               const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
                                                StSmem &sm) {
     const uint32_t tid = opaque_tid(), lane = tid & 63;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
+    const StSplit<COMB> L(p, g);
 #pragma unroll
     for (int x = 0; x < 2; x++) {
         if (tid < g.kt[x] && x < p.ntab) {
@@ -2664,151 +2719,153 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
             }
             sm.L.list[x][tid] = make_uint2((g.tb[x] + tid) * (uint32_t)p.tab[x].tile + o0[x], vs);
             if (len[x]) {
-                sm.L.at[x][vs] = (uint16_t)tid;
-                atomicOr(&sm.L.starts[x][vs >> 5], 1u << (vs & 31));
-                for (uint32_t b = (vs + 63) >> 6; b << 6 < vs + len[x]; b++) sm.L.btab[x][b] = (uint16_t)tid;
+                const uint32_t c = (x ? L.sp : 0u) + vs;  // group row of the range's first row
+                const uint16_t e = (uint16_t)(x * kStList + tid);
+                sm.L.at[c] = e;
+                atomicOr(&sm.L.starts[c >> 5], 1u << (c & 31));
+                for (uint32_t b = (c + 63) >> 6; b << 6 < c + len[x]; b++) sm.L.btab[b] = e;
             }
         }
     }
     __syncthreads();
     ST_SUB(4);
-    const uint32_t n[2] = {g.nR, p.ntab > 1 ? g.nS : 0u};
+    const i64x2 *tB0 = reinterpret_cast<const i64x2 *>(p.tab[0].tempB);
+    const i64x2 *tB1 = reinterpret_cast<const i64x2 *>(p.tab[1].tempB);
 #pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t v = tid + k * kStThreads, b = v >> 6;
-            i64x2 r = {0, 0};
-            if (v < n[x]) {
-                const uint64_t m = ((uint64_t)sm.L.starts[x][2 * b + 1] << 32 | sm.L.starts[x][2 * b]) &
-                                   ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
-                const uint32_t j = m ? sm.L.at[x][(b << 6) + 63 - __clzll((long long)m)] : sm.L.btab[x][b];
-                const uint2 e = sm.L.list[x][j];
-                if (ST_ABL(4)) {
-                    const int64_t k = g.base + (int64_t)((v * 3u) % max(g.span, 1u));
-                    r = {p.tab[x].key ? (int64_t)v : k, p.tab[x].key ? k : (int64_t)v};
-                } else {
-                    int64_t ix = (int64_t)e.x + (v - e.y);
-                    if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
-                        atomicOr(&p.plan->err, 2u);
-                        ix = 0;
-                    }
-                    r = reinterpret_cast<const i64x2 *>(p.tab[x].tempB)[ix];
+    for (int k = 0; k < kStIt; k++) {
+        const uint32_t v = tid + k * kStThreads, b = v >> 6;
+        i64x2 r = {0, 0};
+        if (L.valid(k, v)) {
+            const uint64_t m = ((uint64_t)sm.L.starts[2 * b + 1] << 32 | sm.L.starts[2 * b]) &
+                               ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
+            const uint32_t e = m ? sm.L.at[(b << 6) + 63 - __clzll((long long)m)] : sm.L.btab[b];
+            const uint32_t x = COMB ? (e >= (uint32_t)kStList ? 1u : 0u) : (L.is_s(k, v) ? 1u : 0u);
+            const uint2 le = sm.L.list[x][e - x * kStList];
+            const uint32_t vt = v - (x ? L.sp : 0u);  // table row
+            if (ST_ABL(4)) {
+                const int64_t kk = g.base + (int64_t)((v * 3u) % max(g.span, 1u));
+                r = {p.tab[x].key ? (int64_t)v : kk, p.tab[x].key ? kk : (int64_t)v};
+            } else {
+                int64_t ix = (int64_t)le.x + (vt - le.y);
+                if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
+                    atomicOr(&p.plan->err, 2u);
+                    ix = 0;
                 }
+                r = (x ? tB1 : tB0)[ix];
             }
-            rows[x][k] = r;
         }
+        rows[k] = r;
+    }
     ST_SUB(5);
 }
 
 __device__ __forceinline__ int64_t st_key(const i64x2 &r, int key) { return key ? r.y : r.x; }
 
-// Stable LSD sort of a group's sort words by their residual (two 6-bit
-// digits) for groups whose equal-key runs are too long for the odd-even
-// rounds (Zipf-skewed keys: C5).  w[x][k] = the word of group row
-// v = tid + k * kStThreads (~0u: none; overwritten); words leave sorted in
-// sm.key[x].
-// A pass ranks each (item, wave) group of 64 rows by wave ballots on the
-// digit, prefixes the 16 groups' counts per digit (v order = item, wave,
-// lane) and scatters; pass 2 reads pass 1's order back the same way.  Both
-// tables go through a pass together (round 3: half the barriers, and the
-// two per-digit prefixes run on two waves at once).
-// Counters: 2 x 16 x 64 words in the list region (idle during the sort).
-__device__ __forceinline__ void st_lsd(uint32_t (&cur)[2][kStIt], const int (&n)[2], StSmem &sm) {
-    constexpr int G = kStIt * kStWaves, DB = 6, D = 1 << DB;
-    static_assert(2 * G * D * 4 <= (int)sizeof(sm.L), "LSD counters of both tables fit the list region");
-    static_assert(kStRange <= (1 << (2 * DB)), "two digits cover the residual");
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(&sm.L);  // [table][g][d]
+// Stable LSD sort of a group's sort words for groups whose equal-key runs are
+// too long for the odd-even rounds (Zipf-skewed keys: C5).  w[k] = the word
+// of group row v = tid + k * kStThreads (~0u: none; overwritten); words leave
+// in sm.key sorted by (table, residual, group row).  Pass 1 sorts by the
+// residual's low 6 bits, pass 2 by (table << 6 | its high 6 bits), each a
+// stable counting pass: every (item, wave) group of 64 rows is ranked by wave
+// ballots on the digit, and one wave prefixes the 32 groups' u16 counts per
+// digit (v order = item, wave, lane; two digits per lane).
+__device__ __forceinline__ void st_lsd(uint32_t (&cur)[kStIt], uint32_t nR, uint32_t sp, int n, StSmem &sm) {
+    constexpr int G = kStIt * kStWaves, DB = 6, D = 128;
+    static_assert(sizeof(sm.lsd) <= sizeof(sm.L), "LSD counters fit the list region");
+    static_assert(kStRange <= (1 << (2 * DB)), "two 6-bit digits cover the residual");
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+    uint32_t *c32 = reinterpret_cast<uint32_t *>(&sm.lsd[0][0]);
 #pragma unroll
     for (int pass = 0; pass < 2; pass++) {
-        const int sh = kFinIdxBits + DB * pass;
-        for (int i = tid; i < 2 * G * D; i += kStThreads) cnt[i] = 0;
+        for (int i = tid; i < G * D / 2; i += kStThreads) c32[i] = 0;
         __syncthreads();
-        uint32_t rk[2][kStIt];
+        uint32_t rk[kStIt], dg[kStIt];
 #pragma unroll
-        for (int x = 0; x < 2; x++)
+        for (int k = 0; k < kStIt; k++) {
+            const bool v = cur[k] != ~0u;
+            const uint32_t res = cur[k] >> kStIdx;
+            const uint32_t d = pass == 0 ? (res & 63u) : ((((cur[k] & kStIdxMask) >= sp) ? 64u : 0u) | (res >> DB));
+            dg[k] = d;
+            const uint64_t act = __ballot(v);
+            uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
 #pragma unroll
-            for (int k = 0; k < kStIt; k++) {
-                const bool v = cur[x][k] != ~0u;
-                const uint32_t d = (cur[x][k] >> sh) & (D - 1);
-                const uint64_t act = __ballot(v);
-                uint32_t plo = (uint32_t)act, phi = (uint32_t)(act >> 32);
-#pragma unroll
-                for (int b = 0; b < DB; b++) {
-                    const uint32_t sb = (uint32_t)((int32_t)(d << (31 - b)) >> 31);
-                    const uint64_t bb = __ballot(sb != 0u);
-                    plo = peer_fold(plo, (uint32_t)bb, sb);
-                    phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
-                }
-                rk[x][k] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
-                const uint64_t peers = ((uint64_t)phi << 32) | plo;
-                if (v && (peers >> lane) == 1ull) cnt[(x * G + k * kStWaves + wave) * D + d] = (uint32_t)__popcll(peers);
+            for (int b = 0; b < DB + 1; b++) {
+                const uint32_t sb = (uint32_t)((int32_t)(d << (31 - b)) >> 31);
+                const uint64_t bb = __ballot(sb != 0u);
+                plo = peer_fold(plo, (uint32_t)bb, sb);
+                phi = peer_fold(phi, (uint32_t)(bb >> 32), sb);
             }
+            rk[k] = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+            const uint64_t peers = ((uint64_t)phi << 32) | plo;
+            if (v && (peers >> lane) == 1ull) sm.lsd[k * kStWaves + wave][d] = (uint16_t)__popcll(peers);
+        }
         __syncthreads();
-        if (tid < 2 * D && n[tid >> DB] > 0) {  // wave x, lane d: prefix over the groups in v order, then the digits
-            uint32_t *c = cnt + (tid >> DB) * G * D;
-            const int d = tid & (D - 1);
-            uint32_t t = 0;
-#pragma unroll 4
-            for (int g = 0; g < G; g++) t += c[g * D + d];
-            uint32_t run = wave_incl_scan(t, lane) - t;
-#pragma unroll 4
+        if (wave == 0) {  // lane l: digits 2l, 2l + 1 (one u32 word per group)
+            uint32_t t0 = 0, t1 = 0;
+#pragma unroll 8
             for (int g = 0; g < G; g++) {
-                const uint32_t q = c[g * D + d];
-                c[g * D + d] = run;
-                run += q;
+                const uint32_t w2 = c32[g * (D / 2) + lane];
+                t0 += w2 & 0xffffu;
+                t1 += w2 >> 16;
+            }
+            uint32_t r0 = wave_incl_scan(t0 + t1, lane) - (t0 + t1), r1 = r0 + t0;
+#pragma unroll 8
+            for (int g = 0; g < G; g++) {
+                const uint32_t w2 = c32[g * (D / 2) + lane];
+                c32[g * (D / 2) + lane] = r0 | (r1 << 16);
+                r0 += w2 & 0xffffu;
+                r1 += w2 >> 16;
             }
         }
         __syncthreads();
+        // (pass 2 puts S's rows right after R's: they belong at sp)
+        const uint32_t shS = pass == 1 ? sp - nR : 0u;
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < kStIt; k++)
-                if (cur[x][k] != ~0u)
-                    sm.key[x][cnt[(x * G + k * kStWaves + wave) * D + ((cur[x][k] >> sh) & (D - 1))] + rk[x][k]] =
-                        cur[x][k];
+        for (int k = 0; k < kStIt; k++)
+            if (cur[k] != ~0u)
+                sm.key[(uint32_t)sm.lsd[k * kStWaves + wave][dg[k]] + rk[k] + ((dg[k] & 64u) ? shS : 0u)] = cur[k];
         __syncthreads();
         if (pass == 0) {
 #pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int k = 0; k < kStIt; k++) {
-                    const int o = tid + k * kStThreads;
-                    cur[x][k] = o < n[x] ? sm.key[x][o] : ~0u;
-                }
+            for (int k = 0; k < kStIt; k++) {
+                const int o = tid + k * kStThreads;
+                cur[k] = o < n ? sm.key[o] : ~0u;
+            }
         }
     }
 }
 
 // stage + counting sort of group g whose rows are in `rows`, then the zip
-// join lookups (mmask / part); false: an equal-key run over kMaxDupRun (the
-// group is handed to the radix list)
+// join lookups (mmask / part)
+template <bool COMB>
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
-                                        const i64x2 (&rows)[2][kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
+                                        const i64x2 (&rows)[kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
                                         uint32_t &nex) {
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
-    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
-    uint32_t w[2][kStIt];  // residual << 16 | atomic rank among its equal residuals (~0u: no row)
+    const StSplit<COMB> L(p, g);
+    const uint32_t nR = L.nR, nS = L.nS, sp = L.sp;
+    const int n = (int)(nR + nS);
+    uint32_t w[kStIt];  // residual << 16 | atomic rank among its table's equal residuals (~0u: no row)
     if (tid == 0) sm.flag[wsb] = 0;  // longest equal-key run (0: none)
     // for the next group's st_issue_lists (the list region is idle until then;
     // the barriers below order this before its atomicOr)
-    for (int i = tid; i < 2 * kGroupCap / 32; i += kStThreads) (&sm.L.starts[0][0])[i] = 0;
+    for (int i = tid; i < kStRows / 32; i += kStThreads) sm.L.starts[i] = 0;
+    const int kc0 = p.tab[0].key, kc1 = p.tab[1].key;
 #pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const int v = tid + k * kStThreads;
-            w[x][k] = ~0u;
-            if (v < n[x]) {
-                sm.pay[x][v] = p.tab[x].key ? rows[x][k].x : rows[x][k].y;
-                const uint32_t res = (uint32_t)((uint64_t)st_key(rows[x][k], p.tab[x].key) - (uint64_t)g.base);
-                const uint32_t sh = 16u * (res & 1u);
-                w[x][k] = (res << 16) | ((atomicAdd(&sm.hist[x][res >> 1], 1u << sh) >> sh) & 0xffffu);
-            }
+    for (int k = 0; k < kStIt; k++) {
+        const int v = tid + k * kStThreads;
+        w[k] = ~0u;
+        if (L.valid(k, (uint32_t)v)) {
+            const bool x = L.is_s(k, (uint32_t)v);
+            const int kc = x ? kc1 : kc0;
+            sm.pay[v] = kc ? rows[k].x : rows[k].y;
+            const uint32_t res = (uint32_t)((uint64_t)st_key(rows[k], kc) - (uint64_t)g.base);
+            const uint32_t sh = 16u * (res & 1u);
+            w[k] = (res << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][res >> 1], 1u << sh) >> sh) & 0xffffu);
         }
+    }
     __syncthreads();
     ST_SUB(0);
     constexpr int W = kStRange / 2 / kStThreads;  // histogram words per thread
@@ -2854,7 +2911,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     const bool lsd = fl > (uint32_t)SMJ_ST_MAXRUN;  // block-uniform
     if (lsd && tid == 0) atomicAdd(&p.plan->nlsd, 1u);
 #pragma unroll
-    for (int x = 0; x < 2; x++) {
+    for (int x = 0; x < 2; x++) {  // per-table starts (table rows)
         uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);
 #pragma unroll
         for (int i = 0; i < W; i++) {
@@ -2866,38 +2923,37 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     __syncthreads();
     if (lsd) {  // an equal-key run over kMaxDupRun: stable LSD instead of scatter + rounds
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < kStIt; k++)
-                if (w[x][k] != ~0u) w[x][k] = ((w[x][k] >> 16) << kFinIdxBits) | (uint32_t)(tid + k * kStThreads);
-        st_lsd(w, n, sm);
+        for (int k = 0; k < kStIt; k++)
+            if (w[k] != ~0u) w[k] = ((w[k] >> 16) << kStIdx) | (uint32_t)(tid + k * kStThreads);
+        st_lsd(w, nR, sp, n, sm);
     } else {
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int k = 0; k < kStIt; k++)
-                if (w[x][k] != ~0u) {
-                    const uint32_t res = w[x][k] >> 16, sh = 16u * (res & 1u);
-                    sm.key[x][((sm.hist[x][res >> 1] >> sh) & 0xffffu) + (w[x][k] & 0xffffu)] =
-                        (res << kFinIdxBits) | (uint32_t)(tid + k * kStThreads);
-                }
+        for (int k = 0; k < kStIt; k++)
+            if (w[k] != ~0u) {
+                const uint32_t v = (uint32_t)(tid + k * kStThreads), x = L.is_s(k, v) ? 1u : 0u;
+                const uint32_t res = w[k] >> 16, sh = 16u * (res & 1u);
+                sm.key[(x ? sp : 0u) + ((sm.hist[x][res >> 1] >> sh) & 0xffffu) + (w[k] & 0xffffu)] =
+                    (res << kStIdx) | v;
+            }
         __syncthreads();
     }
     ST_SUB(2);
     // equal residuals were placed in atomic order: odd-even transposition
-    // rounds (as many as the longest run) order every run by group row.
-    // (Measured slower: ranking each run member by a scan of its run, r01k;
-    // the run's first thread insertion-sorting the run, r01ah: 2.81 vs 2.32 ms.)
-    static_assert(kGroupCap / 2 <= kStThreads, "one compare-exchange per thread per table and round");
+    // rounds (as many as the longest run) order every run by group row.  A
+    // pair across the R / S boundary never swaps (R's group rows are the
+    // smaller).  (Measured slower: ranking each run member by a scan of its
+    // run, r01k; the run's first thread insertion-sorting the run, r01ah:
+    // 2.81 vs 2.32 ms.)
+    static_assert(kStRows / 2 == 2 * kStThreads, "two compare-exchanges per thread and round");
     for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd) ? 0u : fl); rd++) {
 #pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const int q = 2 * tid + (int)(rd & 1u);
-            if (q + 1 < n[x]) {
-                const uint32_t a = sm.key[x][q], b = sm.key[x][q + 1];
-                if ((a >> kFinIdxBits) == (b >> kFinIdxBits) && a > b) {
-                    sm.key[x][q] = b;
-                    sm.key[x][q + 1] = a;
+        for (int h = 0; h < 2; h++) {
+            const uint32_t q = 2u * (uint32_t)(tid + h * kStThreads) + (rd & 1u);
+            if (L.valid_pos(q) && L.valid_pos(q + 1)) {
+                const uint32_t a = sm.key[q], b = sm.key[q + 1];
+                if ((a >> kStIdx) == (b >> kStIdx) && a > b) {
+                    sm.key[q] = b;
+                    sm.key[q + 1] = a;
                 }
             }
         }
@@ -2907,20 +2963,24 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // zip join from the histogram starts: R position i with residual r pairs
     // with S position startS(r) + (i - startR(r)) while i - startR(r) < countS(r)
     mmask = 0;
-    if (p.join && n[0] > 0 && n[1] > 0) {
+    // R positions tid * JI + q (consecutive per thread: the block scan of the
+    // match counts keeps R order); per-table groups have <= kGroupCap R rows
+    constexpr int JI = COMB ? kStIt : kStIt / 2;
 #pragma unroll
-        for (int q = 0; q < kStIt; q++) {
-            const int i = tid * kStIt + q;
-            part[q] = 0;
-            if (i < n[0]) {
-                const uint32_t res = sm.key[0][i] >> kFinIdxBits, sh = 16u * (res & 1u);
+    for (int q = 0; q < kStIt; q++) part[q] = 0;
+    if (p.join && nR > 0 && nS > 0) {
+#pragma unroll
+        for (int q = 0; q < JI; q++) {
+            const uint32_t i = (uint32_t)tid * JI + q;
+            if (i < nR) {
+                const uint32_t res = sm.key[i] >> kStIdx, sh = 16u * (res & 1u);
                 const uint32_t sR = (sm.hist[0][res >> 1] >> sh) & 0xffffu;
                 const uint32_t hS = sm.hist[1][res >> 1];
                 const uint32_t sS = (hS >> sh) & 0xffffu;
                 const uint32_t eS = (res & 1u) ? ((res + 1u < (uint32_t)kStRange) ? (sm.hist[1][(res + 1) >> 1] & 0xffffu)
-                                                                                 : (uint32_t)n[1])
+                                                                                 : nS)
                                                : (hS >> 16);
-                const uint32_t occ = (uint32_t)i - sR;
+                const uint32_t occ = i - sR;
                 if (occ < eS - sS) {
                     part[q] = sS + occ;
                     mmask |= 1u << q;
@@ -2933,46 +2993,46 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
 
 // sorted rows out (coalesced), join rows out (word-coalesced); the histogram
 // is zeroed for the next group here (no one reads it after the lookups)
+template <bool COMB>
 __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, StSmem &sm,
                                         int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt]) {
-    constexpr uint32_t IDX = (1u << kFinIdxBits) - 1u;
     const int tid = opaque_tid();
-    const int n[2] = {(int)g.nR, p.ntab > 1 ? (int)g.nS : 0};
+    const StSplit<COMB> L(p, g);
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
         for (int i = tid; i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
     }
+    i64x2 *dR = reinterpret_cast<i64x2 *>(p.tab[0].out) + g.outR;
+    i64x2 *dS = reinterpret_cast<i64x2 *>(p.tab[1].out) + g.outS - L.sp;  // S row q - sp
+    const int kc0 = p.tab[0].key, kc1 = p.tab[1].key;
 #pragma unroll
-    for (int x = 0; x < 2; x++) {
-        i64x2 *dst = reinterpret_cast<i64x2 *>(p.tab[x].out) + (x ? g.outS : g.outR);
-        const int kc = p.tab[x].key;
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const int q = tid + k * kStThreads;
-            if (q < n[x] && !ST_ABL(2)) {
-                const uint32_t w = sm.key[x][q];
-                const int64_t key = g.base + (int64_t)(w >> kFinIdxBits), pay = sm.pay[x][w & IDX];
-                i64x2 r;
-                r.x = kc ? pay : key;
-                r.y = kc ? key : pay;
-                __builtin_nontemporal_store(r, dst + q);  // final rows: streamed
-            }
+    for (int k = 0; k < kStIt; k++) {
+        const uint32_t q = tid + k * kStThreads;
+        if (L.valid(k, q) && !ST_ABL(2)) {
+            const bool x = L.is_s(k, q);
+            const uint32_t w = sm.key[q];
+            const int64_t key = g.base + (int64_t)(w >> kStIdx), pay = sm.pay[w & kStIdxMask];
+            const int kc = x ? kc1 : kc0;
+            i64x2 r;
+            r.x = kc ? pay : key;
+            r.y = kc ? key : pay;
+            __builtin_nontemporal_store(r, (x ? dS : dR) + q);  // final rows: streamed
         }
     }
     if (!p.join || ST_ABL(8)) return;
-    const uint32_t *kR = sm.key[0], *kS = sm.key[1];
+    const uint32_t *kS = sm.key + L.sp;
     uint32_t total;
     uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
     wsb ^= 1;
     if (tid == 0) p.counts[gi] = total;
     if (total == 0) return;
+    constexpr int JI = COMB ? kStIt : kStIt / 2;  // as in st_sort
 #pragma unroll
-    for (int q = 0; q < kStIt; q++)
-        if ((mmask >> q) & 1u) sm.match[o++] = ((uint32_t)(tid * kStIt + q) << kFinIdxBits) | part[q];
+    for (int q = 0; q < JI; q++)
+        if ((mmask >> q) & 1u) sm.match[o++] = (((uint32_t)tid * JI + q) << kStIdx) | part[q];
     __syncthreads();
     // output word wd = row * 3 + column: R key, R payload, S payload
     int64_t *dst = p.slots + (int64_t)g.outR * 3;
-    const int kc0 = p.tab[0].key;
     // fixed trip count (total <= kGroupCap), see st_load_recs
     constexpr int EMIT_IT = (3 * kGroupCap + kStThreads - 1) / kStThreads;
 #pragma unroll
@@ -2983,10 +3043,10 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
             const uint32_t m = sm.match[row];
             int64_t val;
             if (c < 2) {  // R's columns: the key from the sort word, the payload staged
-                const uint32_t w = kR[m >> kFinIdxBits];
-                val = c == kc0 ? g.base + (int64_t)(w >> kFinIdxBits) : sm.pay[0][w & IDX];
+                const uint32_t w = sm.key[m >> kStIdx];
+                val = (int)c == kc0 ? g.base + (int64_t)(w >> kStIdx) : sm.pay[w & kStIdxMask];
             } else {      // S's column other than key2: its payload
-                val = sm.pay[1][kS[m & IDX] & IDX];
+                val = sm.pay[kS[m & kStIdxMask] & kStIdxMask];
             }
             __builtin_nontemporal_store(val, dst + wd);  // join slots: read back by msd_compact only
         }
@@ -3019,6 +3079,7 @@ constexpr int kXcdSlots = 8;
 #ifndef SMJ_ST_MINW
 #define SMJ_ST_MINW 6
 #endif
+template <bool COMB>
 __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     const int64_t ng = p.plan->ngroups;
@@ -3035,7 +3096,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
     if (0 < cnt) st_load_recs(p, g0, gs, 0, cnt, sm, 0);
     if (kStRecs < cnt) st_load_recs(p, g0, gs, kStRecs, cnt, sm, 1);
     __syncthreads();
-    i64x2 cur[2][kStIt];
+    i64x2 cur[kStIt];
     int wsb = 0;
     bool have = false;  // cur holds the rows of group gi
     for (int64_t li = 0; li < cnt; li++) {
@@ -3051,15 +3112,20 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
             have = false;
             continue;
         }
-        if (!st_ok(p, g)) {
-            if (opaque_tid() == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+        if (!st_ok<COMB>(p, g)) {
+            // (the group kernel packs over kGroupCap rows of a table only where
+            // every group fits this kernel: the radix tier takes <= kGroupCap)
+            if (opaque_tid() == 0) {
+                if (g.nR > (uint32_t)kGroupCap || (p.ntab > 1 && g.nS > (uint32_t)kGroupCap)) atomicOr(&p.plan->err, 4u);
+                p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            }
             have = false;
             continue;
         }
         if (!have) {
             uint32_t o0[2], o1[2];
             st_load_offs(p, g, o0, o1);
-            st_issue(p, g, o0, o1, cur, sm, wsb);
+            st_issue<COMB>(p, g, o0, o1, cur, sm, wsb);
             __syncthreads();  // the list region is reused by the join
         }
         FIN_STAMP(0);
@@ -3067,13 +3133,13 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         const MsdGroup &gn = sm.recs[(li + 1) % (2 * kStRecs)];
         uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
         if (li + 1 < cnt) {
-            nfit = st_ok(p, gn);
+            nfit = st_ok<COMB>(p, gn);
             if (nfit) st_load_offs(p, gn, o0, o1);
         }
         FIN_STAMP(1);
         uint32_t mmask = 0, part[kStIt];
         uint32_t nex;  // the next group's run-length prefix, scanned with this group's bins
-        const bool ok = st_sort(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex);  // cur is staged in LDS here
+        const bool ok = st_sort<COMB>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex);  // cur is staged in LDS here
         FIN_STAMP(2);
         // st_issue_lists writes only the list region (unused by the sort; its
         // start bitmap was zeroed, and its run lengths scanned, inside
@@ -3083,12 +3149,12 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         // wave reaches after its st_issue_lists reads.  Without a next group
         // one barrier does both.
         if (nfit)  // the next group's rows: in flight while this one is written out
-            st_issue_lists(p, gn, o0, o1, nex, cur, sm);
+            st_issue_lists<COMB>(p, gn, o0, o1, nex, cur, sm);
         else
             __syncthreads();
         FIN_STAMP(3);
         if (ok) {
-            st_emit(p, g, gi, sm, wsb, mmask, part);
+            st_emit<COMB>(p, g, gi, sm, wsb, mmask, part);
         } else {  // hand-over: the histogram still needs zeroing
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
             for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
@@ -4264,8 +4330,12 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     if (two) {
         constexpr int kStGrid = SMJ_ST_GRID;
         static_assert(kStGrid % kXcdSlots == 0, "whole XCD sets");
-        hipLaunchKernelGGL(msd_final_stage_kernel, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads),
-                           pad, s, p);
+        if (p.combined)
+            hipLaunchKernelGGL(msd_final_stage_kernel<true>, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads), pad,
+                               s, p);
+        else
+            hipLaunchKernelGGL(msd_final_stage_kernel<false>, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads), pad,
+                               s, p);
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
         q.radix_list = nullptr;

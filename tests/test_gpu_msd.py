@@ -68,6 +68,12 @@ FUSED_CASES = [
     # positions), and none at all (every splitter INT64_MAX)
     (200_000, 200_000, 2, 2, 0, 0, "uniform", (0, 599_000), (0, 590_000)),
     (100_000, 100_000, 2, 2, 0, 0, "uniform", (0, 299_995), (0, 299_995)),
+    # skewed sizes: final groups of up to 2048 rows of both tables together
+    # (R's rows then S's in one LDS sort; equal-key runs in both, the LSD path)
+    (30_000, 300_000, 2, 2, 0, 0, "uniform", (0, 5000), None),
+    (400_000, 25_000, 2, 2, 0, 0, "zipf", None, (0, 50)),
+    (20_000, 220_000, 2, 2, 0, 0, "dups", None, None),
+    (150_000, 1_200_000, 2, 2, 1, 1, "zipf", None, None),
     # rows wider than 8 columns (index sort + row gathers)
     (120_000, 90_000, 12, 9, 5, 8, "dups", (2, -10), (0, 0)),
     (50_000, 70_000, 20, 2, 19, 0, "uniform", None, (0, 5000)),
