@@ -436,6 +436,7 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_threads(COLS) == kMsdThreads ?
 // The look-back never waits on a later ticket, so the grid always drains; a
 // wait over 2^24 polls (a bug) sets flags[2].
 constexpr uint64_t kP1Agg = 1ull << 62, kP1Inc = 2ull << 62, kP1Val = (1ull << 62) - 1;
+
 template <int COLS>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart1Params p) {
     constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = 64;
@@ -496,6 +497,9 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart
         unsigned long long *st = p.status + t * nb;
         if (t > 0) {
             if (lane < nb) atomicExch(&st[lane], kP1Agg | cnt);
+            // (one predecessor per lane with all its part words -- 64 tiles per
+            // round trip -- was slower: C4 partition 19.4 vs 14.4 ms, its 7x
+            // more uncached status loads per round; profiles/r03/r03w_ab_c4.txt)
             const int J = max(1, 64 / nb);  // predecessors per round
             const int j = lane / nb, b = lane - j * nb;
             const bool lv = lane < J * nb;
