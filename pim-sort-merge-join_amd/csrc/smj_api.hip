@@ -1226,10 +1226,18 @@ int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64
             oc[64 + b] = cap;
             roff[x][b + 1] = roff[x][b] + cap;
         }
-        SMJ_TRY(grow(&ms->pst[x], &ms->c_pst[x], (size_t)roff[x][nb] * in[x].cols * sizeof(T)));
+        // the regions need ~1.3x the table on top of the in-place partition's
+        // memory: if the device cannot hold them, the counting partition runs
+        if (grow(&ms->pst[x], &ms->c_pst[x], (size_t)roff[x][nb] * in[x].cols * sizeof(T)) != SMJ_OK) {
+            (void)hipGetLastError();
+            return SMJ_OK;  // *staged = false
+        }
         nt[x] = (in[x].n + tile - 1) / tile;
     }
-    SMJ_TRY(grow(&ms->p1st, &ms->c_p1st, (size_t)std::max(nt[0], nt[1]) * nb * 8));
+    if (grow(&ms->p1st, &ms->c_p1st, (size_t)std::max(nt[0], nt[1]) * nb * 8) != SMJ_OK) {
+        (void)hipGetLastError();
+        return SMJ_OK;
+    }
     for (int x = 0; x < ntab; x++) {
         if (in[x].n == 0) continue;
         int64_t *d = ms->p1d + x * kP1Words;

@@ -492,6 +492,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart
         const uint32_t d = dig[it] & 0xffffu;
         dig[it] = (d << 16) | (s_bin[d] + wc[d] + (dig[it] >> 16));  // part << 16 | staging slot
     }
+    __syncthreads();  // counters read out: the region becomes the staging tile
+    // waves 1..7 stage their rows while wave 0 looks back (then stages its own)
     if (wave == 0) {
         const uint32_t cnt = lane < nb ? s_bin[lane + 1] - s_bin[lane] : 0u;
         unsigned long long *st = p.status + t * nb;
@@ -547,7 +549,6 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart
             if (t == p.ntiles - 1) p.tot[lane] = (long long)(ex + cnt);
         }
     }
-    __syncthreads();  // counters read out: the region becomes the staging tile
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) {
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart
             store_row<COLS>(s_rows + (size_t)slot * COLS, rows[it]);
             s_pd[slot] = (uint8_t)(dig[it] >> 16);
         }
-    __syncthreads();
+    __syncthreads();  // staging tile, prefixes and region checks published
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
         const uint32_t slot = (uint32_t)(tid + it * kMsdThreads);
