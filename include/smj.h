@@ -21,7 +21,9 @@
  *     points; smj_sort_merge_join / smj_dev_sort_merge_join map to them;
  *   - row counts must be < 2^31 per table (dpu_block_t.row_num is an int,
  *     common.h:17) and col_num in [1, 1024].  Tables over 1.6e8 rows are
- *     range-partitioned on the key inside the library, tables over 8 columns
+ *     range-partitioned on the key inside the library (in one pass into
+ *     part regions of ~1.3x the table of library scratch when the device
+ *     has room, else counted and scattered in place), tables over 8 columns
  *     are sorted as (key, row id) pairs and gathered; the
  *     LSD and partition entry points take 1..8 columns (else
  *     SMJ_ERR_UNSUPPORTED).

@@ -191,7 +191,7 @@ constexpr int kStRows = 2 * kGroupCap;     // rows of both tables in one group o
 constexpr int kStList = SMJ_ST_LIST;       // pass-B tiles per bucket and table a staged group may span
 constexpr int kStageRange = 4096;          // key range of the staged final path's counting sort
 #ifndef SMJ_BG_MAX_ROWS
-#define SMJ_BG_MAX_ROWS 131072
+#define SMJ_BG_MAX_ROWS 65536  // C5: 65536 beats 131072 and 32768 (profiles/r03/r03za/ab_c5_bg_max.txt)
 #endif
 constexpr uint32_t kBgMaxRows = SMJ_BG_MAX_ROWS;  // rows per table of an oversized group one workgroup sorts
 constexpr uint32_t kBgSeg = 32768;               // rows per table of a job of a larger group (msd_giant_*)

@@ -205,7 +205,7 @@ def test_small_span_oversized_groups_on_device(gpu, oracle_built, monkeypatch, k
     sort over the residual in input-order chunks -- bit-exact against the
     oracle, including keys heavy in one table only, adjacent heavy keys in one
     sub-bucket, a group of several chunks, the key in column 1 and a WHERE.
-    giant: the groups over the one-workgroup limit (lowered here from 131072
+    giant: the groups over the one-workgroup limit (lowered here from 65536
     to 2048 rows) go through the job split (msd_giant_*: per-job counts,
     scatter and join launches; jobs of 2048 rows)."""
     from smj import ops
