@@ -1213,7 +1213,7 @@ int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64
             sc[std::lower_bound(spl.begin(), spl.end(), k) - spl.begin()]++;
         }
         const double w = (double)in[x].n / (double)m;
-        const int64_t tile = msd_tile(in[x].cols);
+        const int64_t tile = p1_tile(in[x].cols);
         const char *cs = getenv("SMJ_PART1_CAP");  // tests: scaled-down regions force the fallback
         const double scale = cs ? atof(cs) : 1.0;
         int64_t *oc = ms->p1h + x * kP1Words;

@@ -162,7 +162,16 @@ __host__ __device__ constexpr int msd_tile(int cols) { return kMsdThreads * msd_
 #define SMJ_PA_BIG 0
 #endif
 __host__ __device__ constexpr int pa_threads(int cols) { return (SMJ_PA_BIG && cols == 2) ? 1024 : kMsdThreads; }
-__host__ __device__ constexpr int msd_tile_a(int cols) { return pa_threads(cols) * msd_items(cols); }
+// SMJ_PA_ITEMS: rows per thread of a 2-column pass-A tile (8: 4096 rows, two
+// workgroups per CU; 6: 3072 rows, three)
+#ifndef SMJ_PA_ITEMS
+#define SMJ_PA_ITEMS 8
+#endif
+__host__ __device__ constexpr int pa_items(int cols) { return cols == 2 ? SMJ_PA_ITEMS : msd_items(cols); }
+__host__ __device__ constexpr int msd_tile_a(int cols) { return pa_threads(cols) * pa_items(cols); }
+__host__ __device__ constexpr int pa_waves_per_eu(int cols) {
+    return pa_threads(cols) != kMsdThreads ? 4 : pa_items(cols) >= 8 ? 4 : 6;
+}
 // pass-B tiles (rows); part_b runs 1024 threads x 4 rows for 2-column tables
 // (64 VGPRs, 2 x 16 waves per CU: part_b is latency-bound)
 __host__ __device__ constexpr int msd_tile_b(int cols) { return msd_tile(cols); }
@@ -363,7 +372,15 @@ int msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int sc1, i
                                int64_t *dS, int64_t *dRs, int64_t *dSs, int64_t *dJ, int64_t *h_rows, hipStream_t s,
                                hipStream_t copy, hipEvent_t landed);
 
-// the partitioned mode's one-pass range partition (msd_part1_kernel)
+// the partitioned mode's one-pass range partition (msd_part1_kernel): its
+// tile (SMJ_P1_ITEMS rows per thread for 2-column tables; fewer rows = less
+// LDS = more workgroups per CU to hide the look-back) and occupancy
+#ifndef SMJ_P1_ITEMS
+#define SMJ_P1_ITEMS 8
+#endif
+__host__ __device__ constexpr int p1_items(int cols) { return cols == 2 ? SMJ_P1_ITEMS : msd_items(cols); }
+__host__ __device__ constexpr int p1_tile(int cols) { return kMsdThreads * p1_items(cols); }
+__host__ __device__ constexpr int p1_waves_per_eu(int cols) { return p1_items(cols) >= 8 ? 4 : p1_items(cols) >= 6 ? 6 : 8; }
 struct MsdPart1Params {
     const int64_t *src;
     int64_t n;

@@ -340,14 +340,14 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 #define SMJ_PB_NTLOAD 0  // A/B switch: the pipelined part_b's gathers through nontemporal loads
 #endif
 template <int COLS>
-__global__ __launch_bounds__(pa_threads(COLS), pa_threads(COLS) == kMsdThreads ? 2 : 1) void msd_part_a_kernel(
+__global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_part_a_kernel(
     const MsdPartA2 q) {
     // one launch may cover both tables (the same column count): blocks past
     // q.tiles0 take table 1's tiles
     const bool second = blockIdx.x >= q.tiles0;
     const MsdPartAParams &p = second ? q.t[1] : q.t[0];
     const unsigned bx = blockIdx.x - (second ? q.tiles0 : 0u);
-    constexpr int ITEMS = msd_items(COLS), T = msd_tile_a(COLS), RADIX = kBucketsA;
+    constexpr int ITEMS = pa_items(COLS), T = msd_tile_a(COLS), RADIX = kBucketsA;
     constexpr int NT = pa_threads(COLS), NW = NT / 64;
     constexpr int ROWB = T * COLS * 8, CNTB = NW * RADIX * 4;
     constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
@@ -438,8 +438,8 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_threads(COLS) == kMsdThreads ?
 constexpr uint64_t kP1Agg = 1ull << 62, kP1Inc = 2ull << 62, kP1Val = (1ull << 62) - 1;
 
 template <int COLS>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart1Params p) {
-    constexpr int ITEMS = msd_items(COLS), T = msd_tile(COLS), RADIX = 64;
+__global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_kernel(const MsdPart1Params p) {
+    constexpr int ITEMS = p1_items(COLS), T = p1_tile(COLS), RADIX = 64;
     constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
     constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
@@ -561,6 +561,8 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_part1_kernel(const MsdPart
     for (int it = 0; it < ITEMS; it++) {
         const uint32_t slot = (uint32_t)(tid + it * kMsdThreads);
         if (slot < total) {
+            // (searching the part starts instead of keeping s_pd: C4 partition
+            // +0.5-0.9 ms, profiles/r03/r03ze_ab_c4.txt)
             const uint32_t b = s_pd[slot];
             if (s_ok[b]) {
                 int64_t r[COLS];
