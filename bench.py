@@ -17,9 +17,13 @@ of the previous stage (smj/dist.py).
 
 value = (|R| + |S| over all ranks) / max-over-ranks seconds per step.
 
---workload c4 / c5 (single GPU, not the driver's default line) times the
-other BASELINE tables on ONE MI355X through the library's partitioned mode:
-C4's 1e9 x 1e9 uniform tables, C5's 1e8 x 1e9 Zipf(0.9) tables.
+--workload c4 / c5 times the other BASELINE tables: C4's 1e9 x 1e9 uniform
+tables (configs[3]), C5's 1e8 x 1e9 Zipf(0.9) tables (configs[4]).  On one GPU
+they run through the library's partitioned mode; under torchrun (or
+--loopback) they are STRONG-scaled: the job's tables are fixed and rank r
+generates its contiguous slice, global rows [r n / W, (r + 1) n / W) (row0 =
+r n / W: the generators are functions of the global row, so the tables do not
+depend on W), then the range partition + RCCL exchange of smj/dist.py.
 """
 import argparse
 import json
@@ -85,6 +89,19 @@ def parse():
     return p.parse_args()
 
 
+def workload_name(w, world, distributed):
+    """config.workload: the BASELINE.json config the line measures."""
+    if w == "c3":
+        return ("C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, JOIN_KEY 0"
+                + ("; range partition + RCCL exchange, weak scaling (|R|=|S|=%d x 1e8)" % world if distributed else ""))
+    base = {"c4": "C4 (BASELINE configs[3]) 1B x 1B rows, uniform int64 keys in [1,3e9]",
+            "c5": "C5 (BASELINE configs[4]) 100M x 1B rows, Zipf(0.9) keys over 1e8 values"}[w]
+    if distributed:
+        return base + ", WHERE col0 > 5000; range-partitioned across %d GPU%s via RCCL%s (strong scaling)" % (
+            world, "s" if world > 1 else "", " loopback" if world == 1 else "")
+    return base + ", WHERE col0 > 5000; ONE GPU (the library's partitioned mode)"
+
+
 def step_single(R, S, bufs):
     """One pass of the hot path: the fused MSD pipeline (select + stable sort of
     R and S, 1:1 zip join; sorted tables and joined rows all written)."""
@@ -113,20 +130,30 @@ def main():
     distributed = world > 1 or a.loopback
 
     n = a.rows
-    if a.workload != "c3" and world > 1:
-        raise SystemExit("--workload c4 / c5 are single-GPU measurements")
-    if a.workload in ("c4", "c5"):
-        n = 1_000_000_000  # (C5: |S|)
-    total = n * world
-    key_range = 3 * total if a.workload != "c5" else 100_000_000  # C5: the Zipf domain
-    if a.workload == "c5":
-        nr, ns = 100_000_000, 1_000_000_000
-        R = ops.gen_zipf(nr, seed=3, domain=100_000_000, theta=0.9, device=dev)
-        S = ops.gen_zipf(ns, seed=4, domain=100_000_000, theta=0.9, device=dev)
+    strong = a.workload != "c3"  # C4 / C5: the job's tables are fixed (BASELINE configs[3], [4])
+    if a.workload == "c3":
+        NR = NS = n * world       # weak: n rows per table per GPU
+    elif a.workload == "c4":
+        NR = NS = 1_000_000_000
     else:
-        nr = ns = n
-        R = ops.gen_uniform(n, row0=rank * n, seed=1, key_range=key_range, device=dev)
-        S = ops.gen_uniform(n, row0=rank * n, seed=2, key_range=key_range, device=dev)
+        NR, NS = 100_000_000, 1_000_000_000
+    key_range = 3 * NR if a.workload != "c5" else 100_000_000  # C5: the Zipf domain
+
+    def shard(N):  # this rank's contiguous slice of a table of N global rows
+        if not strong:
+            return rank * n, n
+        r0 = N * rank // world
+        return r0, N * (rank + 1) // world - r0
+
+    (r0R, nr), (r0S, ns) = shard(NR), shard(NS)
+    if a.workload == "c5":
+        R = ops.gen_zipf(nr, row0=r0R, seed=3, domain=100_000_000, theta=0.9, device=dev)
+        S = ops.gen_zipf(ns, row0=r0S, seed=4, domain=100_000_000, theta=0.9, device=dev)
+    else:
+        R = ops.gen_uniform(nr, row0=r0R, seed=1, key_range=key_range, device=dev)
+        S = ops.gen_uniform(ns, row0=r0S, seed=2, key_range=key_range, device=dev)
+    if strong:
+        n = NS  # rows per table of one single-GPU call (the PMC summary's key)
     bufs = None
     if not distributed:
         bufs = {"R": torch.empty_like(R), "S": torch.empty_like(S),
@@ -173,6 +200,11 @@ def main():
             f"(groups, radix-tier, wide-tier, in-LDS LSD): {ops.msd_groups()}")
 
     joined = int(res) if not distributed else int(res.shape[0])
+    rank_rows = [nr + ns]  # every rank's generated input rows (R + S), rank order
+    if world > 1:
+        got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([nr + ns], dtype=torch.int64, device=dev))
+        rank_rows = [int(g.item()) for g in got]
     t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=dev)
     if world > 1:
         tt = t.clone()
@@ -181,17 +213,21 @@ def main():
         joined = int(tt[1].item())
         dt = float(t[0].item())
     ms_step = dt / a.steps * 1e3
-    rows_step = 2 * total if a.workload != "c5" else nr + ns
+    rows_step = NR + NS  # the whole job's input rows per step
     value = rows_step / (dt / a.steps)
 
     # roofline of the dominant kernel: algorithmic bytes / its event time
     dom = max(prof.items(), key=lambda kv: kv[1]["ms"]) if prof else (None, None)
     roof = None
     pmc = None
-    if os.path.exists(a.pmc):
+    # the PMC summary is per launch of ONE configuration (profiles/pmc_traffic.json:
+    # the single-GPU C3 call): its bytes are attached only to a line timing the
+    # same launches -- never to the dist / loopback stages (half-size launches)
+    # or another workload
+    if os.path.exists(a.pmc) and not distributed:
         with open(a.pmc) as f:
             pmc = json.load(f)
-        if pmc.get("rows_per_table") != n:
+        if pmc.get("rows_per_table") != n or pmc.get("workload", "c3") != a.workload:
             pmc = None
     if dom[0]:
         name, d = dom
@@ -221,6 +257,11 @@ def main():
         # each pass writes what it reads and HBM's data bus carries both
         # directions: a pass can fetch at most half the peak
         sort_passes["read_ceiling_frac_of_peak"] = 0.5
+        if any(v["frac_of_peak"] > 0.5 for v in sort_passes.values() if isinstance(v, dict)):
+            log("PMC summary does not match the timed launches: traffic / sort_passes dropped")
+            sort_passes = None
+            if roof:
+                roof["traffic"] = None
     # whole-pipeline roofline: 48 B per input row + 24 B per joined row
     b_alg = 48.0 * rows_step + 24.0 * joined
     pipe_gbs = b_alg / (dt / a.steps) / 1e9
@@ -264,18 +305,16 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "rows/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None, "dtype": "int64",
             "data": "synthetic: splitmix64 keys iid uniform in [1,3n], payload = global row index (generated on device)",
-            "config": {"workload": {"c3": "C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, "
-                                          "JOIN_KEY 0; N>1: range partition + RCCL all-to-all, weak scaling",
-                                    "c4": "C4's tables (|R|=|S|=1e9, uniform keys in [1,3e9]) on ONE GPU "
-                                          "(partitioned mode), WHERE col0 > 5000",
-                                    "c5": "C5's tables (|R|=1e8, |S|=1e9, Zipf 0.9 over 1e8 keys) on ONE GPU "
-                                          "(partitioned mode), WHERE col0 > 5000"}[a.workload],
-                       "rows_per_table_per_gpu": n if a.workload != "c5" else [nr, ns], "rows_per_table_total": total if a.workload != "c5" else [nr, ns], "key_range": key_range,
+            "config": {"workload": workload_name(a.workload, world, distributed),
+                       "rows_per_table_per_gpu": [nr, ns], "rows_per_table_total": [NR, NS],
+                       "rank_input_rows": rank_rows, "key_range": key_range,
                        "joined_rows": joined, "parallelism": f"range-partition x{world}" + (" (RCCL loopback)" if a.loopback else ""),
                        "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
+                       "rank_rows_after_exchange": lb.get("loads"),
                        "exchange_stages": lb.get("stages", 0)},
             "roofline": roof,
             "pipeline_roofline": {"alg_bytes_per_step": b_alg, "achieved": round(pipe_gbs, 1),

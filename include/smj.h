@@ -23,7 +23,9 @@
  *     common.h:17) and col_num in [1, 1024].  Tables over 1.6e8 rows are
  *     range-partitioned on the key inside the library (in one pass into
  *     part regions of ~1.3x the table of library scratch when the device
- *     has room, else counted and scattered in place), tables over 8 columns
+ *     has room, else counted and scattered in place; the regions stay
+ *     allocated for the next call until smj_finalize, and are released
+ *     when they cannot all be had), tables over 8 columns
  *     are sorted as (key, row id) pairs and gathered; the
  *     LSD and partition entry points take 1..8 columns (else
  *     SMJ_ERR_UNSUPPORTED).
@@ -137,8 +139,14 @@ int smj_join(const dpu_block_t *r, const int64_t *R, const dpu_block_t *s, const
              int key2, int64_t **out, int64_t *out_rows);
 
 /* The whole app.c pipeline (select -> sort -> merge -> join, :172-692) in one
- * call with one H2D copy per table and one D2H copy of the result.
- * *out is malloc'd (caller frees).  timing may be NULL. */
+ * call.  On one GPU the tables cross PCIe in chunks on a copy stream while the
+ * first partition pass runs on the chunks already landed (a table that fits
+ * one chunk takes one copy), and the result comes back through pinned slots
+ * by several host threads.  With a device set of n > 1 GPUs (smj_init(n) /
+ * smj_init_devices) the tables are range-partitioned on the key over the
+ * GPUs, exchanged over xGMI, and each GPU sorts and joins its key range; the
+ * result is the GPUs' outputs in key order.  *out is malloc'd (caller frees).
+ * timing may be NULL. */
 int smj_sort_merge_join(const dpu_block_t *r, const int64_t *R, const dpu_block_t *s, const int64_t *S,
                         int select_col1, int64_t select_val1, int select_col2, int64_t select_val2,
                         int key1, int key2, int64_t **out, int64_t *out_rows, smj_timing_t *timing);
@@ -321,6 +329,10 @@ void smj_debug_msd_tiers(int64_t *out4);
 /* Run every pipeline call in the partitioned mode with `parts` key-range
  * parts (tests); 0 = automatic (tables over 1.6e8 rows). */
 void smj_debug_force_parts(int parts);
+/* Polls the pipeline's cross-workgroup look-back makes before it gives up
+ * and the call returns SMJ_ERR_TIMEOUT (tests: 0 forces the timeout path);
+ * a negative value restores the default (2^26). */
+void smj_debug_spin_limit(int64_t polls);
 /* Rows (R + S, after the WHERE clause) each device of the set received in
  * the last sharded call (load balance); returns the device count, writes at
  * most `max` entries. */

@@ -8,6 +8,7 @@
 #define _POSIX_C_SOURCE 200809L
 #include "cpu_ref.h"
 
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -295,6 +296,35 @@ void smj_ref_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint
         uint64_t h = smj_ref_splitmix64(g + salt);
         uint64_t k = (uint64_t)(((unsigned __int128)h * key_range) >> 64);
         out[2 * i] = (T)(1 + k);
+        out[2 * i + 1] = (T)g;
+    }
+}
+
+/* Zipf(theta) keys over [1, domain], the restatement of the
+ * device generator gen_zipf_kernel (pim-sort-merge-join_amd/csrc/smj_kernels.hip):
+ * global row g draws u = splitmix64(g + seed * 0xD1B54A32D192ED03) / 2^64
+ * (53 bits), the rank by Gray et al.'s inverse CDF approximation (ranks 1
+ * and 2 exact), scattered over the domain by rank * 2654435761 + 12345 mod
+ * domain; payload = g.  A function of g only: the table is the same however
+ * it is sharded. */
+void smj_ref_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t n, double theta, double zetan)
+{
+    const uint64_t salt = seed * 0xD1B54A32D192ED03ULL;
+    const double alpha = 1.0 / (1.0 - theta);
+    const double zeta2 = 1.0 + pow(0.5, theta);
+    const double eta = (1.0 - pow(2.0 / (double)n, 1.0 - theta)) / (1.0 - zeta2 / zetan);
+    for (int64_t i = 0; i < rows; i++) {
+        const uint64_t g = (uint64_t)(row0 + i);
+        const double u = (double)(smj_ref_splitmix64(g + salt) >> 11) * 0x1.0p-53;
+        const double uz = u * zetan;
+        int64_t rank;
+        if (uz < 1.0) rank = 1;
+        else if (uz < zeta2) rank = 2;
+        else rank = 1 + (int64_t)((double)n * pow(eta * u - eta + 1.0, alpha));
+        rank = rank < 1 ? 1 : (rank > n ? n : rank);
+        const uint64_t key = (uint64_t)(((unsigned __int128)(uint64_t)(rank - 1) * 2654435761ULL + 12345u) %
+                                        (unsigned __int128)(uint64_t)n);
+        out[2 * i] = (T)(key + 1);
         out[2 * i + 1] = (T)g;
     }
 }

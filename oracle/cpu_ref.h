@@ -79,6 +79,9 @@ uint64_t smj_ref_splitmix64(uint64_t x);
  * therefore iid uniform in [1, key_range]; the table is identical however it
  * is sharded. */
 void smj_ref_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range);
+/* Zipf(theta) keys over [1, n] of global rows [row0, row0 + rows) (the
+ * device generator's restatement; zetan = sum_{i<=n} i^-theta). */
+void smj_ref_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t n, double theta, double zetan);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,8 @@ def _bind(l, ktype):
                                ctypes.POINTER(_P)]
     l.smj_ref_gen_uniform.restype = None
     l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
+    l.smj_ref_gen_zipf.restype = None
+    l.smj_ref_gen_zipf.argtypes = [_P, _L, _L, ctypes.c_uint64, _L, ctypes.c_double, ctypes.c_double]
     l.smj_ref_csv_size.restype = ctypes.c_int
     l.smj_ref_csv_size.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     l.smj_ref_load_csv.restype = ctypes.c_int
@@ -139,6 +141,26 @@ def gen_uniform(rows, row0=0, seed=1, key_range=None):
         key_range = 3 * rows
     out = np.empty((rows, 2), dtype=np.int64)
     lib().smj_ref_gen_uniform(out.ctypes.data_as(_P), row0, rows, seed, key_range)
+    return out
+
+
+def zipf_zeta(n, theta):
+    """sum_{i<=n} i^-theta: exact for i <= 1e6, Euler-Maclaurin for the tail
+    (as smj_zipf_zeta)."""
+    H = min(n, 1_000_000)
+    z = float(np.sum(np.arange(H, 0, -1, dtype=np.float64) ** -theta))
+    if n > H:
+        a, b, s = float(H), float(n), 1.0 - theta
+        z += (b ** s - a ** s) / s + 0.5 * (b ** -theta - a ** -theta) - theta / 12.0 * (b ** (-theta - 1) - a ** (-theta - 1))
+    return z
+
+
+def gen_zipf(rows, row0=0, seed=3, domain=100_000_000, theta=0.9, zeta=None):
+    """Zipf(theta) keys over [1, domain], payload = global row (the device
+    generator's restatement, smj_ref_gen_zipf)."""
+    out = np.empty((rows, 2), dtype=np.int64)
+    z = zipf_zeta(domain, theta) if zeta is None else zeta
+    lib().smj_ref_gen_zipf(out.ctypes.data_as(_P), row0, rows, seed, domain, theta, z)
     return out
 
 

@@ -522,6 +522,9 @@ PbLast g_pb_last[2];
 int g_pb_ntab = 0;
 MsdFinalParams g_fin_last{};  // last pipeline call's final launch (smj_debug_final_time)
 
+// polls of msd_group_kernel's look-back before it gives up (smj_debug_spin_limit)
+uint32_t g_spin_limit = kMsdSpinLimit;
+
 MsdBgLimits msd_bg_limits() {  // read per call: a test may change them between calls
     MsdBgLimits r{kBgMaxRows, kBgSeg};
     if (const char *e = getenv("SMJ_BG_MAX_ROWS")) r.max_rows = (uint32_t)std::max(1, atoi(e));
@@ -1044,6 +1047,7 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         gp.plan = ms->plan;
         gp.single_list = ms->single_list;
         gp.big_list = ms->big_list;
+        gp.spin_limit = g_spin_limit;
         ProfScope ps("msd_group", 0, s);
         HIP_TRY(launch_msd_group(gp, s));
     }
@@ -1096,10 +1100,13 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     }
     HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (ms->h_plan->err) {
-        fprintf(stderr, "smj: pipeline %s\n", (ms->h_plan->err & 1u) ? "look-back wait timed out"
-                                                                  : "run metadata inconsistent (SMJ_BOUNDS check)");
-        return (ms->h_plan->err & 1u) ? SMJ_ERR_TIMEOUT : SMJ_ERR_HIP;
+    if (ms->h_plan->err) {  // every kernel after msd_group returned at entry (msd_plan_failed)
+        const uint32_t e = ms->h_plan->err;
+        fprintf(stderr, "smj: pipeline %s (err 0x%x)\n",
+                (e & 1u) ? "look-back wait timed out" : (e & 2u) ? "run metadata inconsistent (SMJ_BOUNDS check)"
+                                                             : "group plan inconsistent",
+                e);
+        return (e & 1u) ? SMJ_ERR_TIMEOUT : SMJ_ERR_HIP;
     }
     if (t_slot < 0) {
         g_msd_stats[0] = ms->h_plan->nsingle;
@@ -1190,6 +1197,21 @@ bool msd_part1_on(const MsdIn *in, int ntab) {
     return on;
 }
 
+// The one-pass partition's regions (~1.3x each table) stay allocated between
+// calls (a C4 step would otherwise pay hipFree + hipMalloc of ~20 GB); they are
+// released when they cannot all be had -- before the counting partition runs
+// -- and by smj_finalize.
+void msd_part1_release(MsdScratch *ms) {
+    for (int x = 0; x < 2; x++) {
+        if (ms->pst[x]) hipFree(ms->pst[x]);
+        ms->pst[x] = nullptr;
+        ms->c_pst[x] = 0;
+    }
+    if (ms->p1st) hipFree(ms->p1st);
+    ms->p1st = nullptr;
+    ms->c_p1st = 0;
+}
+
 // Region capacities from the key sample (ms->h_samp: table x's sampled keys at
 // [x * kSampleMax, + min(n, kSampleMax)), INT64_MAX for a row the select
 // drops): part b's estimated rows plus 8 binomial standard deviations plus a
@@ -1230,12 +1252,16 @@ int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64
         // memory: if the device cannot hold them, the counting partition runs
         if (grow(&ms->pst[x], &ms->c_pst[x], (size_t)roff[x][nb] * in[x].cols * sizeof(T)) != SMJ_OK) {
             (void)hipGetLastError();
-            return SMJ_OK;  // *staged = false
+            if (getenv("SMJ_DEBUG_PART1")) fprintf(stderr, "smj: one-pass partition regions not allocated (%zu B)\n",
+                                                    (size_t)roff[x][nb] * in[x].cols * sizeof(T));
+            msd_part1_release(ms);  // the counting partition runs with all of it free
+            return SMJ_OK;          // *staged = false
         }
         nt[x] = (in[x].n + tile - 1) / tile;
     }
     if (grow(&ms->p1st, &ms->c_p1st, (size_t)std::max(nt[0], nt[1]) * nb * 8) != SMJ_OK) {
         (void)hipGetLastError();
+        msd_part1_release(ms);
         return SMJ_OK;
     }
     for (int x = 0; x < ntab; x++) {
@@ -1335,6 +1361,9 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     std::vector<int64_t> cnt[2], off[2], roff[2];
     bool staged = false;
     if (msd_part1_on(in, ntab)) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
+    if (getenv("SMJ_DEBUG_PART1"))
+        fprintf(stderr, "smj: partitioned mode: %lld x %lld rows, %d parts, %s\n", (long long)in[0].n,
+                (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, staged ? "one-pass regions" : "counting partition");
     for (int x = 0; x < ntab; x++) {
         if (!staged) {
             cnt[x].assign(nspl + 1, 0);
@@ -1631,6 +1660,10 @@ int smj::msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int s
 // Diagnostic only (not part of smj.h): run every pipeline call in the
 // partitioned mode with `parts` parts (0 = automatic: tables over 1.6e8 rows).
 extern "C" void smj_debug_force_parts(int parts) { g_force_parts = parts > 0 ? parts : 0; }
+
+extern "C" void smj_debug_spin_limit(int64_t polls) {
+    g_spin_limit = polls < 0 ? kMsdSpinLimit : (uint32_t)std::min<int64_t>(polls, UINT32_MAX);
+}
 
 // ---------------------------------------------------------------------------
 // T = UINT64 / DOUBLE (common.h:3-9): the int64 pipeline

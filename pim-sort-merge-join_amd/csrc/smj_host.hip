@@ -193,14 +193,34 @@ int d2h_result(HostDev &hd, void *dst, const void *src, size_t bytes) {
         return SMJ_OK;
     }
     if (hd.ds.empty()) {
-        hd.ds.assign(kD2HThreads, nullptr);
-        hd.de.assign(2 * kD2HThreads, nullptr);
-        hd.dslot.assign(2 * kD2HThreads, nullptr);
-        for (int t = 0; t < kD2HThreads; t++) HIP_TRY(hipStreamCreateWithFlags(&hd.ds[t], hipStreamNonBlocking));
-        for (int i = 0; i < 2 * kD2HThreads; i++) {
-            HIP_TRY(hipEventCreateWithFlags(&hd.de[i], hipEventDisableTiming));
-            HIP_TRY(hipHostMalloc((void **)&hd.dslot[i], kD2HSlot, hipHostMallocDefault));
+        // created into locals and kept only once all exist: a failure part way
+        // frees the partial set, so a later call never copies through a null
+        // stream or slot
+        std::vector<hipStream_t> ds(kD2HThreads, nullptr);
+        std::vector<hipEvent_t> de(2 * kD2HThreads, nullptr);
+        std::vector<char *> dslot(2 * kD2HThreads, nullptr);
+        auto release = [&]() {
+            for (auto x : ds)
+                if (x) hipStreamDestroy(x);
+            for (auto x : de)
+                if (x) hipEventDestroy(x);
+            for (auto x : dslot)
+                if (x) hipHostFree(x);
+        };
+        hipError_t e = hipSuccess;
+        for (int t = 0; t < kD2HThreads && e == hipSuccess; t++) e = hipStreamCreateWithFlags(&ds[t], hipStreamNonBlocking);
+        for (int i = 0; i < 2 * kD2HThreads && e == hipSuccess; i++) {
+            e = hipEventCreateWithFlags(&de[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipHostMalloc((void **)&dslot[i], kD2HSlot, hipHostMallocDefault);
         }
+        if (e != hipSuccess) {
+            fprintf(stderr, "smj: D2H staging setup failed: %s\n", hipGetErrorString(e));
+            release();
+            return e == hipErrorOutOfMemory ? SMJ_ERR_NOMEM : SMJ_ERR_HIP;
+        }
+        hd.ds = std::move(ds);
+        hd.de = std::move(de);
+        hd.dslot = std::move(dslot);
     }
     std::vector<int> rc(kD2HThreads, SMJ_OK);
     auto part = [&](int t) {

@@ -286,8 +286,18 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t njobs;      // their jobs
     uint32_t err;        // bit 0: a cross-workgroup wait gave up (msd_group_kernel) -> SMJ_ERR_TIMEOUT;
                          // bit 1: inconsistent run metadata (SMJ_BOUNDS builds) -> SMJ_ERR_HIP;
-                         // bit 2: a combined group missed the staged kernel (a bug) -> SMJ_ERR_HIP
+                         // bit 2: a combined group missed the staged kernel (a bug) -> SMJ_ERR_HIP;
+                         // bit 3: a dense group index past kSlots (a bug) -> SMJ_ERR_HIP.
+                         // Every kernel after msd_group_kernel returns at entry once err != 0
+                         // (msd_plan_failed), so a failed plan never drives a gather or a store.
+    uint32_t gticket;    // msd_group_kernel: bucket tickets, taken in the order workgroups start
 };
+// A kernel launched after msd_group_kernel reads the plan's error word first:
+// a set bit means the dense group array may hold slots this call never wrote.
+__device__ __forceinline__ bool msd_plan_failed(const MsdPlan *pl) {
+    return __builtin_expect(*(const volatile uint32_t *)&pl->err != 0u, 0);
+}
+constexpr uint32_t kMsdSpinLimit = 1u << 26;  // polls before a cross-workgroup wait gives up
 struct MsdBasesParams {
     const uint32_t *totL[2];   // rows / runs of each bucket over all pass-A tiles (msd_seg_scan_kernel)
     const uint32_t *totC[2];
@@ -333,6 +343,7 @@ struct MsdGroupParams {
     MsdPlan *plan;
     uint32_t *single_list, *big_list;  // dense group indices
     int combined;           // as MsdBasesParams::combined
+    uint32_t spin_limit;    // polls of the look-back before it gives up (kMsdSpinLimit; 0 in the forced-timeout test)
 };
 struct MsdTab {          // a table as the final kernels see it
     const int64_t *tempB;

@@ -1560,8 +1560,18 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     __shared__ uint32_t s_nl[2], s_lb[2];  // this bucket's single / oversized groups: count, then list base
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];   // groups: sub-buckets [b0, b1)
-    __shared__ int s_ng;
-    const int a = blockIdx.x, t = threadIdx.x;
+    __shared__ int s_ng, s_a;
+    // The bucket is a ticket, not blockIdx.x: dispatch order (and which XCD
+    // gets a workgroup when) is undefined, so a workgroup waiting on a lower
+    // blockIdx could wait on one that is not resident yet -- and with other
+    // processes' kernels filling that XCD (eight ranks sharing one GPU: the
+    // r03za fault) on one that never becomes resident before the spin runs
+    // out.  A ticket is taken by a running workgroup, so every bucket waited
+    // on belongs to a workgroup that is already executing and waits only on
+    // lower tickets itself: the look-back always completes.
+    if (threadIdx.x == 0) s_a = (int)atomicAdd(&p.plan->gticket, 1u);
+    __syncthreads();
+    const int a = s_a, t = threadIdx.x;
     uint32_t nzmask = 0;  // thread t's sub-buckets [t*SB, t*SB + SB) that hold rows
     for (int x = 0; x < 2; x++) {
         uint32_t tot[SB];
@@ -1696,16 +1706,16 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         atomicExch(&p.ngrp[a], (uint32_t)ng | kGrpReady);
     }
     // dense base = the group counts of buckets < a, as they are published
-    // (workgroups wait only on earlier, already dispatched ones).  Relaxed
+    // (by workgroups already executing: the bucket tickets above).  Relaxed
     // atomics: nothing else this kernel writes is read back in it.
     {
         uint32_t v = 0;
         if (t < a) {
             // bounded, so the grid always drains: on exhaustion the plan's error
-            // word is set and msd_run returns SMJ_ERR_TIMEOUT instead of a join
-            // built on a wrong dense base
+            // word is set, every later kernel of the call returns at entry
+            // (msd_plan_failed) and msd_run returns SMJ_ERR_TIMEOUT
             uint32_t spin = 0;
-            for (; spin < (1u << 26); spin++) {
+            for (; spin < p.spin_limit; spin++) {
                 v = __hip_atomic_load(&p.ngrp[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v & kGrpReady) break;
                 __builtin_amdgcn_s_sleep(1);
@@ -1773,6 +1783,10 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.span = sp > 0xffffffffu ? 0xffffffffu : (uint32_t)sp;
         // dense, key-ordered index; the streamed / oversized lists
         const uint32_t gi = base + (uint32_t)j;
+        if (gi >= (uint32_t)kSlots) {  // the group array's capacity (a wrong base: never stored past it)
+            atomicOr(&p.plan->err, 8u);
+            continue;
+        }
         p.groups[gi] = gr;
         uint32_t cnt = 0;
         if (gr.flags == kGroupSingle) {
@@ -2503,6 +2517,7 @@ __device__ unsigned long long g_fin_phase[16];
 template <int C1, int C2>
 __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p) {
     __shared__ FinSmem sm;
+    if (msd_plan_failed(p.plan)) return;
     unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     // contiguous mode: workgroup b walks a range of dense groups (pipelined one
     // group deep); list mode: the groups msd_final_stage_kernel handed over
@@ -3089,6 +3104,7 @@ constexpr int kXcdSlots = 8;
 template <bool COMB>
 __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
+    if (msd_plan_failed(p.plan)) return;
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
     const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
@@ -3123,8 +3139,12 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
             // (the group kernel packs over kGroupCap rows of a table only where
             // every group fits this kernel: the radix tier takes <= kGroupCap)
             if (opaque_tid() == 0) {
-                if (g.nR > (uint32_t)kGroupCap || (p.ntab > 1 && g.nS > (uint32_t)kGroupCap)) atomicOr(&p.plan->err, 4u);
-                p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+                // the radix tier stages <= kGroupCap rows per table in LDS: a
+                // group over that is only flagged (the call fails), never listed
+                if (g.nR > (uint32_t)kGroupCap || (p.ntab > 1 && g.nS > (uint32_t)kGroupCap))
+                    atomicOr(&p.plan->err, 4u);
+                else
+                    p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
             }
             have = false;
             continue;
@@ -3181,6 +3201,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
 template <int C1, int C2>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const MsdFinalParams p) {
     __shared__ FinalSmem sm;
+    if (msd_plan_failed(p.plan)) return;
     const uint32_t nw = p.plan->nwide;
     for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
         final_group<C1, C2>(p, p.wide_list[i], sm);
@@ -3661,6 +3682,7 @@ __device__ unsigned long long g_bg_cls[2][32], g_bg_ph[8];
 
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
+    if (msd_plan_failed(p.plan)) return;
     const uint32_t nbig = p.plan->nbig;
     const int tid = threadIdx.x;
     const bool join = p.join && p.ntab > 1;
@@ -3764,6 +3786,7 @@ __device__ __forceinline__ GiantJob giant_job(const MsdFinalParams &p, uint32_t 
 
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_count_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
+    if (msd_plan_failed(p.plan)) return;
     const uint32_t nj = p.plan->njobs;
     for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
         const GiantJob jb = giant_job(p, t);
@@ -3815,6 +3838,7 @@ __device__ __forceinline__ void giant_totals(const MsdFinalParams &p, const Gian
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
     constexpr int RP = kStRange / kMsdThreads;
+    if (msd_plan_failed(p.plan)) return;
     const uint32_t nj = p.plan->njobs;
     const bool join = p.join && p.ntab > 1;
     for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
@@ -3846,6 +3870,7 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_scatter_kernel(const
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_giant_join_kernel(const MsdFinalParams p) {
     __shared__ BgSmem sm;
     constexpr int RP = kStRange / kMsdThreads;
+    if (msd_plan_failed(p.plan)) return;
     const uint32_t nj = p.plan->njobs;
     const bool join = p.join && p.ntab > 1;
     for (uint32_t t = blockIdx.x; t < nj; t += gridDim.x) {
@@ -3888,6 +3913,7 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
     __shared__ uint64_t s_tmp[kGroupCap];
     __shared__ uint32_t s_addr[2][kGroupCap];
     __shared__ uint32_t s_wsum[kMsdWaves];
+    if (msd_plan_failed(p.plan)) return;
     const uint2 w = work[blockIdx.x];
     const MsdGroup g = p.groups[w.x];
     const int tid = threadIdx.x;
@@ -4032,6 +4058,7 @@ __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restr
                                                           int64_t *__restrict__ out, int after_fallback) {
     constexpr int U = 8;
     const int lane = threadIdx.x & 63;
+    if (msd_plan_failed(plan)) return;
     if (!after_fallback && plan->nsingle + plan->nbig > 0) return;
     const int64_t ng = plan->ngroups, step = (int64_t)gridDim.x * 4;
     int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -4117,6 +4144,7 @@ __device__ __forceinline__ void count_load(const uint32_t *counts, int64_t ng, i
 __global__ __launch_bounds__(256) void msd_count_part_kernel(const uint32_t *__restrict__ counts,
                                                              uint32_t *__restrict__ part, const MsdPlan *plan) {
     __shared__ uint32_t s_w[4];
+    if (msd_plan_failed(plan)) return;
     const int64_t ng = plan->ngroups, c0 = (int64_t)blockIdx.x * kCountChunk;
     if (c0 >= ng) return;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -4135,6 +4163,7 @@ __global__ __launch_bounds__(256) void msd_count_scan_kernel(const uint32_t *__r
                                                              const uint32_t *__restrict__ part,
                                                              uint32_t *__restrict__ offs, MsdPlan *plan) {
     __shared__ uint32_t s_w[4], s_base;
+    if (msd_plan_failed(plan)) return;
     const int64_t ng = plan->ngroups, c0 = (int64_t)blockIdx.x * kCountChunk;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (ng == 0) {

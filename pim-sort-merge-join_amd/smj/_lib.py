@@ -66,6 +66,7 @@ SIGNATURES = {
     "smj_debug_msd_groups": (None, [_PL]),
     "smj_debug_msd_tiers": (None, [_PL]),
     "smj_debug_force_parts": (None, [_I]),
+    "smj_debug_spin_limit": (None, [_L]),
     "smj_debug_shard_rows": (_I, [_PL, _I]),
     "smj_prof_enable": (None, [_I]),
     "smj_prof_report": (_I, [ctypes.c_char_p, ctypes.c_size_t]),

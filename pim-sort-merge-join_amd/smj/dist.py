@@ -54,6 +54,25 @@ DEFAULT_STAGES = int(os.environ.get("SMJ_DIST_STAGES", "2"))
 # instead of a device copy, and one rank runs the whole distributed path: the
 # RCCL exchange on a one-GPU box
 LOOPBACK = os.environ.get("SMJ_DIST_LOOPBACK", "0") == "1"
+# diagnostics: SMJ_DIST_TRACE=1 synchronises after every phase and prints its
+# wall time (rank 0, stderr) -- it serialises the overlap, so never in a timed run
+TRACE = os.environ.get("SMJ_DIST_TRACE", "0") == "1"
+
+
+class _Tracer:
+    def __init__(self, on, rank):
+        import time
+        self.on, self.rank, self.time = on and rank == 0, rank, time
+        self.t = self.time.perf_counter() if self.on else 0.0
+
+    def __call__(self, what):
+        if not self.on:
+            return
+        torch.cuda.synchronize()
+        t = self.time.perf_counter()
+        import sys
+        print(f"smj.dist trace: {what}: {(t - self.t) * 1e3:.2f} ms", file=sys.stderr, flush=True)
+        self.t = t
 
 
 class HipOps:
@@ -339,8 +358,10 @@ def _compute_stream(device):
 def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
     nseg = world * K
+    tr = _Tracer(TRACE and R.is_cuda, rank)
 
     spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg)  # host sync 1
+    tr("splitters")
     bounds, single = bucket_bounds(spl)
     nb = len(bounds) + 1
     # R: counted and scattered; S: counted only (its plan keeps the per-chunk
@@ -352,9 +373,13 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     planS = ops.partition_plan(S, bounds, cnt[nb:], k2, sc2, sv2)
     del planR
     wire = _wire_device(rowsR, group)
-    sends = [rowsR.to(wire), None]
-    del rowsR
     allc = gather_counts(cnt, world, group, _wire_device(R, group))  # host sync 2
+    mine = [sum(allc[rank][t * nb:(t + 1) * nb]) for t in range(2)]  # this rank's selected rows per table
+    tr("partition R + plan S + counts")
+    # partition_apply's buffer has n rows; only the selected prefix is sent
+    # (under gloo the wire copy to the host then moves only those rows)
+    sends = [rowsR[:mine[0]].to(wire), None]
+    del rowsR
     G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
     cuts = choose_cuts(G[0], G[1], single, nseg)
     # every source rank's rows per segment, from the gathered counts
@@ -378,11 +403,13 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group, loopback)]  # R's stage 0
     rowsS = ops.partition_apply(S, bounds, planS, k2, sc2, sv2)  # overlaps R's stage-0 exchange
     del planS
-    sends[1] = rowsS.to(wire)
+    sends[1] = rowsS[:mine[1]].to(wire)
     del rowsS
     pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group, loopback))
+    tr("J alloc + S scatter + stage 0 posted")
     for k in range(K):
         Rk, Sk = _wait_all(pending)
+        tr(f"stage {k} received")
         if k + 1 < K:
             pending = [post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group, loopback)]
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
@@ -394,12 +421,13 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         else:
             parts.append(ops.sort_merge_join(Rk, Sk, k1, k2, None, None)[2])
         del Rk, Sk
+        tr(f"stage {k} sorted + joined")
     del sends
     if stats is not None:  # every rank's load, from the gathered counts (no communication)
         loads = [sum(seg[t][r][d * K + k] for t in range(2) for r in range(world) for k in range(K))
                  for d in range(world)]
         mean = sum(loads) / world
-        stats.update(rows_in=rows_in, load_max_over_mean=(max(loads) / mean) if mean else 1.0,
+        stats.update(rows_in=rows_in, loads=loads, load_max_over_mean=(max(loads) / mean) if mean else 1.0,
                      cuts=cuts, buckets=nb, stages=K)
     if into:
         return J[:at]

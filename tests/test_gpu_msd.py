@@ -102,6 +102,42 @@ def test_fused_pipeline_matches_oracle(gpu, oracle_built, nr, ns, c1, c2, k1, k2
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
 
 
+@pytest.mark.parametrize("nr,ns,kind,parts", [
+    (300_000, 300_000, "uniform", 0),   # per-table staged groups
+    (40_000, 400_000, "zipf", 0),       # combined groups + oversized groups (the device big tiers)
+    (300_000, 200_000, "dups", 3),      # the partitioned mode: the error leaves msd_large too
+])
+def test_forced_timeout_is_fault_safe(gpu, oracle_built, nr, ns, kind, parts):
+    """with msd_group_kernel's look-back given no polls
+    (smj_debug_spin_limit(0)) every bucket after the first gives up, the plan's
+    error word is set, every later kernel returns at entry -- the dense group
+    array is never read -- and the call returns SMJ_ERR_TIMEOUT; the next call,
+    with the limit restored, is bit-exact."""
+    from smj import _lib, ops
+    rng = np.random.default_rng(nr + ns)
+    R = table(rng, nr, 2, kind, 0, 0)
+    S = table(rng, ns, 2, kind, 0, 10 ** 9)
+    dR, dS = dev(R), dev(S)
+    lib = _lib.load()
+    ops.force_parts(parts)
+    try:
+        lib.smj_debug_spin_limit(0)
+        with pytest.raises(_lib.SmjError) as ei:
+            ops.sort_merge_join(dR, dS, 0, 0, (0, 5000), None)
+        assert ei.value.code == -6, ei.value  # SMJ_ERR_TIMEOUT
+        torch.cuda.synchronize()  # no fault left behind on the stream
+    finally:
+        lib.smj_debug_spin_limit(-1)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dR, dS, 0, 0, (0, 5000), None)
+    finally:
+        ops.force_parts(0)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, (0, 5000), None)
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
 def test_single_key_groups_stream(gpu, oracle_built):
     """Heavy keys (over the LDS group capacity) take the no-sort streaming path."""
     from smj import ops

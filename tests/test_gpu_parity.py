@@ -161,6 +161,34 @@ def test_partition_fused_matches_numpy(gpu, n, cols, nspl, sv):
     np.testing.assert_array_equal(host(got), keep[np.argsort(bucket, kind="stable")])
 
 
+@pytest.mark.parametrize("n,cols,sv", [(300_001, 2, -900), (0, 2, None), (70_000, 3, 2000), (1, 2, None)])
+def test_partition_plan_apply_matches_numpy(gpu, n, cols, sv):
+    """smj_dev_partition_plan / _apply (smj/dist.py's two-call partition): the
+    counts land in a device tensor without a host sync, the plan survives an
+    intervening library call (a fused pipeline call reuses the scratch), and
+    apply writes the stable bucket order; in == out is refused."""
+    from smj import _lib, ops
+    rng = np.random.default_rng(n + 17)
+    t = rng.integers(-1000, 1000, size=(n, cols), dtype=np.int64)
+    t[:, 1] = np.arange(n)
+    bounds = [-600, -1, 0, 0, 17, 400]
+    dt = dev(t).reshape(n, cols)
+    cnt = torch.zeros(len(bounds) + 1, dtype=torch.int64, device="cuda")
+    sc = cols - 1
+    plan = ops.partition_plan(dt, bounds, cnt, 0, sc, sv)
+    # an intervening pipeline call on other tables
+    other = dev(rand_table(np.random.default_rng(1), 50_000, 2, "uniform"))
+    ops.sort_merge_join(other, other.clone(), 0, 0, (0, 10), None)
+    got = ops.partition_apply(dt, bounds, plan, 0, sc, sv)
+    keep = t if sv is None else t[t[:, sc] > sv]
+    bucket = np.searchsorted(np.array(bounds), keep[:, 0], side="left")
+    assert host(cnt).tolist() == np.bincount(bucket, minlength=len(bounds) + 1).tolist()
+    np.testing.assert_array_equal(host(got)[:len(keep)], keep[np.argsort(bucket, kind="stable")])
+    if n:
+        with pytest.raises(_lib.SmjError):
+            ops.partition_apply(dt, bounds, plan, 0, sc, sv, out=dt)
+
+
 def test_gen_uniform_matches_oracle(gpu, oracle_built):
     from smj import ops
     got = ops.gen_uniform(1_000_003, row0=12345, seed=2, key_range=3_000_000)
@@ -173,6 +201,25 @@ def test_gen_zipf_shape(gpu):
     assert z[:, 0].min() >= 1 and z[:, 0].max() <= 100_000_000
     top = np.bincount(np.unique(z[:, 0], return_inverse=True)[1]).max() / len(z)
     assert 0.012 < top < 0.03  # top key ~1.9 % of rows
+
+
+def test_gen_zipf_sharded_matches_oracle(gpu, oracle_built):
+    """The C5 tables under --gpus W (strong scaling): rank r generates rows
+    [r n / W, (r + 1) n / W) with row0 = r n / W.  The shards concatenate to the
+    one-GPU table bit for bit, and the device generator equals its C
+    restatement (keys differ only if pow() rounded differently: counted, at
+    most 1 in 1e5 rows)."""
+    from smj import ops
+    n, W = 2_000_003, 8
+    full = host(ops.gen_zipf(n, seed=4, domain=100_000_000, theta=0.9))
+    parts = np.concatenate([host(ops.gen_zipf(n * (r + 1) // W - n * r // W, row0=n * r // W, seed=4,
+                                              domain=100_000_000, theta=0.9)) for r in range(W)])
+    np.testing.assert_array_equal(full, parts)
+    from smj import _lib
+    ref = oracle.gen_zipf(n, 0, seed=4, domain=100_000_000, theta=0.9,
+                          zeta=_lib.load().smj_zipf_zeta(100_000_000, 0.9))
+    np.testing.assert_array_equal(full[:, 1], ref[:, 1])
+    assert int((full[:, 0] != ref[:, 0]).sum()) <= n // 100_000
 
 
 def sha(path):

@@ -1,57 +1,82 @@
 #!/bin/bash
-# tools/gpu_run.sh TAG [steps...] -- the standard GPU-box sequence.  Every
-# GPU step runs under its own time limit; the script stops at the first
-# step that faults / aborts / times out (rc other than 0 or 1).
-# Steps: smoke tests bench prof pmc (default: smoke tests bench prof)
+# tools/gpu_run.sh TAG [steps...] -- the one parameterised GPU-box runner
+# (replaces the per-run tools/rNN_cmd.sh records of rounds 2-3; the commands
+# each run used are in git history and its outputs under profiles/).
+#
+#   gpurun -- 'bash tools/gpu_run.sh r04a tests smoke c3 c4 c5 loop prof'
+#
+# Output goes to gpurun_out/TAG; if that directory already exists a fresh
+# TAG_2, TAG_3, ... is used, so a re-run never overwrites a failing log.  Every
+# GPU step runs under its own time limit; the script stops at the first step
+# that faults / aborts / times out (rc other than 0 or 1) and, for the test
+# steps, at a failing test too (rc 1).  Extra bench.py flags for the bench
+# steps: BENCH_ARGS="--steps 5"; an A/B library: SMJ_LIB=/path/libsmj_hip.so.
 set -u
-TAG=${1:-r01}; shift || true
-STEPS=${*:-smoke tests bench prof}
+TAG=${1:-run}; shift || true
+STEPS=${*:-smoke tests c3 prof}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
+i=2
+while [ -e "$OUT" ]; do OUT=$ROOT/gpurun_out/${TAG}_$i; i=$((i + 1)); done
 mkdir -p "$OUT"
 cd "$ROOT"
-run() {  # name timeout cmd...
+export TMPDIR=/tmp
+BA=${BENCH_ARGS:-}
+NOCPU="--cpu-sample 0 --cpu-mt 0"
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+run() {  # name timeout cmd...   (rc 1 tolerated: a bench step's stderr is read afterwards)
   local name=$1 lim=$2; shift 2
   echo "[$(date +%T)] $name: $*" | tee -a "$OUT/steps.log"
   timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
   local rc=$?
   echo "[$(date +%T)] $name rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" | tee -a "$OUT/steps.log"; exit $rc; fi
-  return 0
+  return $rc
+}
+test_run() {  # a pytest step: stop on any failure
+  run "$@" || { tail -30 "$OUT/$1.out"; echo "stopping after $1 (tests failed)" | tee -a "$OUT/steps.log"; exit 1; }
+}
+summ() {  # one-line summary of a bench JSON
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline') or {}; print(sys.argv[2], d['ms_per_step'], 'ms/step', d['value'], r.get('kernel'), r.get('frac'), {k: v['ms_per_step'] for k, v in d['kernels'].items() if v['ms_per_step'] > 0.1})" "$1" "$2" | tee -a "$OUT/steps.log"
 }
 for s in $STEPS; do
   case $s in
-    build) run build 600 make -s -j16 -C pim-sort-merge-join_amd ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    msd)   run msd 600 python -u -m pytest tests/test_gpu_msd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    bench) run bench 600 python bench.py ;;
-    dist)  run dist 600 python -u -m pytest tests/test_dist_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    quick) run quick 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
-    qfull) SMJ_PASSB_FULL=1 run qfull 300 python bench.py --cpu-sample 0 --cpu-mt 0 ;;
+    smoke) test_run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) test_run tests 1200 $PYT tests -m gpu ;;
+    msd)   test_run msd 600 $PYT tests/test_gpu_msd.py ;;
+    parity) test_run parity 600 $PYT tests/test_gpu_parity.py ;;
+    large) test_run large 900 $PYT tests/test_gpu_large.py ;;
+    dist)  test_run dist 600 $PYT tests/test_dist_gloo.py -m gpu ;;
+    multidev) test_run multidev 600 $PYT tests/test_gpu_multidev.py ;;
+    c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
+    quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
+    c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
+    c5)    run c5 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c5.out" c5 ;;
+    loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
+    loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
+    loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
+               python3 "$ROOT/bench.py" --steps 10 --warmup 2 $NOCPU
+           rm -f "$OUT/prof/c3_kernel_trace.csv" ;;
+    prof5) run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o c5 -- \
+               python3 "$ROOT/bench.py" --workload c5 --steps 2 --warmup 1 $NOCPU
+           rm -f "$OUT/prof5/c5_kernel_trace.csv" ;;
+    prof4) run prof4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o c4 -- \
+               python3 "$ROOT/bench.py" --workload c4 --steps 2 --warmup 1 $NOCPU
+           rm -f "$OUT/prof4/c4_kernel_trace.csv" ;;
+    proflp) run proflp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflp" -o loop -- \
+               python3 "$ROOT/bench.py" --loopback --steps 5 --warmup 2 $NOCPU
+           rm -f "$OUT/proflp/loop_kernel_trace.csv" ;;
+    pmcf)  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+               python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
+    pmcw)  run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+               python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
+    pmcsq) run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
+               --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     phases) run phases 300 python tools/msd_phases.py ;;
-    l3)    run l3 300 python tools/l3_probe.py ;;
-    large) run large 900 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 400 --timeout-method thread -p no:cacheprovider ;;
-    pbab)  run pbab 300 python tools/pb_ablate.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
-    h2d)   run h2d 300 python tools/h2d_probe.py ;;
-    part)  run part 300 python tools/part_probe.py ;;
-    ptest) run ptest 600 python -u -m pytest tests -m gpu -x -v -k "partition or distributed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    typed) run typed 600 python -u -m pytest tests -m gpu -x -q -k "typed" --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    prof)  export TMPDIR=/tmp
-           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 --cpu-mt 0
-           rm -f "$OUT/prof/run_kernel_trace.csv" ;;
-    pmcf)  export TMPDIR=/tmp
-           run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
-    pmcsq) export TMPDIR=/tmp
-           run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
-               --output-format csv -d "$OUT/pmc_sq" -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
-    pmcw)  export TMPDIR=/tmp
-           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-               python "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --cpu-mt 0 ;;
+    pbab)  run pbab 300 python tools/pb_ablate.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
-echo "[$(date +%T)] done" | tee -a "$OUT/steps.log"
+echo "[$(date +%T)] done ($OUT)" | tee -a "$OUT/steps.log"
