@@ -242,6 +242,21 @@ int smj_dev_partition_apply(const int64_t *in, int64_t n_rows, int col_num, int 
                             int64_t select_val, int key_col, const int64_t *h_splitters, int n_split,
                             const void *d_plan, int64_t *out, void *stream);
 
+/* The partition in ONE read of the table, for a driver that can size the
+ * buckets' destinations from a key sample (smj/dist.py): bucket b's selected
+ * rows go, stably, to out rows [h_region[b], h_region[b] + count_b), where
+ * h_region[0..n_split] are ascending, disjoint region starts and
+ * h_region[n_split + 1 + b] region b's capacity (rows; out must hold the last
+ * region).  d_counts (DEVICE int64, n_split + 2 entries) gets the n_split + 1
+ * exact bucket counts and d_counts[n_split + 1] = 0, or bit 0 set when a
+ * bucket outgrew its region (its rows past the capacity were NOT written: the
+ * caller re-partitions with plan / apply) / bit 1 when the decoupled
+ * look-back timed out (a bug).  Decoupled look-back over 4096-row tiles
+ * (msd_part1_kernel); nothing synchronises; <= 64 buckets, 1..8 columns. */
+int smj_dev_partition_regions(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                              int64_t select_val, int key_col, const int64_t *h_splitters, int n_split,
+                              const int64_t *h_region, int64_t *out, int64_t *d_counts, void *stream);
+
 /* Synthetic 2-column table (key, payload) for rows [row0, row0 + rows):
  * key = 1 + floor(splitmix64(g + seed * 0xD1B54A32D192ED03) * key_range / 2^64),
  * payload = g (the global row index).  Identical to the oracle's

@@ -187,6 +187,8 @@ struct DevScratch {
     int64_t *dcount = nullptr;                       // device scratch int64 x 256
     SortPlan *h_plan = nullptr;                      // pinned
     int64_t *h_small = nullptr;                      // pinned, 256 int64
+    void *rst = nullptr; size_t c_rst = 0;           // smj_dev_partition_regions: look-back words
+    int64_t *rwords = nullptr;                       // its region words (128) + flags (u32 x 4)
 };
 std::map<int, DevScratch> g_scratch;
 
@@ -1361,9 +1363,12 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     std::vector<int64_t> cnt[2], off[2], roff[2];
     bool staged = false;
     if (msd_part1_on(in, ntab)) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
-    if (getenv("SMJ_DEBUG_PART1"))
-        fprintf(stderr, "smj: partitioned mode: %lld x %lld rows, %d parts, %s\n", (long long)in[0].n,
-                (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, staged ? "one-pass regions" : "counting partition");
+    if (getenv("SMJ_DEBUG_PART1")) {
+        fprintf(stderr, "smj: partitioned mode: %lld x %lld rows, %d parts (%zu weighted samples), %s; splitters", (long long)in[0].n,
+                (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, kw.size(), staged ? "one-pass regions" : "counting partition");
+        for (int64_t k : spl) fprintf(stderr, " %lld", (long long)k);
+        fprintf(stderr, "\n");
+    }
     for (int x = 0; x < ntab; x++) {
         if (!staged) {
             cnt[x].assign(nspl + 1, 0);
@@ -1963,6 +1968,61 @@ extern "C" int smj_dev_partition_plan(const T *in, int64_t n, int cols, int use_
     return SMJ_OK;
 }
 
+extern "C" int smj_dev_partition_regions(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
+                                         int key_col, const T *h_spl, int n_split, const int64_t *h_region, T *out,
+                                         int64_t *d_counts, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    PassSpec ps;
+    SMJ_TRY(partition_spec(in, n, cols, use_select, sel_col, sel_val, key_col, h_spl, n_split, ps));
+    if (!d_counts || !h_region) return SMJ_ERR_INVALID;
+    const int nb = n_split + 1;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * (nb + 1), s));
+        return SMJ_OK;
+    }
+    if (!in || !out || in == out) return SMJ_ERR_INVALID;
+    // region starts / capacities and the splitters travel as kernel arguments
+    // (stream-ordered: no host staging buffer a second call could overwrite)
+    P1Words w{};
+    for (int b = 0; b < nb; b++) {
+        if (h_region[b] < 0 || h_region[nb + b] < 0 || (b && h_region[b] < h_region[b - 1] + h_region[nb + b - 1]))
+            return SMJ_ERR_INVALID;  // regions ascending and disjoint (the caller sized out for them)
+        w.v[b] = h_region[b];
+        w.v[64 + b] = h_region[nb + b];
+    }
+    for (int i = 0; i < n_split; i++) w.v[128 + i] = h_spl[i];
+    DevScratch *sc;
+    SMJ_TRY(scratch(&sc));
+    if (!sc->rwords) HIP_TRY(hipMalloc(&sc->rwords, sizeof(int64_t) * (192 + 2)));
+    const int64_t tile = p1_tile(cols), nt = (n + tile - 1) / tile;
+    SMJ_TRY(grow(&sc->rst, &sc->c_rst, (size_t)nt * nb * 8));
+    uint32_t *flags = (uint32_t *)(sc->rwords + 192);
+    HIP_TRY(launch_p1_words(w, sc->rwords, flags, s));
+    HIP_TRY(hipMemsetAsync(sc->rst, 0, (size_t)nt * nb * 8, s));
+    HIP_TRY(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * nb, s));
+    MsdPart1Params p{};
+    p.src = in;
+    p.n = n;
+    p.use_sel = use_select;
+    p.sel_col = sel_col;
+    p.key_col = key_col;
+    p.nspl = n_split;
+    p.sel_val = sel_val;
+    p.spl = sc->rwords + 128;
+    p.oc = sc->rwords;
+    p.dst = out;
+    p.status = (unsigned long long *)sc->rst;
+    p.tot = (long long *)d_counts;
+    p.flags = flags;
+    p.ntiles = nt;
+    {
+        ProfScope ps1("partition_1pass", 16.0 * cols * n, s);
+        HIP_TRY(launch_msd_part1(p, cols, s));
+    }
+    HIP_TRY(launch_p1_finish(flags, d_counts + nb, s));
+    return SMJ_OK;
+}
+
 extern "C" int smj_dev_partition_apply(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
                                        int key_col, const T *h_spl, int n_split, const void *d_plan, T *out,
                                        void *stream) {
@@ -2023,7 +2083,7 @@ void smj::api_free_all() {
         if (s.dev < 0) continue;
         hipSetDevice(s.dev);
         for (void *q : {s.tmp, s.status, s.apart, (void *)s.hist, (void *)s.plan, (void *)s.ctr, (void *)s.dcount,
-                        (void *)s.segsum, (void *)s.trash})
+                        (void *)s.segsum, (void *)s.trash, s.rst, (void *)s.rwords})
             hipFree(q);
         hipHostFree(s.h_plan);
         hipHostFree(s.h_small);

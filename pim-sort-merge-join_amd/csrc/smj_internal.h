@@ -406,6 +406,11 @@ struct MsdPart1Params {
     int64_t ntiles;
 };
 hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s);
+struct P1Words {  // region starts [0, 64) and capacities [64, 128), rows; splitters [128, 192)
+    int64_t v[192];
+};
+hipError_t launch_p1_words(const P1Words &w, int64_t *oc, uint32_t *flags, hipStream_t s);
+hipError_t launch_p1_finish(const uint32_t *flags, int64_t *out, hipStream_t s);
 hipError_t launch_msd_sample(const MsdSampleParams &p, hipStream_t s);
 // the sample gather alone: samp[x * kSampleMax + j] = sampled key j of table x
 // (INT64_MAX for a row the select drops or a missing row), samp[2 kSampleMax

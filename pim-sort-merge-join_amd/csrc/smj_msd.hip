@@ -4222,6 +4222,31 @@ hipError_t launch_msd_sample_gather(const MsdSampleParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// the one-pass partition's per-call words for smj_dev_partition_regions: the
+// region starts / capacities arrive as kernel arguments (stream-ordered, no
+// host staging buffer that a second call could overwrite), the ticket /
+// overflow / timeout flags are zeroed
+__global__ void p1_set_words_kernel(const P1Words w, int64_t *oc, uint32_t *flags) {
+    const int t = threadIdx.x;
+    if (t < 192) oc[t] = w.v[t];
+    if (t < 4) flags[t] = 0u;
+}
+
+// after the partition: out = overflow (bit 0) | look-back timeout (bit 1)
+__global__ void p1_finish_kernel(const uint32_t *flags, int64_t *out) {
+    if (threadIdx.x == 0) *out = (flags[1] ? 1 : 0) | (flags[2] ? 2 : 0);
+}
+
+hipError_t launch_p1_words(const P1Words &w, int64_t *oc, uint32_t *flags, hipStream_t s) {
+    hipLaunchKernelGGL(p1_set_words_kernel, dim3(1), dim3(192), 0, s, w, oc, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_p1_finish(const uint32_t *flags, int64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(p1_finish_kernel, dim3(1), dim3(64), 0, s, flags, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s) {
     if (p.ntiles <= 0) return hipSuccess;
     // one tile per workgroup: a persistent form that took its next ticket

@@ -59,6 +59,7 @@ SIGNATURES = {
     "smj_partition_plan_bytes": (ctypes.c_size_t, [_L, _I, _I]),
     "smj_dev_partition_plan": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P]),
     "smj_dev_partition_apply": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P]),
+    "smj_dev_partition_regions": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P, _P]),
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),

@@ -82,6 +82,8 @@ class HipOps:
     partition_count = staticmethod(hip_ops.partition_count)
     partition_plan = staticmethod(hip_ops.partition_plan)    # asynchronous: counts stay on the device
     partition_apply = staticmethod(hip_ops.partition_apply)
+    partition_regions = staticmethod(hip_ops.partition_regions)  # one read of the table (msd_part1_kernel)
+    region_capacities = staticmethod(hip_ops.region_capacities)
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
 
@@ -120,11 +122,13 @@ def _wire_device(t, group=None):
     return t.device
 
 
-def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None):
+def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None):
     """parts - 1 (default W - 1) sorted key splitters, identical on every rank,
     as a host list: one all_gather of every rank's sample (a fixed-size buffer,
     padded with INT64_MAX, plus its valid count), the sort and the order
-    statistics on the device, one device -> host copy of the result."""
+    statistics on the device, one device -> host copy of the result.  own (a
+    list): gets this rank's sampled keys per table (host lists, from the same
+    copy) -- partition_regions sizes its regions from them."""
     parts = parts or world
     home = tables_and_keys[0][0].device
     dev = _wire_device(tables_and_keys[0][0], group)
@@ -147,10 +151,17 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
     # the pads sort last (a real INT64_MAX key sorts among them: the same value)
     keys = torch.sort(allb[:, 1:].reshape(-1)).values
     pos = (torch.arange(1, parts, dtype=torch.int64, device=dev) * L // parts - 1).clamp(min=0)
-    got = torch.cat([keys[pos], L.view(1)]).tolist()
-    if got[-1] == 0:
+    got = torch.cat([keys[pos], L.view(1), buf[1:at]]).tolist()
+    if own is not None:
+        mine = got[parts:]
+        o = 0
+        for t, _ in tables_and_keys:
+            c = min(samples, t.shape[0])
+            own.append(mine[o: o + c])
+            o += c
+    if got[parts - 1] == 0:
         return [0] * (parts - 1)
-    return got[:-1]
+    return got[:parts - 1]
 
 
 def bucket_bounds(spl):
@@ -224,6 +235,29 @@ def slice_counts(local, prefix, cuts, nb):
     return [edges[d + 1] - edges[d] for d in range(len(edges) - 1)]
 
 
+def slice_ranges(local, prefix, cuts, nb):
+    """The rows of this rank's bucket-partitioned table per destination
+    segment, as (bucket, lo, hi) local offset ranges: cut (b, o) splits bucket
+    b at the local rows whose global occurrence (prefix[b] + local offset) is
+    below o.  Every segment's ranges ascend in bucket order; their row counts
+    are slice_counts(...)."""
+    def at(cut):
+        b, o = cut
+        return (b, 0) if b >= nb else (b, min(max(o - prefix[b], 0), local[b]))
+    edges = [(0, 0)] + [at(c) for c in cuts] + [(nb, 0)]
+    out = []
+    for d in range(len(edges) - 1):
+        (b0, c0), (b1, c1) = edges[d], edges[d + 1]
+        rs = []
+        for b in range(b0, min(b1, nb - 1) + 1):
+            lo = c0 if b == b0 else 0
+            hi = c1 if b == b1 else local[b]
+            if hi > lo:
+                rs.append((b, lo, hi))
+        out.append(rs)
+    return out
+
+
 def gather_counts(counts, world, group=None, device=None):
     """all_gather of this rank's integer vector (a list, or a device tensor
     that stays on the device until the one host copy of the gathered
@@ -269,34 +303,40 @@ def _wait_all(pending):
     return out
 
 
-def post_stage(k, K, sends, offs, seg, rank, world, home, group=None, loopback=False):
+def post_stage(k, K, sends, regs, sl, rank, world, home, group=None, loopback=False):
     """Post stage k's exchange: segment d*K + k of every table goes to rank d.
-    seg[t][r][j] = rows of src rank r's table-t buffer in segment j (known on
-    every rank from the gathered counts, so no count exchange is needed);
-    offs[t][j] = start of segment j in this rank's buffer.  sends are on the
-    wire device (_wire_device), None for a table not posted in this call;
-    received rows are returned on `home`."""
+    sl[t][r][j] = the (bucket, lo, hi) local row ranges of src rank r's table-t
+    buffer in segment j (known on every rank from the gathered counts, so no
+    count exchange is needed); regs[t][b] = where bucket b's rows start in
+    this rank's buffer.  One message per (bucket range, peer): received ranges
+    are placed in source-rank, then bucket order -- the global input order of
+    the segment's rows.  sends are on the wire device (_wire_device), None for
+    a table not posted in this call; received rows are returned on `home`."""
     p2p, recvs = [], []
     loopback = loopback and dist.get_backend(group) != "gloo"  # gloo pairs never connect a rank to itself
+    me = rank * K + k
     for t, wire in enumerate(sends):
         if wire is None:
             recvs.append(None)
             continue
-        me = rank * K + k
-        rc = [seg[t][r][me] for r in range(world)]
-        recv = torch.empty((sum(rc), wire.shape[1]), dtype=wire.dtype, device=wire.device)
+        rc = sum(hi - lo for r in range(world) for (_, lo, hi) in sl[t][r][me])
+        recv = torch.empty((rc, wire.shape[1]), dtype=wire.dtype, device=wire.device)
         at = 0
         for r in range(world):
-            if rc[r] and r == rank and not loopback:
-                recv[at: at + rc[r]].copy_(wire[offs[t][me]: offs[t][me] + rc[r]])
-            elif rc[r]:
-                p2p.append(dist.P2POp(dist.irecv, recv[at: at + rc[r]], r, group, tag=t * 4096 + k))
-            at += rc[r]
+            for b, lo, hi in sl[t][r][me]:
+                c = hi - lo
+                if r == rank and not loopback:
+                    o = regs[t][b] + lo
+                    recv[at: at + c].copy_(wire[o: o + c])
+                else:
+                    p2p.append(dist.P2POp(dist.irecv, recv[at: at + c], r, group, tag=(t * 64 + b) * 64 + k))
+                at += c
         for d in range(world):
-            j = d * K + k
-            c = seg[t][rank][j]
-            if c and (d != rank or loopback):
-                p2p.append(dist.P2POp(dist.isend, wire[offs[t][j]: offs[t][j] + c], d, group, tag=t * 4096 + k))
+            if d == rank and not loopback:
+                continue
+            for b, lo, hi in sl[t][rank][d * K + k]:
+                o = regs[t][b] + lo
+                p2p.append(dist.P2POp(dist.isend, wire[o: o + hi - lo], d, group, tag=(t * 64 + b) * 64 + k))
         recvs.append(recv)
     works = dist.batch_isend_irecv(p2p) if p2p else []
     return _Stage(works, recvs, home)
@@ -355,63 +395,91 @@ def _compute_stream(device):
     return s
 
 
+REGIONS = os.environ.get("SMJ_DIST_REGIONS", "1") != "0"  # 0: the counting partition (plan / apply), A/B
+REGION_SCALE = float(os.environ.get("SMJ_DIST_REGION_SCALE", "1"))  # tests: < 1 forces the overflow fallback
+
+
+def _partition(ops, T, bounds, cnt, own, k, sc, sv):
+    """This rank's table T partitioned by bucket.  With partition_regions (one
+    read of T): bucket b's rows at region starts sized from T's sample `own`;
+    else the counting partition (plan + apply: two reads), bucket-contiguous.
+    cnt (device, nb + 1) gets the counts and the overflow flag.  Returns
+    (buffer, region starts or None = contiguous)."""
+    nb = len(bounds) + 1
+    if REGIONS and hasattr(ops, "partition_regions"):
+        reg, _ = ops.region_capacities(own, T.shape[0], bounds)
+        if REGION_SCALE < 1.0:
+            caps = [int(c * REGION_SCALE) for c in reg[nb:]]
+            reg = [sum(caps[:b]) for b in range(nb)] + caps
+        return ops.partition_regions(T, bounds, reg, cnt, k, sc, sv), reg[:nb]
+    cnt[nb:].zero_()
+    plan = ops.partition_plan(T, bounds, cnt[:nb], k, sc, sv)
+    return ops.partition_apply(T, bounds, plan, k, sc, sv), None
+
+
+def _repartition(ops, T, bounds, k, sc, sv):
+    """The counting partition of a table whose one-read partition overflowed a
+    region (counts unchanged: the one-read pass counts every row)."""
+    nb = len(bounds) + 1
+    cnt = torch.empty(nb, dtype=torch.int64, device=T.device)
+    plan = ops.partition_plan(T, bounds, cnt, k, sc, sv)
+    return ops.partition_apply(T, bounds, plan, k, sc, sv)
+
+
 def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
     K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
     nseg = world * K
     tr = _Tracer(TRACE and R.is_cuda, rank)
 
-    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg)  # host sync 1
+    own = []
+    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own)  # host sync 1
     tr("splitters")
     bounds, single = bucket_bounds(spl)
     nb = len(bounds) + 1
-    # R: counted and scattered; S: counted only (its plan keeps the per-chunk
-    # starts), so that R's stage-0 rows can leave while S is being scattered.
-    # Nothing here waits for the device: the counts stay in `cnt`.
-    cnt = torch.empty(2 * nb, dtype=torch.int64, device=R.device)
-    planR = ops.partition_plan(R, bounds, cnt[:nb], k1, sc1, sv1)
-    rowsR = ops.partition_apply(R, bounds, planR, k1, sc1, sv1)
-    planS = ops.partition_plan(S, bounds, cnt[nb:], k2, sc2, sv2)
-    del planR
-    wire = _wire_device(rowsR, group)
+    # both tables partitioned (one read each with partition_regions); their
+    # counts and overflow flags stay on the device until the one gather
+    tabs = [(R, k1, sc1, sv1), (S, k2, sc2, sv2)]
+    cnt = torch.empty(2 * (nb + 1), dtype=torch.int64, device=R.device)
+    parts_ = [_partition(ops, T, bounds, cnt[t * (nb + 1):(t + 1) * (nb + 1)], own[t], k, sc, sv)
+              for t, (T, k, sc, sv) in enumerate(tabs)]
     allc = gather_counts(cnt, world, group, _wire_device(R, group))  # host sync 2
-    mine = [sum(allc[rank][t * nb:(t + 1) * nb]) for t in range(2)]  # this rank's selected rows per table
-    tr("partition R + plan S + counts")
-    # partition_apply's buffer has n rows; only the selected prefix is sent
-    # (under gloo the wire copy to the host then moves only those rows)
-    sends = [rowsR[:mine[0]].to(wire), None]
-    del rowsR
-    G = [[sum(allc[r][t * nb + b] for r in range(world)) for b in range(nb)] for t in range(2)]
-    cuts = choose_cuts(G[0], G[1], single, nseg)
-    # every source rank's rows per segment, from the gathered counts
-    seg = [[slice_counts(allc[r][t * nb:(t + 1) * nb],
-                         [sum(allc[q][t * nb + b] for q in range(r)) for b in range(nb)], cuts, nb)
-            for r in range(world)] for t in range(2)]
-    offs = []
+    tr("partition R + S + counts")
+    counts = [[allc[r][t * (nb + 1): t * (nb + 1) + nb] for r in range(world)] for t in range(2)]
+    wire = _wire_device(R, group)
+    sends, regs = [], []
     for t in range(2):
-        o, acc = [], 0
-        for c in seg[t][rank]:
-            o.append(acc)
-            acc += c
-        offs.append(o)
+        buf, reg = parts_[t]
+        if reg is not None and allc[rank][t * (nb + 1) + nb]:  # a region overflowed: the counting partition
+            T, k, sc, sv = tabs[t]
+            buf, reg = _repartition(ops, T, bounds, k, sc, sv), None
+        if reg is None:  # bucket-contiguous
+            reg = [sum(counts[t][rank][:b]) for b in range(nb)]
+        end = max([reg[b] + counts[t][rank][b] for b in range(nb)] + [0])
+        # only the rows the regions hold go to the wire (under gloo: a host copy)
+        sends.append(buf[:end].to(wire))
+        regs.append(reg)
+    del parts_
+    G = [[sum(counts[t][r][b] for r in range(world)) for b in range(nb)] for t in range(2)]
+    cuts = choose_cuts(G[0], G[1], single, nseg)
+    # every source rank's row ranges per segment, from the gathered counts
+    sl = [[slice_ranges(counts[t][r], [sum(counts[t][q][b] for q in range(r)) for b in range(nb)], cuts, nb)
+           for r in range(world)] for t in range(2)]
+    seg = [[[sum(hi - lo for (_, lo, hi) in sl[t][r][j]) for j in range(nseg)] for r in range(world)]
+           for t in range(2)]
     rows_in = [sum(seg[t][r][rank * K + k] for r in range(world) for k in range(K)) for t in range(2)]
     bound = sum(min(sum(seg[0][r][rank * K + k] for r in range(world)),
                     sum(seg[1][r][rank * K + k] for r in range(world))) for k in range(K))
     into = getattr(ops, "writes_into", False)
     ncols = R.shape[1] + S.shape[1] - 1
+    pending = [post_stage(0, K, sends, regs, sl, rank, world, R.device, group, loopback)]
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
-    pending = [post_stage(0, K, sends, offs, seg, rank, world, R.device, group, loopback)]  # R's stage 0
-    rowsS = ops.partition_apply(S, bounds, planS, k2, sc2, sv2)  # overlaps R's stage-0 exchange
-    del planS
-    sends[1] = rowsS[:mine[1]].to(wire)
-    del rowsS
-    pending.append(post_stage(0, K, [None, sends[1]], offs, seg, rank, world, R.device, group, loopback))
-    tr("J alloc + S scatter + stage 0 posted")
+    tr("stage 0 posted")
     for k in range(K):
         Rk, Sk = _wait_all(pending)
         tr(f"stage {k} received")
         if k + 1 < K:
-            pending = [post_stage(k + 1, K, sends, offs, seg, rank, world, R.device, group, loopback)]
+            pending = [post_stage(k + 1, K, sends, regs, sl, rank, world, R.device, group, loopback)]
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
             continue
         if into:

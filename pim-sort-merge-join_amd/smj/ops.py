@@ -339,6 +339,60 @@ def partition_apply(table, bounds, plan, key_col=0, select_col=0, select_val=Non
     return out
 
 
+def region_capacities(sample_keys, n, bounds, tile=4096, sigmas=8.0):
+    """Region starts / capacities (rows) for partition_regions from a key
+    sample of the table (host list): bucket b's estimated rows + sigmas binomial
+    standard deviations + one tile, capped at n (as msd_part1 sizes the
+    partitioned mode's regions).  Returns (h_region list of 2 (nb) ints, rows
+    the output buffer needs)."""
+    import bisect
+    nb = len(bounds) + 1
+    m = len(sample_keys)
+    sc = [0] * nb
+    for k in sample_keys:
+        sc[bisect.bisect_left(bounds, k)] += 1
+    starts, caps, at = [], [], 0
+    for b in range(nb):
+        if m == 0:
+            cap = n
+        else:
+            f = sc[b] / m
+            est = n * f
+            sd = n / m * (m * f * (1.0 - f) + 1.0) ** 0.5
+            cap = min(n, int(est + sigmas * sd) + tile)
+        starts.append(at)
+        caps.append(cap)
+        at += cap
+    return starts + caps, at
+
+
+def partition_regions(table, bounds, region, counts, key_col=0, select_col=0, select_val=None, out=None,
+                      stream=None):
+    """One-read stable partition (smj_dev_partition_regions): bucket b's rows
+    at out[region[b]: region[b] + count_b]; `counts` (a 1-D int64 CUDA tensor of
+    len(bounds) + 2 entries) gets the exact counts and, last, the overflow /
+    timeout flag word.  Asynchronous.  Returns out."""
+    lib = _lib.load()
+    _table(table, "table")
+    n, cols = table.shape
+    nb = len(bounds) + 1
+    if len(region) != 2 * nb:
+        raise ValueError("region must hold 2 (len(bounds) + 1) entries")
+    need = max(region[b] + region[nb + b] for b in range(nb)) if n else 0
+    if not (counts.is_cuda and counts.dtype == torch.int64 and counts.is_contiguous() and counts.numel() == nb + 1):
+        raise ValueError("counts must be a contiguous int64 CUDA tensor of len(bounds) + 2 entries")
+    out = torch.empty((max(need, 1), cols), dtype=torch.int64, device=table.device) if out is None else \
+        _out(out, "out", need, cols, table)
+    spl, ns = _host_splitters(bounds)
+    reg = (ctypes.c_int64 * len(region))(*[int(v) for v in region])
+    use = select_val is not None
+    _lib.check(lib.smj_dev_partition_regions(_ptr(table), n, cols, int(use), select_col,
+                                             int(select_val) if use else 0, key_col, spl, ns, reg, _ptr(out),
+                                             ctypes.c_void_p(counts.data_ptr()), _stream(stream)),
+               "smj_dev_partition_regions")
+    return out
+
+
 def gen_uniform(rows, row0=0, seed=1, key_range=None, device="cuda", out=None, stream=None):
     """Synthetic (key, payload) table: keys iid uniform in [1, key_range],
     payload = global row index."""

@@ -71,6 +71,28 @@ class OracleOps:
         return torch.from_numpy(keep[np.argsort(bucket, kind="stable")].copy())
 
     @staticmethod
+    def region_capacities(own, n, bounds):
+        from smj import ops as hip_ops  # pure host arithmetic (no GPU)
+        return hip_ops.region_capacities(own, n, bounds)
+
+    @staticmethod
+    def partition_regions(T, bounds, reg, counts, key=0, sc=0, sv=None):
+        """smj_dev_partition_regions' contract: bucket b's rows (stable) at
+        reg[b], at most reg[nb + b] of them; exact counts; flag on overflow."""
+        keep, bucket = OracleOps._keep(T, key, sc, sv, torch.tensor(bounds, dtype=torch.int64))
+        nb = len(bounds) + 1
+        out = np.zeros((max(max(reg[b] + reg[nb + b] for b in range(nb)), 1), T.shape[1]), dtype=np.int64)
+        over = 0
+        for b in range(nb):
+            rows = keep[bucket == b]
+            c = min(len(rows), reg[nb + b])
+            out[reg[b]: reg[b] + c] = rows[:c]
+            over |= len(rows) > reg[nb + b]
+        cnt = np.bincount(bucket, minlength=nb).astype(np.int64)
+        counts.copy_(torch.from_numpy(np.concatenate([cnt, [int(over)]]).astype(np.int64)))
+        return torch.from_numpy(out)
+
+    @staticmethod
     def partition(T, spl, key=0, sc=0, sv=None):
         counts, _ = OracleOps.partition_count(T, spl, key, sc, sv)
         return counts, OracleOps.partition_scatter(T, spl, counts, key, sc, sv)
@@ -174,6 +196,14 @@ def test_distributed_hip_eight_ranks_one_gpu(tmp_path, oracle_built, pkg_built, 
     _run_and_check(tmp_path, 8, kind, cfg, 800_000)
 
 
+def test_region_overflow_falls_back(tmp_path, oracle_built, monkeypatch):
+    """Regions sized below the bucket counts (SMJ_DIST_REGION_SCALE): the
+    overflowing ranks re-partition with plan / apply and the result is the
+    same (the one-read pass counts every row, so the cuts do not change)."""
+    monkeypatch.setenv("SMJ_DIST_REGION_SCALE", "0.5")
+    _run_and_check(tmp_path, 3, "skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 8}, 30_000)
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
     """Loopback mode (each rank's own segments through send / receive to
@@ -222,6 +252,19 @@ def test_stage_count():
     # 2 (W K - 1) boundaries must fit the 64-bucket partition kernel
     assert [sdist.stage_count(w, 4) for w in (2, 4, 8, 16)] == [4, 4, 4, 2]
     assert sdist.stage_count(8, 1) == 1 and sdist.stage_count(32, 4) == 1
+
+
+def test_slice_ranges_match_slice_counts():
+    """Per-segment (bucket, lo, hi) ranges: their sizes are slice_counts', they
+    tile each bucket's local rows, and a single-key bucket is split at the
+    occurrence cut."""
+    from smj import dist as sdist
+    local, prefix = [3, 0, 7, 5, 2], [1, 0, 4, 0, 9]
+    cuts = [(2, 6), (2, 6), (3, 0), (4, 10)]
+    rs = sdist.slice_ranges(local, prefix, cuts, 5)
+    assert [sum(h - l for _, l, h in r) for r in rs] == sdist.slice_counts(local, prefix, cuts, 5)
+    assert rs[0] == [(0, 0, 3), (2, 0, 2)] and rs[1] == [] and rs[2] == [(2, 2, 7)]
+    assert rs[3] == [(3, 0, 5), (4, 0, 1)] and rs[4] == [(4, 1, 2)]
 
 
 def test_choose_cuts_pure():
