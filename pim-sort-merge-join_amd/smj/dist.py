@@ -48,7 +48,21 @@ from . import ops as hip_ops
 INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
 MAX_BOUNDS = 63  # smj_dev_partition*: <= 64 buckets
-DEFAULT_STAGES = int(os.environ.get("SMJ_DIST_STAGES", "2"))
+# Exchange stages K (key sub-ranges per rank whose exchange overlaps the
+# previous one's sort + join).  One GPU (the RCCL loopback) measured best at
+# K = 2 (profiles/r03/r03zg_loop_stages.txt: the self-copies share HBM with the
+# pipeline, so more stages only add calls).  Across GPUs the exchange runs
+# over xGMI, not HBM, and dominates: (W - 1) / W of 3.2 GB per C3 rank over
+# W - 1 links of ~76 GB/s per direction (W = 8: ~5 ms, W = 2: ~21 ms, against
+# ~5 ms of local compute), so the exposed part, ~T_x / K + max(T_x, T_c) (K -
+# 1) / K + T_c / K, is smallest at the largest K the partition allows (4 at W
+# = 8; stage_count).  A model, not a measurement: no 8-GPU node has run it.
+_STAGES_ENV = os.environ.get("SMJ_DIST_STAGES")
+DEFAULT_STAGES = int(_STAGES_ENV) if _STAGES_ENV else None
+
+
+def default_stages(world):
+    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (2 if world == 1 else 4)
 # loopback: a rank's own segment also travels through the point-to-point
 # transport (send / receive to itself; RCCL only: gloo keeps the device copy)
 # instead of a device copy, and one rank runs the whole distributed path: the
@@ -427,7 +441,7 @@ def _repartition(ops, T, bounds, k, sc, sv):
 
 
 def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
-    K = stage_count(world, DEFAULT_STAGES if stages is None else stages)
+    K = stage_count(world, default_stages(world) if stages is None else stages)
     nseg = world * K
     tr = _Tracer(TRACE and R.is_cuda, rank)
 
