@@ -84,9 +84,13 @@ def parse():
     p.add_argument("--loopback", action="store_true",
                    help="N = 1 through the distributed path (smj.dist, RCCL process group of one rank, "
                         "own segments sent to itself): the multi-GPU pipeline's cost without cross-GPU traffic")
-    p.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
-                   help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field")
-    return p.parse_args()
+    p.add_argument("--pmc", default=None,
+                   help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field "
+                        "(default: profiles/pmc_traffic.json for c3, profiles/pmc_traffic_<workload>.json otherwise)")
+    a = p.parse_args()
+    if a.pmc is None:
+        a.pmc = os.path.join(REPO, "profiles", "pmc_traffic.json" if a.workload == "c3" else f"pmc_traffic_{a.workload}.json")
+    return a
 
 
 def workload_name(w, world, distributed):

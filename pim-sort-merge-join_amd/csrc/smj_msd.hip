@@ -2665,6 +2665,9 @@ struct StSmem {
 #ifndef SMJ_ABLATE
 #define SMJ_ABLATE 0
 #endif
+#ifndef SMJ_ST_BATCH
+#define SMJ_ST_BATCH 0  // st_issue_lists: the row lookups batched over the items (A/B)
+#endif
 #ifndef SMJ_ST_FIX
 #define SMJ_ST_FIX 0  // equal-key runs ordered by a rank within the run (two barriers) instead of fl transposition rounds
 #endif
@@ -2756,6 +2759,56 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
     ST_SUB(4);
     const i64x2 *tB0 = reinterpret_cast<const i64x2 *>(p.tab[0].tempB);
     const i64x2 *tB1 = reinterpret_cast<const i64x2 *>(p.tab[1].tempB);
+    if (SMJ_ST_BATCH && !ST_ABL(4)) {
+        // the same lookups with every LDS read unconditional (indices clamped),
+        // stage by stage over the items: the four items' reads are issued
+        // together instead of three dependent round trips per item behind
+        // each item's branch (the "next gathers" phase, profiles/r03/r03q);
+        // only the global loads stay predicated
+        const uint64_t lm = ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
+        uint64_t m[kStIt];
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t b = (tid + k * kStThreads) >> 6;  // wave-uniform
+            const uint2 sw = *reinterpret_cast<const uint2 *>(&sm.L.starts[2 * b]);
+            m[k] = (((uint64_t)sw.y << 32) | sw.x) & lm;
+        }
+        uint32_t e[kStIt];
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t v = tid + k * kStThreads, b = v >> 6;
+            const uint32_t ia = (b << 6) + 63u - (uint32_t)__clzll((long long)(m[k] | 1ull));
+            const uint32_t ea = sm.L.at[ia], eb = sm.L.btab[b];
+            e[k] = m[k] ? ea : eb;
+        }
+        uint2 le[kStIt];
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t v = tid + k * kStThreads;
+            const uint32_t x = COMB ? (e[k] >= (uint32_t)kStList ? 1u : 0u) : (L.is_s(k, v) ? 1u : 0u);
+            const uint32_t j = min(e[k] - x * (uint32_t)kStList, (uint32_t)kStList - 1u);  // clamped: a row no group holds
+            le[k] = sm.L.list[x][j];
+        }
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) asm volatile("" ::"v"(le[k].x), "v"(le[k].y));  // not sunk into the branches
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t v = tid + k * kStThreads;
+            const uint32_t x = COMB ? (e[k] >= (uint32_t)kStList ? 1u : 0u) : (L.is_s(k, v) ? 1u : 0u);
+            i64x2 r = {0, 0};
+            if (L.valid(k, v)) {
+                int64_t ix = (int64_t)le[k].x + ((v - (x ? L.sp : 0u)) - le[k].y);
+                if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
+                    atomicOr(&p.plan->err, 2u);
+                    ix = 0;
+                }
+                r = (x ? tB1 : tB0)[ix];
+            }
+            rows[k] = r;
+        }
+        ST_SUB(5);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kStIt; k++) {
         const uint32_t v = tid + k * kStThreads, b = v >> 6;

@@ -317,6 +317,18 @@ def _wait_all(pending):
     return out
 
 
+# RCCL point-to-point messages above ~2 GiB arrive corrupted (tools/rccl_big.py,
+# profiles/r04/r04e: a 2.34 GiB send to self differs, 0.5 GiB is exact), so
+# every (peer, bucket range) message is cut into pieces of at most this many
+# bytes -- on both sides alike, in order
+MAX_MSG_BYTES = int(os.environ.get("SMJ_DIST_MAX_MSG", str(512 << 20)))
+
+
+def _pieces(lo, hi, cols):
+    step = max(1, MAX_MSG_BYTES // (8 * cols))
+    return [(a, min(hi, a + step)) for a in range(lo, hi, step)]
+
+
 def post_stage(k, K, sends, regs, sl, rank, world, home, group=None, loopback=False):
     """Post stage k's exchange: segment d*K + k of every table goes to rank d.
     sl[t][r][j] = the (bucket, lo, hi) local row ranges of src rank r's table-t
@@ -336,6 +348,7 @@ def post_stage(k, K, sends, regs, sl, rank, world, home, group=None, loopback=Fa
         rc = sum(hi - lo for r in range(world) for (_, lo, hi) in sl[t][r][me])
         recv = torch.empty((rc, wire.shape[1]), dtype=wire.dtype, device=wire.device)
         at = 0
+        cols = wire.shape[1]
         for r in range(world):
             for b, lo, hi in sl[t][r][me]:
                 c = hi - lo
@@ -343,14 +356,16 @@ def post_stage(k, K, sends, regs, sl, rank, world, home, group=None, loopback=Fa
                     o = regs[t][b] + lo
                     recv[at: at + c].copy_(wire[o: o + c])
                 else:
-                    p2p.append(dist.P2POp(dist.irecv, recv[at: at + c], r, group, tag=(t * 64 + b) * 64 + k))
+                    for a0, a1 in _pieces(at, at + c, cols):
+                        p2p.append(dist.P2POp(dist.irecv, recv[a0: a1], r, group, tag=(t * 64 + b) * 64 + k))
                 at += c
         for d in range(world):
             if d == rank and not loopback:
                 continue
             for b, lo, hi in sl[t][rank][d * K + k]:
                 o = regs[t][b] + lo
-                p2p.append(dist.P2POp(dist.isend, wire[o: o + hi - lo], d, group, tag=(t * 64 + b) * 64 + k))
+                for a0, a1 in _pieces(o, o + hi - lo, cols):
+                    p2p.append(dist.P2POp(dist.isend, wire[a0: a1], d, group, tag=(t * 64 + b) * 64 + k))
         recvs.append(recv)
     works = dist.batch_isend_irecv(p2p) if p2p else []
     return _Stage(works, recvs, home)

@@ -216,13 +216,18 @@ def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
 @pytest.mark.parametrize("kind,cfg", [
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
     ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True, "stages": 4}),
+    # messages cut into 64 KiB pieces (SMJ_DIST_MAX_MSG; RCCL corrupts p2p
+    # messages over ~2 GiB, profiles/r04/r04e): hundreds of pieces per stage
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "max_msg": 65536}),
 ])
-def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
+def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, monkeypatch, kind, cfg):
     """The RCCL transport of smj/dist.py on the one GPU a test box has: one
     rank under the nccl backend (RCCL) in loopback mode, so the partition,
     the device-resident send buffers, the staged batch_isend_irecv over the
     RCCL communicator (to itself) and the stage-overlapped local pipeline
     all run as on the 8-GPU node, bit-exact against the oracle."""
+    if cfg.get("max_msg"):
+        monkeypatch.setenv("SMJ_DIST_MAX_MSG", str(cfg["max_msg"]))
     _run_and_check(tmp_path, 1, kind, dict(cfg, backend="nccl", loopback=True), 1_000_000)
 
 
@@ -252,6 +257,19 @@ def test_stage_count():
     # 2 (W K - 1) boundaries must fit the 64-bucket partition kernel
     assert [sdist.stage_count(w, 4) for w in (2, 4, 8, 16)] == [4, 4, 4, 2]
     assert sdist.stage_count(8, 1) == 1 and sdist.stage_count(32, 4) == 1
+
+
+def test_message_pieces_tile_the_range(monkeypatch):
+    """A (peer, bucket range) message is cut into pieces of <= MAX_MSG_BYTES;
+    sender and receiver cut identically (same lengths from their own base)."""
+    from smj import dist as sdist
+    monkeypatch.setattr(sdist, "MAX_MSG_BYTES", 1000)
+    p = sdist._pieces(5, 5 + 200, 2)  # 62 rows of 16 B per piece
+    assert p[0] == (5, 67) and p[-1][1] == 205 and all(b - a <= 62 for a, b in p)
+    assert all(p[i][1] == p[i + 1][0] for i in range(len(p) - 1))
+    q = sdist._pieces(1000, 1200, 2)
+    assert [b - a for a, b in p] == [b - a for a, b in q]
+    assert sdist._pieces(7, 7, 2) == []
 
 
 def test_slice_ranges_match_slice_counts():

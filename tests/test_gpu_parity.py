@@ -189,6 +189,46 @@ def test_partition_plan_apply_matches_numpy(gpu, n, cols, sv):
             ops.partition_apply(dt, bounds, plan, 0, sc, sv, out=dt)
 
 
+@pytest.mark.parametrize("n,cols,sv,scale", [(300_001, 2, -900, 1.0), (0, 2, None, 1.0), (70_000, 3, 2000, 1.0),
+                                             (1, 2, None, 1.0), (250_000, 4, None, 0.4), (1_000_000, 2, None, 1.0)])
+def test_partition_regions_matches_numpy(gpu, n, cols, sv, scale):
+    """smj_dev_partition_regions (smj/dist.py's one-read partition): bucket b's
+    selected rows, stable, at their region start; exact counts; the overflow
+    flag when regions are sized below the counts (scale < 1: the rows past a
+    region's capacity are not written, the counts stay exact); in == out
+    refused."""
+    from smj import _lib, ops
+    rng = np.random.default_rng(n + 29)
+    t = rng.integers(-1000, 1000, size=(n, cols), dtype=np.int64)
+    if n:
+        t[:, 1] = np.arange(n)
+    bounds = [-600, -1, 0, 0, 17, 400]
+    nb = len(bounds) + 1
+    dt = dev(t).reshape(n, cols)
+    sample = t[:, 0][np.linspace(0, max(n - 1, 0), min(n, 4096)).astype(int)].tolist() if n else []
+    reg, need = ops.region_capacities(sample, n, bounds)
+    if scale < 1.0:
+        caps = [int(c * scale) for c in reg[nb:]]
+        reg = [sum(caps[:b]) for b in range(nb)] + caps
+    cnt = torch.full((nb + 1,), -1, dtype=torch.int64, device="cuda")
+    sc = cols - 1
+    out = ops.partition_regions(dt, bounds, reg, cnt, 0, sc, sv)
+    keep = t if sv is None else t[t[:, sc] > sv]
+    bucket = np.searchsorted(np.array(bounds), keep[:, 0], side="left")
+    c = host(cnt)
+    assert c[:nb].tolist() == np.bincount(bucket, minlength=nb).tolist()
+    over = any(c[b] > reg[nb + b] for b in range(nb))
+    assert (c[nb] & 1) == int(over) and (c[nb] & 2) == 0 and over == (scale < 1.0 and n > 0)
+    got = host(out)
+    for b in range(nb):
+        rows = keep[bucket == b]
+        k = min(len(rows), reg[nb + b])
+        np.testing.assert_array_equal(got[reg[b]: reg[b] + k], rows[:k])
+    if n:
+        with pytest.raises((_lib.SmjError, ValueError)):  # the C layer (in == out) or the size check first
+            ops.partition_regions(dt, bounds, reg, cnt, 0, sc, sv, out=dt)
+
+
 def test_gen_uniform_matches_oracle(gpu, oracle_built):
     from smj import ops
     got = ops.gen_uniform(1_000_003, row0=12345, seed=2, key_range=3_000_000)

@@ -73,6 +73,9 @@ for s in $STEPS; do
                python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmcsq) run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
                --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
+    pmcsq2) run pmc_sq2 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES \
+               --output-format csv -d "$OUT/pmc_sq2" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
+    pmclist) run pmclist 60 rocprofv3 -L ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;

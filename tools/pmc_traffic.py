@@ -39,6 +39,12 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_count_scan_kernel", "msd_count_scan", True),
     (r"msd_compact_kernel", "msd_compact", True),
     (r"gen_uniform_kernel", "gen_uniform", True),
+    (r"gen_zipf_kernel", "gen_zipf", True),
+    (r"msd_part1_kernel", "partition_1pass", True),
+    (r"msd_big_res_kernel", "msd_big_dev", True),
+    (r"msd_big_stage_kernel", "msd_big_dev", False),
+    (r"msd_giant_\w+_kernel", "msd_big_dev", False),
+    (r"msd_single_kernel", "msd_single", True),
 ]
 
 
@@ -86,6 +92,7 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--workload", default="c3", help="bench.py --workload the runs timed (c3 / c4 / c5)")
     ap.add_argument("-o", "--out", default="profiles/pmc_traffic.json")
     a = ap.parse_args()
     base = os.path.splitext(a.out)[0]
@@ -99,7 +106,7 @@ def main():
         w = write.get(t, 0.0) / max(nw.get(t, 0), 1)
         kernels[t] = {"launches": nf.get(t, 0), "fetch_kib_raw": round(f, 1),
                       "write_kib": round(w, 1), "hbm_bytes_per_launch": round((2 * f + w) * 1024)}
-    out = {"rows_per_table": a.rows, "source": [fcsv, wcsv],
+    out = {"rows_per_table": a.rows, "workload": a.workload, "source": [fcsv, wcsv],
            "raw_runs": [a.fetch_dir, a.write_dir],
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB per scope launch (gfx950: FETCH_SIZE "
                          "counts half of a wide coalesced read; MI355X_MICROARCH.md, HBM)",
