@@ -291,7 +291,6 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
                          // Every kernel after msd_group_kernel returns at entry once err != 0
                          // (msd_plan_failed), so a failed plan never drives a gather or a store.
     uint32_t gticket;    // msd_group_kernel: bucket tickets, taken in the order workgroups start
-    uint32_t bgticket_res;  // msd_big_res_kernel's group tickets
 };
 // A kernel launched after msd_group_kernel reads the plan's error word first:
 // a set bit means the dense group array may hold slots this call never wrote.

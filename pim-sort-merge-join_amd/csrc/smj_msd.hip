@@ -2665,12 +2665,6 @@ struct StSmem {
 #ifndef SMJ_ABLATE
 #define SMJ_ABLATE 0
 #endif
-#ifndef SMJ_ST_BATCH
-#define SMJ_ST_BATCH 0  // st_issue_lists: the row lookups batched over the items (A/B)
-#endif
-#ifndef SMJ_ST_FIX
-#define SMJ_ST_FIX 0  // equal-key runs ordered by a rank within the run (two barriers) instead of fl transposition rounds
-#endif
 #define ST_ABL(bit) (SMJ_ABLATE && (p.dbg & (bit)))
 
 template <bool COMB>
@@ -2759,56 +2753,6 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
     ST_SUB(4);
     const i64x2 *tB0 = reinterpret_cast<const i64x2 *>(p.tab[0].tempB);
     const i64x2 *tB1 = reinterpret_cast<const i64x2 *>(p.tab[1].tempB);
-    if (SMJ_ST_BATCH && !ST_ABL(4)) {
-        // the same lookups with every LDS read unconditional (indices clamped),
-        // stage by stage over the items: the four items' reads are issued
-        // together instead of three dependent round trips per item behind
-        // each item's branch (the "next gathers" phase, profiles/r03/r03q);
-        // only the global loads stay predicated
-        const uint64_t lm = ((2ull << lane) - 1ull) & ~1ull;  // range starts in (64b, v]
-        uint64_t m[kStIt];
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t b = (tid + k * kStThreads) >> 6;  // wave-uniform
-            const uint2 sw = *reinterpret_cast<const uint2 *>(&sm.L.starts[2 * b]);
-            m[k] = (((uint64_t)sw.y << 32) | sw.x) & lm;
-        }
-        uint32_t e[kStIt];
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t v = tid + k * kStThreads, b = v >> 6;
-            const uint32_t ia = (b << 6) + 63u - (uint32_t)__clzll((long long)(m[k] | 1ull));
-            const uint32_t ea = sm.L.at[ia], eb = sm.L.btab[b];
-            e[k] = m[k] ? ea : eb;
-        }
-        uint2 le[kStIt];
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t v = tid + k * kStThreads;
-            const uint32_t x = COMB ? (e[k] >= (uint32_t)kStList ? 1u : 0u) : (L.is_s(k, v) ? 1u : 0u);
-            const uint32_t j = min(e[k] - x * (uint32_t)kStList, (uint32_t)kStList - 1u);  // clamped: a row no group holds
-            le[k] = sm.L.list[x][j];
-        }
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) asm volatile("" ::"v"(le[k].x), "v"(le[k].y));  // not sunk into the branches
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t v = tid + k * kStThreads;
-            const uint32_t x = COMB ? (e[k] >= (uint32_t)kStList ? 1u : 0u) : (L.is_s(k, v) ? 1u : 0u);
-            i64x2 r = {0, 0};
-            if (L.valid(k, v)) {
-                int64_t ix = (int64_t)le[k].x + ((v - (x ? L.sp : 0u)) - le[k].y);
-                if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
-                    atomicOr(&p.plan->err, 2u);
-                    ix = 0;
-                }
-                r = (x ? tB1 : tB0)[ix];
-            }
-            rows[k] = r;
-        }
-        ST_SUB(5);
-        return;
-    }
 #pragma unroll
     for (int k = 0; k < kStIt; k++) {
         const uint32_t v = tid + k * kStThreads, b = v >> 6;
@@ -3029,41 +2973,6 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // run, r01k; the run's first thread insertion-sorting the run, r01ah:
     // 2.81 vs 2.32 ms.)
     static_assert(kStRows / 2 == 2 * kStThreads, "two compare-exchanges per thread and round");
-    if (SMJ_ST_FIX && !lsd && fl > 2u && !ST_ABL(16)) {
-        // runs of up to kMaxDupRun equal residuals in two barriers whatever
-        // their length: every word of a run ranks itself among the run's words
-        // by group row (the run's bounds from the histogram starts) and moves
-        // to start + rank (fl > 2: two rounds of the transposition cost the
-        // same two barriers)
-        uint32_t nw[kStIt], np[kStIt];
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t q = (uint32_t)(tid + k * kStThreads);
-            np[k] = ~0u;
-            nw[k] = 0;
-            if (L.valid_pos(q)) {
-                const uint32_t w0 = sm.key[q], res = w0 >> kStIdx, x = q >= sp ? 1u : 0u, sh = 16u * (res & 1u);
-                const uint32_t hw = sm.hist[x][res >> 1];
-                const uint32_t st = (hw >> sh) & 0xffffu;
-                const uint32_t en = (res & 1u) ? ((res + 1u < (uint32_t)kStRange) ? (sm.hist[x][(res + 1) >> 1] & 0xffffu)
-                                                                                 : (x ? nS : nR))
-                                               : (hw >> 16);
-                if (en - st > 1u) {
-                    const uint32_t b0 = (x ? sp : 0u) + st, me = w0 & kStIdxMask;
-                    uint32_t rk = 0;
-                    for (uint32_t j = b0; j < b0 + (en - st); j++) rk += (sm.key[j] & kStIdxMask) < me ? 1u : 0u;
-                    np[k] = b0 + rk;
-                    nw[k] = w0;
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kStIt; k++)
-            if (np[k] != ~0u) sm.key[np[k]] = nw[k];
-        __syncthreads();
-        fl = 0;  // no transposition rounds
-    }
     for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd) ? 0u : fl); rd++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -3681,119 +3590,6 @@ __device__ __forceinline__ void bg_scatter_ids(const MsdFinalParams &p, const Ms
     }
 }
 
-// ---- one read per row (round 4): tables of <= kBgResRows rows ------------
-// The two-pass path reads every row twice (count, then scatter).  A table of
-// at most kBgResRows rows (C5: most oversized groups) is loaded ONCE into
-// registers -- chunk c, item i, lane = the scatter's input order -- counted
-// from them, and placed from them: one table at a time (32 VGPRs of rows), so
-// the counts, ids and starts are per table; the join runs once both tables
-// are placed (bg_jst_from_ends).  Ends of each residual's rows accumulate in
-// sm.end[X] exactly as on the two-pass path.
-#ifndef SMJ_BG_RES
-#define SMJ_BG_RES 1
-#endif
-constexpr int kBgResChunks = 4;
-constexpr uint32_t kBgResRows = kBgResChunks * kGroupCap;
-__device__ __forceinline__ bool bg_res(const MsdFinalParams &p, const MsdGroup &g) {
-    return SMJ_BG_RES && max(g.nR, p.ntab > 1 ? g.nS : 0u) <= kBgResRows;
-}
-
-// per-table ids of the distinct residuals (sm.end[X] = this table's counts)
-// and its exclusive starts in sm.end[X]; ends with a barrier
-template <int X>
-__device__ __forceinline__ void bg_ids_starts_one(BgSmem &sm) {
-    constexpr int RP = kStRange / kMsdThreads;
-    const int tid = threadIdx.x;
-    uint32_t c[RP], f = 0, nz = 0, sum = 0;
-#pragma unroll
-    for (int j = 0; j < RP; j++) {
-        c[j] = sm.end[X][tid * RP + j];
-        f |= c[j] ? (1u << j) : 0u;
-        nz += c[j] ? 1u : 0u;
-        sum += c[j];
-    }
-    uint32_t all, tot;
-    uint32_t ex = block_excl_scan<kMsdWaves>(nz, sm.wsum, &all);
-    uint32_t run = block_excl_scan<kMsdWaves>(sum, sm.wsum, &tot);
-    if (all <= (uint32_t)kBgIds) {
-#pragma unroll
-        for (int j = 0; j < RP; j++)
-            if ((f >> j) & 1u) {
-                const int r = tid * RP + j;
-                sm.id[r] = (uint8_t)ex;
-                sm.rid[ex] = (uint16_t)r;
-                ex++;
-            }
-    }
-#pragma unroll
-    for (int j = 0; j < RP; j++) {
-        sm.end[X][tid * RP + j] = run;
-        run += c[j];
-    }
-    if (tid == 0) sm.nid = all;
-    __syncthreads();
-}
-
-// table X of group g (n <= kBgResRows rows) sorted into its output rows with
-// one read: load, count, ids + starts, place (parallel ranking by ids, or the
-// waves in turn when the table has over kBgIds distinct residuals)
-template <int X>
-__device__ __forceinline__ void bg_resident(const MsdFinalParams &p, const MsdGroup &g, uint32_t n, BgSmem &sm) {
-    const MsdTab &tb = p.tab[X];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    i64x2 rows[kBgResChunks][kBgIt];
-    uint32_t vm[kBgResChunks];
-#pragma unroll
-    for (int c = 0; c < kBgResChunks; c++) bg_load_chunk<X>(p, sm, (uint32_t)c * kGroupCap, n, rows[c], vm[c]);
-    uint32_t *cnt = sm.end[X];
-#pragma unroll
-    for (int c = 0; c < kBgResChunks; c++)
-#pragma unroll
-        for (int i = 0; i < kBgIt; i++) {
-            const bool v = (vm[c] >> i) & 1u;
-            const uint32_t r = (uint32_t)((uint64_t)(tb.key ? rows[c][i].y : rows[c][i].x) - (uint64_t)g.base);
-            const uint64_t act = __ballot(v);
-            if (act == 0) continue;
-            // the wave's rows of its first active residual (the heavy key's, in
-            // a Zipf group) by one atomic, the others lane by lane
-            const int lead = __ffsll((unsigned long long)act) - 1;
-            const uint32_t r0 = (uint32_t)__shfl((int)r, lead, 64);
-            const uint64_t same = __ballot(v && r == r0);
-            if (v && r == r0) {
-                if (lane == lead) atomicAdd(&cnt[r0], (uint32_t)__popcll(same));
-            } else if (v) {
-                atomicAdd(&cnt[r], 1u);
-            }
-        }
-    __syncthreads();
-    bg_ids_starts_one<X>(sm);
-    if (sm.nid <= (uint32_t)kBgIds) {
-#pragma unroll
-        for (int c = 0; c < kBgResChunks; c++)
-            if ((uint32_t)c * kGroupCap < n) bg_place_ids<X>(p, g, rows[c], vm[c], sm);  // block-uniform
-    } else {
-        i64x2 *dst = reinterpret_cast<i64x2 *>(tb.out) + (X ? g.outS : g.outR);
-#pragma unroll
-        for (int c = 0; c < kBgResChunks; c++) {
-            if ((uint32_t)c * kGroupCap >= n) break;
-            uint32_t dig[kBgIt], pos[kBgIt];
-#pragma unroll
-            for (int i = 0; i < kBgIt; i++)
-                dig[i] = ((vm[c] >> i) & 1u)
-                             ? (uint32_t)((uint64_t)(tb.key ? rows[c][i].y : rows[c][i].x) - (uint64_t)g.base)
-                             : 0u;
-            for (int w = 0; w < kMsdWaves; w++) {
-                if (wave == w) bg_rank<kBgIt, 12>(dig, vm[c], sm.end[X], lane, pos);
-                __syncthreads();
-            }
-#pragma unroll
-            for (int i = 0; i < kBgIt; i++)
-                if ((vm[c] >> i) & 1u) dst[pos[i]] = rows[c][i];
-        }
-    }
-    __syncthreads();  // sm.end[X] = this table's ends; ids / per-wave counters free for the next table
-}
-
 // join rows [j0, j1) of group g: row j of residual r (jst[r] <= j < jst[r + 1])
 // pairs occurrence i = j - jst[r] of r in R and in S, whose sorted output
 // rows start at startR(r), startS(r) (ends: those of r - 1)
@@ -3921,7 +3717,6 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
             continue;
         }
         if (!bg_ok(g, p.bg_max)) continue;  // block-uniform: a giant, or left to the host fallback
-        if (bg_res(p, g)) continue;         // one read per row: msd_big_res_kernel
         if ((max(g.nR, g.nS) > kBgLarge) != (round == 0)) continue;
         if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) bg_g = bg_t = __builtin_amdgcn_s_memtime();
         for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
@@ -3960,56 +3755,6 @@ __global__ __launch_bounds__(kMsdThreads, 2) void msd_big_stage_kernel(const Msd
             __syncthreads();
             bg_jst_from_ends(sm);
             bg_join(p, g, 0, J, sm, true);
-        }
-        BG_STAMP(4);
-        if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) {
-            const int c = 31 - __clz(max(max(g.nR, g.nS), 1u));
-            atomicAdd(&g_bg_cls[0][c], bg_t - bg_g);
-            atomicAdd(&g_bg_cls[1][c], 1ull);
-        }
-    }
-}
-
-// the oversized groups whose tables hold <= kBgResRows rows each, one read
-// per row (bg_resident), dealt by tickets over the list: its own kernel, so
-// that the two-pass kernel's registers do not limit this one (128 VGPRs, two
-// workgroups per CU)
-__global__ __launch_bounds__(kMsdThreads, 4) void msd_big_res_kernel(const MsdFinalParams p) {
-    __shared__ BgSmem sm;
-    if (msd_plan_failed(p.plan)) return;
-    const uint32_t nbig = p.plan->nbig;
-    const int tid = threadIdx.x;
-    const bool join = p.join && p.ntab > 1;
-    unsigned long long bg_t = 0, bg_g = 0;
-    for (;;) {
-        __syncthreads();  // LDS of the previous group / ticket read out
-        if (tid == 0) sm.ticket = atomicAdd(&p.plan->bgticket_res, 1u);
-        __syncthreads();
-        const uint32_t bi = sm.ticket;
-        if (bi >= nbig) break;
-        const uint32_t gi = p.big_list[bi];
-        const MsdGroup g = p.groups[gi];
-        if (!(bg_ok(g, p.bg_max) && bg_res(p, g))) continue;  // block-uniform
-        if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) bg_g = bg_t = __builtin_amdgcn_s_memtime();
-        for (int i = tid; i < 2 * kStRange; i += kMsdThreads) (&sm.end[0][0])[i] = 0;
-        bg_lists(p, g, sm);
-        bg_blocks(sm, 0, g.nR, 0, g.nR);
-        if (p.ntab > 1) bg_blocks(sm, 1, g.nS, 0, g.nS);
-        BG_STAMP(0);
-        bg_resident<0>(p, g, g.nR, sm);
-        if (p.ntab > 1) bg_resident<1>(p, g, g.nS, sm);
-        BG_STAMP(3);
-        uint32_t J = 0;
-        if (join) {
-            __threadfence_block();  // the placed rows are read back by this workgroup only
-            __syncthreads();
-            bg_jst_from_ends(sm);
-            J = sm.jst[kStRange];
-            bg_join(p, g, 0, J, sm, true);
-        }
-        if (tid == 0) {
-            p.counts[gi] = J;
-            atomicAdd(&p.plan->nbigdev, 1u);
         }
         BG_STAMP(4);
         if (SMJ_STAMPS && (p.dbg & 32) && tid == 0) {
@@ -4635,8 +4380,6 @@ hipError_t launch_msd_big(const MsdFinalParams &p_in, hipStream_t s) {
     static const int dbg = getenv("SMJ_DEBUG_BIG") ? 32 : 0;
     MsdFinalParams p = p_in;
     p.dbg |= dbg;
-    static const unsigned res_grid = (unsigned)resident_blocks(msd_big_res_kernel, kMsdThreads, 0);
-    hipLaunchKernelGGL(msd_big_res_kernel, dim3(res_grid), dim3(kMsdThreads), 0, s, p);
     hipLaunchKernelGGL(msd_big_stage_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);
     // the groups over the one-workgroup limit it registered, as jobs (no-ops without)
     hipLaunchKernelGGL(msd_giant_count_kernel, dim3(bg_grid), dim3(kMsdThreads), 0, s, p);

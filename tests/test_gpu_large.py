@@ -17,6 +17,8 @@ C5 on one MI355X) of smj_dev_sort_merge_join.
       operations, so the window's oracle result must equal the output slices
       holding its keys.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -217,3 +219,24 @@ def test_c4_full_size_one_gpu(gpu, oracle_built):
     lo = int(gR[n // 3, 0])
     rows, j = check_window(R, S, gR, gS, gJ, lo, lo + 1_500_000)
     assert rows > 500_000 and j > 0
+
+
+@pytest.mark.parametrize("workload,stages", [("c3", 1), ("c5", 2)])
+def test_loopback_full_size_equals_single_call(gpu, workload, stages):
+    """The distributed path at BASELINE sizes on one GPU (RCCL loopback,
+    tools/loop_check.py): C3 with one stage sends 1.6 GB per table, C5 ~7 GB
+    of S per stage -- messages past RCCL's ~1 GiB point-to-point limit
+    (profiles/r04/r04f/rccl_big.txt), so this exercises the piece cutting of
+    smj/dist.py (before it, C4 / C5 loopback joins were wrong).  The joined
+    rows of every step equal the single call's bit for bit (the single call
+    is oracle-checked at these sizes above and in test_gpu_msd.py)."""
+    import subprocess
+    import sys
+    from smj import _lib
+    _lib.load().smj_finalize()  # this process's scratch (the C4 test's ~50 GB) back to the device
+    torch.cuda.empty_cache()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SMJ_DIST_STAGES=str(stages))
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "loop_check.py"), "--workload", workload,
+                        "--steps", "2"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

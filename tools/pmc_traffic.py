@@ -41,8 +41,7 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"gen_uniform_kernel", "gen_uniform", True),
     (r"gen_zipf_kernel", "gen_zipf", True),
     (r"msd_part1_kernel", "partition_1pass", True),
-    (r"msd_big_res_kernel", "msd_big_dev", True),
-    (r"msd_big_stage_kernel", "msd_big_dev", False),
+    (r"msd_big_stage_kernel", "msd_big_dev", True),
     (r"msd_giant_\w+_kernel", "msd_big_dev", False),
     (r"msd_single_kernel", "msd_single", True),
 ]
