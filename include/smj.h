@@ -249,8 +249,9 @@ int smj_dev_partition_apply(const int64_t *in, int64_t n_rows, int col_num, int 
  * h_region[n_split + 1 + b] region b's capacity (rows; out must hold the last
  * region).  d_counts (DEVICE int64, n_split + 2 entries) gets the n_split + 1
  * exact bucket counts and d_counts[n_split + 1] = 0, or bit 0 set when a
- * bucket outgrew its region (its rows past the capacity were NOT written: the
- * caller re-partitions with plan / apply) / bit 1 when the decoupled
+ * bucket outgrew its region (that region's contents are then unspecified --
+ * nothing is written past it -- and the caller re-partitions with plan /
+ * apply; the counts stay exact) / bit 1 when the decoupled
  * look-back timed out (a bug).  Decoupled look-back over 4096-row tiles
  * (msd_part1_kernel); nothing synchronises; <= 64 buckets, 1..8 columns. */
 int smj_dev_partition_regions(const int64_t *in, int64_t n_rows, int col_num, int use_select, int select_col,
