@@ -61,6 +61,25 @@ _STAGES_ENV = os.environ.get("SMJ_DIST_STAGES")
 DEFAULT_STAGES = int(_STAGES_ENV) if _STAGES_ENV else None
 
 
+# Stage shares within a rank (SMJ_DIST_STAGE_FRAC, e.g. "0.35,0.65").  On one
+# GPU (loopback) the exchange is shorter than the pipeline, so a smaller first
+# stage starts the pipeline sooner while the larger second one is in flight
+# (exposed ~ X f0 + max(P f0, X (1 - f0)) + P (1 - f0), best at f0 = X / (X +
+# P) ~ 0.35 for X = 2.7, P = 5 ms); across GPUs the exchange dominates and the
+# stages stay equal.
+_FRAC_ENV = os.environ.get("SMJ_DIST_STAGE_FRAC")
+
+
+def stage_fracs(world, K):
+    if _FRAC_ENV:
+        f = [float(x) for x in _FRAC_ENV.split(",")]
+        if len(f) == K and all(x > 0 for x in f):
+            return f
+    if world == 1 and K == 2:
+        return [0.35, 0.65]
+    return None
+
+
 def default_stages(world):
     return DEFAULT_STAGES if DEFAULT_STAGES is not None else (2 if world == 1 else 4)
 # loopback: a rank's own segment also travels through the point-to-point
@@ -136,7 +155,16 @@ def _wire_device(t, group=None):
     return t.device
 
 
-def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None):
+def seg_fracs(world, K, frac=None):
+    """Cumulative fractions of the W*K - 1 segment boundaries: segment d*K + k
+    (rank d, stage k) holds frac[k] / W of the rows (frac: the stage shares
+    within a rank, equal by default)."""
+    frac = frac or [1.0 / K] * K
+    cum = [sum(frac[:k]) / sum(frac) for k in range(K)]
+    return [(d + cum[k]) / world for d in range(world) for k in range(K)][1:]
+
+
+def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None, fracs=None):
     """parts - 1 (default W - 1) sorted key splitters, identical on every rank,
     as a host list: one all_gather of every rank's sample (a fixed-size buffer,
     padded with INT64_MAX, plus its valid count), the sort and the order
@@ -164,7 +192,11 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
     L = allb[:, 0].sum()
     # the pads sort last (a real INT64_MAX key sorts among them: the same value)
     keys = torch.sort(allb[:, 1:].reshape(-1)).values
-    pos = (torch.arange(1, parts, dtype=torch.int64, device=dev) * L // parts - 1).clamp(min=0)
+    if fracs is None:
+        pos = (torch.arange(1, parts, dtype=torch.int64, device=dev) * L // parts - 1).clamp(min=0)
+    else:  # boundary i at the cumulative fraction fracs[i] of the sample
+        q = torch.tensor([int(round(f_ * (1 << 20))) for f_ in fracs], dtype=torch.int64, device=dev)
+        pos = (q * L // (1 << 20) - 1).clamp(min=0)
     got = torch.cat([keys[pos], L.view(1), buf[1:at]]).tolist()
     if own is not None:
         mine = got[parts:]
@@ -196,7 +228,7 @@ def bucket_bounds(spl):
     return s, single
 
 
-def choose_cuts(GR, GS, single, world):
+def choose_cuts(GR, GS, single, world, fracs=None):
     """W-1 cuts (bucket, occurrence) over the global bucket-ordered sequence,
     balancing R + S rows per rank: rows of buckets < b go left, and of bucket
     b the occurrences < o (o = 0 unless b is a single-key bucket).  The same
@@ -207,7 +239,7 @@ def choose_cuts(GR, GS, single, world):
     total = sum(tot)
     cuts, acc, b, prev = [], 0, 0, (0, 0)
     for d in range(1, world):
-        target = total * d / world
+        target = total * (fracs[d - 1] if fracs else d / world)
         while b < nb and acc + tot[b] <= target:
             acc += tot[b]
             b += 1
@@ -461,7 +493,9 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     tr = _Tracer(TRACE and R.is_cuda, rank)
 
     own = []
-    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own)  # host sync 1
+    fr = stage_fracs(world, K)
+    fracs = seg_fracs(world, K, fr) if fr else None
+    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own, fracs=fracs)  # sync 1
     tr("splitters")
     bounds, single = bucket_bounds(spl)
     nb = len(bounds) + 1
@@ -489,7 +523,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         regs.append(reg)
     del parts_
     G = [[sum(counts[t][r][b] for r in range(world)) for b in range(nb)] for t in range(2)]
-    cuts = choose_cuts(G[0], G[1], single, nseg)
+    cuts = choose_cuts(G[0], G[1], single, nseg, fracs)
     # every source rank's row ranges per segment, from the gathered counts
     sl = [[slice_ranges(counts[t][r], [sum(counts[t][q][b] for q in range(r)) for b in range(nb)], cuts, nb)
            for r in range(world)] for t in range(2)]

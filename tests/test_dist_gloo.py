@@ -196,6 +196,23 @@ def test_distributed_hip_eight_ranks_one_gpu(tmp_path, oracle_built, pkg_built, 
     _run_and_check(tmp_path, 8, kind, cfg, 800_000)
 
 
+def test_uneven_stage_shares(tmp_path, oracle_built, monkeypatch):
+    """Stage shares within a rank (SMJ_DIST_STAGE_FRAC): segment boundaries at
+    uneven cumulative fractions for the splitters and the cuts; the result is
+    the same rows in the same order."""
+    monkeypatch.setenv("SMJ_DIST_STAGE_FRAC", "1,3")
+    _run_and_check(tmp_path, 3, "uniform", {"select": (0, 100, 0, 20000), "keys": (0, 0), "samples": 64,
+                                             "stages": 2}, 30_000)
+
+
+def test_choose_cuts_fractions():
+    from smj import dist as sdist
+    # 8 equal single-row buckets; boundaries at 1/4 and 1/2 -> cuts at buckets 2 and 4
+    GR, GS = [1] * 8, [0] * 8
+    assert sdist.choose_cuts(GR, GS, [False] * 8, 3, [0.25, 0.5]) == [(2, 0), (4, 0)]
+    assert sdist.seg_fracs(2, 2, [1, 3]) == [0.125, 0.5, 0.625]
+
+
 def test_region_overflow_falls_back(tmp_path, oracle_built, monkeypatch):
     """Regions sized below the bucket counts (SMJ_DIST_REGION_SCALE): the
     overflowing ranks re-partition with plan / apply and the result is the
