@@ -62,11 +62,13 @@ DEFAULT_STAGES = int(_STAGES_ENV) if _STAGES_ENV else None
 
 
 # Stage shares within a rank (SMJ_DIST_STAGE_FRAC, e.g. "0.35,0.65").  On one
-# GPU (loopback) the exchange is shorter than the pipeline, so a smaller first
-# stage starts the pipeline sooner while the larger second one is in flight
-# (exposed ~ X f0 + max(P f0, X (1 - f0)) + P (1 - f0), best at f0 = X / (X +
-# P) ~ 0.35 for X = 2.7, P = 5 ms); across GPUs the exchange dominates and the
-# stages stay equal.
+# GPU (loopback) the exchange is shorter than the pipeline, so small first
+# stages start the pipeline sooner while the larger later ones are in flight
+# (two stages: exposed ~ X f0 + max(P f0, X (1 - f0)) + P (1 - f0), best at f0
+# = X / (X + P) ~ 0.35 for X = 2.7, P = 5 ms).  Measured on one box
+# (profiles/r04/r04i): 0.5/0.5 9.88-9.95 ms, 0.35/0.65 9.61-9.62, 0.25/0.75
+# 9.89-9.92, three stages 0.15/0.3/0.55 9.38-9.49 (the default there).  Across
+# GPUs the exchange dominates and the stages stay equal.
 _FRAC_ENV = os.environ.get("SMJ_DIST_STAGE_FRAC")
 
 
@@ -77,11 +79,13 @@ def stage_fracs(world, K):
             return f
     if world == 1 and K == 2:
         return [0.35, 0.65]
+    if world == 1 and K == 3:
+        return [0.15, 0.3, 0.55]
     return None
 
 
 def default_stages(world):
-    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (2 if world == 1 else 4)
+    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (3 if world == 1 else 4)
 # loopback: a rank's own segment also travels through the point-to-point
 # transport (send / receive to itself; RCCL only: gloo keeps the device copy)
 # instead of a device copy, and one rank runs the whole distributed path: the

@@ -345,12 +345,11 @@ def region_capacities(sample_keys, n, bounds, tile=4096, sigmas=8.0):
     standard deviations + one tile, capped at n (as msd_part1 sizes the
     partitioned mode's regions).  Returns (h_region list of 2 (nb) ints, rows
     the output buffer needs)."""
-    import bisect
+    import numpy as np
     nb = len(bounds) + 1
     m = len(sample_keys)
-    sc = [0] * nb
-    for k in sample_keys:
-        sc[bisect.bisect_left(bounds, k)] += 1
+    sc = np.bincount(np.searchsorted(np.asarray(bounds, dtype=np.int64), np.asarray(sample_keys, dtype=np.int64),
+                                     side="left"), minlength=nb).tolist() if m else [0] * nb
     starts, caps, at = [], [], 0
     for b in range(nb):
         if m == 0:
