@@ -347,6 +347,7 @@ def region_capacities(sample_keys, n, bounds, tile=4096, sigmas=8.0):
     the output buffer needs)."""
     import numpy as np
     nb = len(bounds) + 1
+    sample_keys = np.asarray(sample_keys, dtype=np.int64)
     m = len(sample_keys)
     sc = np.bincount(np.searchsorted(np.asarray(bounds, dtype=np.int64), np.asarray(sample_keys, dtype=np.int64),
                                      side="left"), minlength=nb).tolist() if m else [0] * nb
