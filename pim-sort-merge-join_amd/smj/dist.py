@@ -168,34 +168,43 @@ def seg_fracs(world, K, frac=None):
     return [(d + cum[k]) / world for d in range(world) for k in range(K)][1:]
 
 
-def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None, fracs=None):
+def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None, fracs=None,
+                     est=None):
     """parts - 1 (default W - 1) sorted key splitters, identical on every rank,
     as a host list: one all_gather of every rank's sample (a fixed-size buffer,
     padded with INT64_MAX, plus its valid count), the sort and the order
     statistics on the device, one device -> host copy of the result.  own (a
     list): gets this rank's sampled keys per table (host lists, from the same
-    copy) -- partition_regions sizes its regions from them."""
+    copy) -- partition_regions sizes its regions from them.  est (a dict):
+    gets every rank's sampled keys per table and its table rows (host), from
+    which any rank can estimate every bucket's global rows (estimate_counts)."""
     parts = parts or world
     home = tables_and_keys[0][0].device
     dev = _wire_device(tables_and_keys[0][0], group)
-    cap = len(tables_and_keys) * samples
-    # [count, keys..., INT64_MAX pads]: the sampled keys are gathered straight
+    nt = len(tables_and_keys)
+    cap = nt * samples
+    H = 1 + 2 * nt  # header: [total samples, samples per table..., rows per table...]
+    # [header, keys..., INT64_MAX pads]: the sampled keys are gathered straight
     # into their slice (on the wire device when the transport is gloo)
-    buf = torch.full((cap + 1,), INT64_MAX, dtype=torch.int64, device=home)
-    at = 1
-    for t, k in tables_and_keys:
+    buf = torch.full((cap + H,), INT64_MAX, dtype=torch.int64, device=home)
+    at = H
+    hdr = [0] * H
+    for x, (t, k) in enumerate(tables_and_keys):
         n = t.shape[0]
+        c = min(samples, n)
+        hdr[1 + x], hdr[1 + nt + x] = c, n
         if n:
             idx = sample_index(n, samples, t.device)
-            torch.index_select(t[:, k], 0, idx, out=buf[at: at + idx.numel()])
-            at += idx.numel()
-    buf[0] = at - 1
+            torch.index_select(t[:, k], 0, idx, out=buf[at: at + c])
+            at += c
+    hdr[0] = at - H
+    buf[:H] = torch.tensor(hdr, dtype=torch.int64).to(home, non_blocking=True)
     buf = buf.to(dev)
-    allb = torch.empty((world, cap + 1), dtype=torch.int64, device=dev)
+    allb = torch.empty((world, cap + H), dtype=torch.int64, device=dev)
     dist.all_gather(list(allb.unbind(0)), buf, group=group)  # rows of allb (gloo has no all_gather_into_tensor)
     L = allb[:, 0].sum()
     # the pads sort last (a real INT64_MAX key sorts among them: the same value)
-    keys = torch.sort(allb[:, 1:].reshape(-1)).values
+    keys = torch.sort(allb[:, H:].reshape(-1)).values
     if fracs is None:
         pos = (torch.arange(1, parts, dtype=torch.int64, device=dev) * L // parts - 1).clamp(min=0)
     else:  # boundary i at the cumulative fraction fracs[i] of the sample
@@ -203,16 +212,43 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
         pos = (q * L // (1 << 20) - 1).clamp(min=0)
     # one host copy, kept as a numpy array (a .tolist() of the ~8k sampled keys
     # cost ~0.3 ms of host time per step in the loopback trace, profiles/r04/r04j)
-    got = torch.cat([keys[pos], L.view(1), buf[1:at]]).cpu().numpy()
+    parts_ = [keys[pos], L.view(1), buf[H:at]]
+    if est is not None:
+        parts_.append(allb.reshape(-1))
+    got = torch.cat(parts_).cpu().numpy()
     if own is not None:
         o = parts
         for t, _ in tables_and_keys:
             c = min(samples, t.shape[0])
             own.append(got[o: o + c])
             o += c
+    if est is not None:
+        est["all"] = got[parts + (at - H):].reshape(world, cap + H)
+        est["H"], est["nt"] = H, nt
     if int(got[parts - 1]) == 0:
         return [0] * (parts - 1)
     return [int(x) for x in got[:parts - 1]]
+
+
+def estimate_counts(est, t, bounds):
+    """Global rows per bucket of table t estimated from every rank's sample
+    (each rank's samples of t weigh its rows / its sample count); identical on
+    every rank.  Rows a WHERE clause drops are counted too (the sample ignores
+    the select): an estimate for balancing cuts, never for correctness."""
+    import numpy as np
+    a, H, nt = est["all"], est["H"], est["nt"]
+    nb = len(bounds) + 1
+    tot = np.zeros(nb)
+    bnd = np.asarray(bounds, dtype=np.int64)
+    for r in range(a.shape[0]):
+        c = [int(a[r, 1 + x]) for x in range(nt)]
+        n = int(a[r, 1 + nt + t])
+        if c[t] == 0:
+            continue
+        o = H + sum(c[:t])
+        b = np.searchsorted(bnd, a[r, o: o + c[t]], side="left")
+        tot += np.bincount(b, minlength=nb) * (n / c[t])
+    return [int(round(v)) for v in tot]
 
 
 def bucket_bounds(spl):
@@ -492,46 +528,94 @@ def _repartition(ops, T, bounds, k, sc, sv):
     return ops.partition_apply(T, bounds, plan, k, sc, sv)
 
 
+_SIDE = {}
+
+
+class _HostGather:
+    """all_gather of a small int64 device vector (bucket counts + flag) whose
+    host copy waits for the collective only -- not for work enqueued on the
+    compute stream after it (the next table's partition).  Under gloo (CPU
+    wire) it is the synchronous gather_counts."""
+
+    def __init__(self, t, world, group):
+        dev = _wire_device(t, group)
+        self.res = None
+        if dev.type == "cpu":
+            self.res = gather_counts(t, world, group, dev)
+            return
+        self.outs = [torch.empty_like(t) for _ in range(world)]
+        work = dist.all_gather(self.outs, t, group=group, async_op=True)  # ordered after t's producer
+        side = _SIDE.get(t.device)
+        if side is None:
+            side = _SIDE[t.device] = torch.cuda.Stream(device=t.device)
+        with torch.cuda.stream(side):
+            work.wait()
+            self.host = torch.empty((world, t.numel()), dtype=t.dtype, pin_memory=True)
+            self.host.copy_(torch.stack(self.outs), non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record(side)
+
+    def result(self):
+        if self.res is None:
+            self.ev.synchronize()
+            self.res = self.host.tolist()
+            del self.outs
+        return self.res
+
+
 def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
     K = stage_count(world, default_stages(world) if stages is None else stages)
     nseg = world * K
     tr = _Tracer(TRACE and R.is_cuda, rank)
 
-    own = []
+    own, est = [], {}
     fr = stage_fracs(world, K)
     fracs = seg_fracs(world, K, fr) if fr else None
-    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own, fracs=fracs)  # sync 1
+    spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own, fracs=fracs,
+                           est=est)  # host sync 1
     tr("splitters")
     bounds, single = bucket_bounds(spl)
     nb = len(bounds) + 1
-    # both tables partitioned (one read each with partition_regions); their
-    # counts and overflow flags stay on the device until the one gather
     tabs = [(R, k1, sc1, sv1), (S, k2, sc2, sv2)]
-    cnt = torch.empty(2 * (nb + 1), dtype=torch.int64, device=R.device)
-    parts_ = [_partition(ops, T, bounds, cnt[t * (nb + 1):(t + 1) * (nb + 1)], own[t], k, sc, sv)
-              for t, (T, k, sc, sv) in enumerate(tabs)]
-    allc = gather_counts(cnt, world, group, _wire_device(R, group))  # host sync 2
-    tr("partition R + S + counts")
-    counts = [[allc[r][t * (nb + 1): t * (nb + 1) + nb] for r in range(world)] for t in range(2)]
     wire = _wire_device(R, group)
-    sends, regs = [], []
-    for t in range(2):
-        buf, reg = parts_[t]
-        if reg is not None and allc[rank][t * (nb + 1) + nb]:  # a region overflowed: the counting partition
+    # R partitioned (one read), its counts gathered -- the host copy waits for
+    # that gather only -- while S is partitioned behind it on the compute
+    # stream; the cuts come from R's exact counts and S's sample estimate (any
+    # (bucket, occurrence) cut is valid: R and S apply the same one), so R's
+    # first stage leaves before S's partition has finished (round 4; before,
+    # nothing left until both tables were counted)
+    cnt = [torch.empty(nb + 1, dtype=torch.int64, device=R.device) for _ in range(2)]
+    part = [_partition(ops, R, bounds, cnt[0], own[0], k1, sc1, sv1)]
+    gR = _HostGather(cnt[0], world, group)
+    part.append(_partition(ops, S, bounds, cnt[1], own[1], k2, sc2, sv2))
+    gS = _HostGather(cnt[1], world, group)
+    counts, sends, regs, sl = [None, None], [None, None], [None, None], [None, None]
+
+    def finish(t, allc):  # this table's exact counts: overflow fix-up, send buffer, row ranges
+        counts[t] = [allc[r][:nb] for r in range(world)]
+        buf, reg = part[t]
+        if reg is not None and allc[rank][nb]:  # a region overflowed: the counting partition
             T, k, sc, sv = tabs[t]
             buf, reg = _repartition(ops, T, bounds, k, sc, sv), None
         if reg is None:  # bucket-contiguous
             reg = [sum(counts[t][rank][:b]) for b in range(nb)]
         end = max([reg[b] + counts[t][rank][b] for b in range(nb)] + [0])
-        # only the rows the regions hold go to the wire (under gloo: a host copy)
-        sends.append(buf[:end].to(wire))
-        regs.append(reg)
-    del parts_
-    G = [[sum(counts[t][r][b] for r in range(world)) for b in range(nb)] for t in range(2)]
-    cuts = choose_cuts(G[0], G[1], single, nseg, fracs)
-    # every source rank's row ranges per segment, from the gathered counts
-    sl = [[slice_ranges(counts[t][r], [sum(counts[t][q][b] for q in range(r)) for b in range(nb)], cuts, nb)
-           for r in range(world)] for t in range(2)]
+        sends[t] = buf[:end].to(wire)  # only the rows the regions hold (under gloo: a host copy)
+        regs[t] = reg
+        part[t] = None
+        sl[t] = [slice_ranges(counts[t][r], [sum(counts[t][q][b] for q in range(r)) for b in range(nb)], cuts, nb)
+                 for r in range(world)]
+
+    allcR = gR.result()  # host sync 2 (R's counts)
+    tr("partition R + counts")
+    GR = [sum(allcR[r][b] for r in range(world)) for b in range(nb)]
+    GSe = estimate_counts(est, 1, bounds)
+    cuts = choose_cuts(GR, GSe, single, nseg, fracs)
+    finish(0, allcR)
+    pending = [post_stage(0, K, [sends[0], None], regs, sl, rank, world, R.device, group, loopback)]  # R's stage 0
+    finish(1, gS.result())  # host sync 3 (S's counts)
+    tr("partition S + counts; R stage 0 posted")
+    pending.append(post_stage(0, K, [None, sends[1]], regs, sl, rank, world, R.device, group, loopback))
     seg = [[[sum(hi - lo for (_, lo, hi) in sl[t][r][j]) for j in range(nseg)] for r in range(world)]
            for t in range(2)]
     rows_in = [sum(seg[t][r][rank * K + k] for r in range(world) for k in range(K)) for t in range(2)]
@@ -539,7 +623,6 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
                     sum(seg[1][r][rank * K + k] for r in range(world))) for k in range(K))
     into = getattr(ops, "writes_into", False)
     ncols = R.shape[1] + S.shape[1] - 1
-    pending = [post_stage(0, K, sends, regs, sl, rank, world, R.device, group, loopback)]
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
     tr("stage 0 posted")
