@@ -191,7 +191,7 @@ def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, ki
 ])
 def test_distributed_hip_eight_ranks_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
     """The bench's N = 8 configuration (8 ranks, the default stage count:
-    W K - 1 = 15 splitters, 2 stages per rank) on the product operators, the
+    W K - 1 = 31 splitters, 4 stages per rank) on the product operators, the
     8 ranks sharing cuda:0 and the exchange staged through gloo."""
     _run_and_check(tmp_path, 8, kind, cfg, 800_000)
 
