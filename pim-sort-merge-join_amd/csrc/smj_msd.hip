@@ -436,6 +436,9 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
 // The look-back never waits on a later ticket, so the grid always drains; a
 // wait over 2^24 polls (a bug) sets flags[2].
 constexpr uint64_t kP1Agg = 1ull << 62, kP1Inc = 2ull << 62, kP1Val = (1ull << 62) - 1;
+#ifndef SMJ_P1_ABL
+#define SMJ_P1_ABL 0
+#endif
 
 template <int COLS>
 __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_kernel(const MsdPart1Params p) {
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_
     if (wave == 0) {
         const uint32_t cnt = lane < nb ? s_bin[lane + 1] - s_bin[lane] : 0u;
         unsigned long long *st = p.status + t * nb;
-        if (t > 0) {
+        if (t > 0 && !SMJ_P1_ABL) {  // (SMJ_P1_ABL: timing ablation, no look-back -- every tile at its part's start)
             if (lane < nb) atomicExch(&st[lane], kP1Agg | cnt);
             // (one predecessor per lane with all its part words -- 64 tiles per
             // round trip -- was slower: C4 partition 19.4 vs 14.4 ms, its 7x
