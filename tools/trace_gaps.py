@@ -1,31 +1,51 @@
-"""GPU idle time from a rocprofv3 kernel trace: the union of the kernel
-intervals against the wall span, and the largest gaps with the kernels around
-them (what ran before / after each idle period).
+"""GPU idle gaps in a rocprofv3 kernel trace (…_kernel_trace.csv).
 
-    python tools/trace_gaps.py gpurun_out/<tag>/tr/<name>_kernel_trace.csv [t0_ms t1_ms]"""
+    python tools/trace_gaps.py TRACE.csv [--top 25] [--from-kernel NAME]
+
+Prints the union of kernel busy time against the wall span of the trace
+(from the first launch of --from-kernel, if given), the busy time per kernel
+name, and the largest idle gaps with the kernels on either side: where a
+step's time goes outside any kernel (host synchronisations, launch gaps).
+"""
+import argparse
 import csv
-import sys
+from collections import defaultdict
 
 
 def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-    base = ev[0][0]
-    if len(sys.argv) > 3:
-        lo, hi = base + float(sys.argv[2]) * 1e6, base + float(sys.argv[3]) * 1e6
-        ev = [e for e in ev if e[0] >= lo and e[1] <= hi]
-    busy, gaps, end, prev = 0, [], ev[0][0], None
-    for s, e, n in ev:
-        if s > end:
-            gaps.append((s - end, end, prev, n))
-        busy += max(0, e - max(s, end))
-        end = max(end, e)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--from-kernel", default=None)
+    a = ap.parse_args()
+    rows = []
+    with open(a.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][:60]))
+    rows.sort()
+    if a.from_kernel:
+        i0 = next(i for i, r in enumerate(rows) if a.from_kernel in r[2])
+        rows = rows[i0:]
+    busy, gaps, per = 0, [], defaultdict(float)
+    cur_s, cur_e, prev = rows[0][0], rows[0][1], rows[0][2]
+    for s, e, n in rows:
+        per[n] += (e - s) / 1e6
+        if s > cur_e:
+            busy += cur_e - cur_s
+            gaps.append(((s - cur_e) / 1e6, prev, n, (cur_e - rows[0][0]) / 1e6))
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
         prev = n
-    wall = end - ev[0][0]
-    print(f"span {wall / 1e6:.3f} ms, GPU busy {busy / 1e6:.3f} ms ({busy / wall:.1%}), idle {sum(g[0] for g in gaps) / 1e6:.3f} ms "
-          f"in {len(gaps)} gaps")
-    for g, at, a, b in sorted(gaps, reverse=True)[:15]:
-        print(f"  {g / 1e3:8.1f} us at {(at - base) / 1e6:9.3f} ms: after {a[:50]} | before {b[:50]}")
+    busy += cur_e - cur_s
+    wall = (rows[-1][1] - rows[0][0]) / 1e6
+    print(f"kernels {len(rows)}  wall {wall:.3f} ms  busy {busy / 1e6:.3f} ms  idle {wall - busy / 1e6:.3f} ms")
+    print("busy per kernel (ms, overlaps counted per kernel):")
+    for n, t in sorted(per.items(), key=lambda kv: -kv[1])[:20]:
+        print(f"  {t:9.3f}  {n}")
+    print(f"largest idle gaps (ms, after -> before, at ms):")
+    for g, p, n, at in sorted(gaps, reverse=True)[: a.top]:
+        print(f"  {g:8.3f}  {p} -> {n}  @{at:.3f}")
 
 
 if __name__ == "__main__":
