@@ -31,6 +31,10 @@ run() {  # name timeout cmd...   (rc 1 tolerated: a bench step's stderr is read 
   local rc=$?
   echo "[$(date +%T)] $name rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" | tee -a "$OUT/steps.log"; exit $rc; fi
+  # a GPU fault inside a Python step surfaces as an exception (rc 1): stop there too
+  if [ $rc -ne 0 ] && grep -qE "HSA_STATUS_ERROR|Memory access fault|hardware exception|unspecified launch failure|hipErrorLaunchFailure|page not present" "$OUT/$name.err"; then
+    echo "stopping after $name (GPU fault in stderr)" | tee -a "$OUT/steps.log"; exit 3
+  fi
   return $rc
 }
 test_run() {  # a pytest step: stop on any failure
@@ -67,6 +71,14 @@ for s in $STEPS; do
     proflp) run proflp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflp" -o loop -- \
                python3 "$ROOT/bench.py" --loopback --steps 5 --warmup 2 $NOCPU
            rm -f "$OUT/proflp/loop_kernel_trace.csv" ;;
+    tr5)   run tr5 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr5" -o c5 -- \
+               python3 "$ROOT/bench.py" --workload c5 --steps 2 --warmup 1 $NOCPU
+           python3 tools/trace_gaps.py "$OUT/tr5/c5_kernel_trace.csv" --from-kernel msd_sample --top 30 --per msd_part_sample > "$OUT/tr5_gaps.txt" ;;
+    tr4)   run tr4 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr4" -o c4 -- \
+               python3 "$ROOT/bench.py" --workload c4 --steps 2 --warmup 1 $NOCPU
+           python3 tools/trace_gaps.py "$OUT/tr4/c4_kernel_trace.csv" --from-kernel msd_sample --top 30 --per msd_part_sample > "$OUT/tr4_gaps.txt" ;;
+    p1)    run p1_base 300 python tools/p1_probe.py && \
+           SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/p1abl/libsmj_hip.so run p1_abl 300 python tools/p1_probe.py ;;
     pmcf)  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmcw)  run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \

@@ -29,7 +29,7 @@ def timed(fn, reps=5):
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_000_000_000
 T = ops.gen_uniform(n, seed=1, key_range=3 * n)
-sample = T[:, 0][torch.linspace(0, n - 1, 8192).long()].cpu().numpy()
+sample = T[:, 0][torch.arange(8192, device=T.device) * (n // 8192)].cpu().numpy()  # integer indices: in bounds
 bounds = [int(x) for x in np.quantile(sample, np.arange(1, 7) / 7.0)]
 reg, need = ops.region_capacities(sample, n, bounds)
 out = torch.empty((need, 2), dtype=torch.int64, device="cuda")

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--from-kernel", default=None)
+    ap.add_argument("--per", default=None, help="also split the trace into windows at each launch of this kernel")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -46,6 +47,24 @@ def main():
     print(f"largest idle gaps (ms, after -> before, at ms):")
     for g, p, n, at in sorted(gaps, reverse=True)[: a.top]:
         print(f"  {g:8.3f}  {p} -> {n}  @{at:.3f}")
+    if a.per:
+        # per window (from one launch of --per to the next): idle time, and the
+        # idle summed per (kernel before, kernel after) pair over all windows
+        starts = [r[0] for r in rows if a.per in r[2]] + [rows[-1][1] + 1]
+        t0 = rows[0][0]
+        pairs = defaultdict(lambda: [0.0, 0])
+        print(f"windows at {a.per}: start ms, wall ms, idle ms")
+        for w0, w1 in zip(starts[:-1], starts[1:]):
+            gs = [g for g in gaps if w0 <= t0 + g[3] * 1e6 < w1]
+            idle = sum(g[0] for g in gs)
+            last = max(r[1] for r in rows if w0 <= r[0] < w1)
+            print(f"  {(w0 - t0) / 1e6:9.3f}  {(last - w0) / 1e6:8.3f}  {idle:7.3f}")
+            for g in gs:
+                pairs[(g[1], g[2])][0] += g[0]
+                pairs[(g[1], g[2])][1] += 1
+        print("idle per kernel pair over the windows (ms, gaps):")
+        for (p, n), (t, c) in sorted(pairs.items(), key=lambda kv: -kv[1][0])[:20]:
+            print(f"  {t:8.3f} {c:5d}  {p} -> {n}")
 
 
 if __name__ == "__main__":
