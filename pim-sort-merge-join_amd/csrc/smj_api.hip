@@ -509,8 +509,13 @@ struct MsdScratch {
     size_t c_p1st = 0;
     int64_t *p1d = nullptr;             // device [2][kP1Words]: oc[128], tot[64], flags[4] (u32 x 8) per table
     int64_t *p1h = nullptr;             // pinned twin
+    uint32_t *p1c = nullptr;            // chunked partition: device [2][kP1cWords]: rows per (chunk, part), flags
+    uint32_t *h_p1c = nullptr;          // pinned twin
+    void *p1desc[2] = {nullptr, nullptr};  // its parts' part_a tile descriptors per table
+    size_t c_p1desc[2] = {0, 0};
 };
 constexpr int kP1Words = 128 + 64 + 4;
+constexpr int kP1cWords = 1024 * 64 + 64;  // [chunk][64] rows, then flags
 std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
 int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
@@ -558,6 +563,8 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 64));
         HIP_TRY(hipMalloc(&m.p1d, sizeof(int64_t) * 2 * kP1Words));
         HIP_TRY(hipHostMalloc(&m.p1h, sizeof(int64_t) * 2 * kP1Words, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&m.p1c, sizeof(uint32_t) * 2 * kP1cWords));
+        HIP_TRY(hipHostMalloc(&m.h_p1c, sizeof(uint32_t) * 2 * kP1cWords, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
         m.dev = dev;  // only once every buffer exists (a failed call retries the allocation)
@@ -576,9 +583,11 @@ void msd_free_all() {
                 hipFree(p);
         for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                         (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
-                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick})
+                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
+                        (void *)m.p1c, m.p1desc[0], m.p1desc[1]})
             hipFree(p);
         hipHostFree(m.p1h);
+        hipHostFree(m.h_p1c);
         hipHostFree(m.h_pick);
         hipHostFree(m.h_work);
         hipHostFree(m.h_plan);
@@ -593,6 +602,8 @@ struct MsdIn {            // one input table of the pipeline
     int cols, use_sel, sel_col, key;
     T sel_val;
     T *out;               // sorted selected rows
+    const uint64_t *desc = nullptr;  // a chunked part (msd_part1c): its pass-A tiles' rows in src (MsdPartAParams::desc)
+    int64_t ntiles = 0;
 };
 
 // Records the index of the last profiling record (to patch its byte count
@@ -894,10 +905,10 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
         MsdTabScratch &ts = ms->t[x];
         T_[x] = msd_tile_a(t.cols);
         TB_[x] = msd_tile_b(t.cols);
-        tilesA[x] = (t.n + T_[x] - 1) / T_[x];
+        tilesA[x] = t.desc ? t.ntiles : (t.n + T_[x] - 1) / T_[x];
         maxB[x] = (t.n + TB_[x] - 1) / TB_[x] + kBucketsA;  // every bucket adds <= 1 partial pass-B tile
         const size_t W = (size_t)t.cols * 8;
-        SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, std::max<size_t>(1, t.n) * W));
+        SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, (size_t)std::max<int64_t>(1, std::max(t.n, tilesA[x] * T_[x])) * W));
         SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * TB_[x] * W));
         SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsARow * 4));
         SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
@@ -919,7 +930,8 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     {
         MsdSampleParams sp{};
         for (int x = 0; x < ntab; x++)
-            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val};
+            sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val,
+                                 in[x].desc, in[x].ntiles, T_[x]};
         sp.ntab = ntab;
         sp.spl = ms->spl;
         sp.samp = ms->samp;
@@ -944,7 +956,9 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     MsdPartAParams pp[2];
     for (int x = 0; x < ntab; x++)
         pp[x] = MsdPartAParams{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
-                               (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm};
+                               (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm,
+                               in[x].desc, in[x].ntiles};
+    if (stg && (in[0].desc || (ntab > 1 && in[1].desc))) return SMJ_ERR_INVALID;  // (staged input is contiguous)
     // both tables in one launch when nothing is staged and the widths agree (no tail between them)
     const bool pa_fused = !stg && ntab == 2 && in[0].cols == in[1].cols;
     if (pa_fused) {
@@ -1212,6 +1226,123 @@ void msd_part1_release(MsdScratch *ms) {
     if (ms->p1st) hipFree(ms->p1st);
     ms->p1st = nullptr;
     ms->c_p1st = 0;
+    for (int x = 0; x < 2; x++) {
+        if (ms->p1desc[x]) hipFree(ms->p1desc[x]);
+        ms->p1desc[x] = nullptr;
+        ms->c_p1desc[x] = 0;
+    }
+}
+
+// The chunked one-pass partition (msd_part1c_kernel, no look-back; SMJ_PART1C=0
+// keeps the look-back partition).  Chunk g of G takes K consecutive tiles; part
+// b's sub-region per chunk holds the chunk's estimated share of it (the key
+// sample's fraction f of the chunk's rows), plus 8 standard deviations of the
+// sample's estimate of f and 8 of the chunk's own binomial count, plus a tile.
+// *staged = false when a sub-region overflowed (input clustered by key; the
+// caller then runs the look-back partition).  On success part b of table x
+// is the rows at the descriptors (*desc)[x][b] (ntl[x][b] tiles of part_a's
+// tile rows) into ms->pst[x]; cnt[x][b] its rows.
+int msd_part1c(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64_t> &spl, std::vector<int64_t> *cnt,
+               std::vector<const uint64_t *> *desc, std::vector<int64_t> *ntl, bool *staged, hipStream_t s) {
+    static const bool on = [] {
+        const char *e = getenv("SMJ_PART1C");
+        return !(e && e[0] == '0');
+    }();
+    *staged = false;
+    if (!on) return SMJ_OK;
+    const int nspl = (int)spl.size(), nb = nspl + 1;
+    int G[2] = {0, 0};
+    int64_t K[2] = {0, 0};
+    std::vector<int64_t> dbase[2];
+    for (int x = 0; x < ntab; x++) {
+        cnt[x].assign(nb, 0);
+        ntl[x].assign(nb, 0);
+        desc[x].assign(nb, nullptr);
+        if (in[x].n == 0) continue;
+        const int64_t tile = p1_tile(in[x].cols), nt = (in[x].n + tile - 1) / tile, Ta = msd_tile_a(in[x].cols);
+        const int gmax = msd_part1c_grid(in[x].cols);
+        if (gmax < 1) return SMJ_OK;
+        K[x] = (nt + gmax - 1) / gmax;
+        G[x] = (int)((nt + K[x] - 1) / K[x]);
+        const double R = (double)(K[x] * tile);  // rows per chunk (the last one fewer)
+        const int64_t m = std::min<int64_t>(in[x].n, kSampleMax);
+        std::vector<int64_t> sc(nb, 0);
+        for (int64_t j = 0; j < m; j++) {
+            const int64_t k = ms->h_samp[x * kSampleMax + j];
+            if (k == INT64_MAX) continue;
+            sc[std::lower_bound(spl.begin(), spl.end(), k) - spl.begin()]++;
+        }
+        const char *cs = getenv("SMJ_PART1_CAP");  // tests: scaled-down sub-regions force the fallback
+        const double scale = cs ? atof(cs) : 1.0;
+        P1cWords w{};
+        P1cDesc d{};
+        dbase[x].assign(nb + 1, 0);
+        int64_t at = 0;
+        for (int b = 0; b < nb; b++) {
+            const double f = (double)sc[b] / (double)m;
+            const double est = f * R + 8.0 * R * std::sqrt(f * (1.0 - f) / (double)m + 1.0 / ((double)m * m)) +
+                               8.0 * std::sqrt(R * f * (1.0 - f) + 1.0);
+            const int64_t cap = std::min<int64_t>((int64_t)R, (int64_t)(est * scale) + (scale < 1.0 ? 0 : tile));
+            w.v[b] = d.st[b] = at;
+            w.v[64 + b] = d.cap[b] = cap;
+            at += (int64_t)G[x] * cap;
+            d.dbase[b] = dbase[x][b];
+            dbase[x][b + 1] = dbase[x][b] + (int64_t)G[x] * ((cap + Ta - 1) / Ta);
+        }
+        for (int b = 0; b < nspl; b++) w.v[128 + b] = spl[b];
+        if (grow(&ms->pst[x], &ms->c_pst[x], (size_t)std::max<int64_t>(1, at) * in[x].cols * sizeof(T)) != SMJ_OK ||
+            grow(&ms->p1desc[x], &ms->c_p1desc[x], (size_t)std::max<int64_t>(1, dbase[x][nb]) * 8) != SMJ_OK) {
+            (void)hipGetLastError();
+            msd_part1_release(ms);
+            return SMJ_OK;  // the counting partition (with all of it free) or the look-back one runs
+        }
+        uint32_t *c = ms->p1c + (size_t)x * kP1cWords;
+        HIP_TRY(hipMemsetAsync(c + 1024 * 64, 0, 64 * sizeof(uint32_t), s));
+        MsdPart1cParams p{};
+        p.src = in[x].src;
+        p.n = in[x].n;
+        p.use_sel = in[x].use_sel;
+        p.sel_col = in[x].sel_col;
+        p.key_col = in[x].key;
+        p.nspl = nspl;
+        p.sel_val = in[x].sel_val;
+        p.dst = (int64_t *)ms->pst[x];
+        p.cnt = c;
+        p.flags = c + 1024 * 64;
+        p.ntiles = nt;
+        p.chunk = K[x];
+        {
+            ProfScope ps("partition_1pass", 16.0 * in[x].cols * in[x].n, s);
+            HIP_TRY(launch_msd_part1c(p, w, in[x].cols, G[x], s));
+        }
+        HIP_TRY(launch_p1c_desc(c, G[x], nb, (int)Ta, d, (uint64_t *)ms->p1desc[x], s));
+    }
+    for (int x = 0; x < ntab; x++) {
+        if (in[x].n == 0) continue;
+        const size_t off = (size_t)x * kP1cWords;
+        HIP_TRY(hipMemcpyAsync(ms->h_p1c + off, ms->p1c + off, sizeof(uint32_t) * (size_t)G[x] * 64, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ms->h_p1c + off + 1024 * 64, ms->p1c + off + 1024 * 64, sizeof(uint32_t) * 4,
+                               hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int x = 0; x < ntab; x++) {
+        if (in[x].n == 0) continue;
+        const uint32_t *h = ms->h_p1c + (size_t)x * kP1cWords;
+        if (h[1024 * 64 + 1]) {
+            if (getenv("SMJ_DEBUG_PART1")) fprintf(stderr, "smj: chunked partition overflowed a sub-region\n");
+            return SMJ_OK;  // *staged = false
+        }
+        const int64_t Ta = msd_tile_a(in[x].cols);
+        for (int g = 0; g < G[x]; g++)
+            for (int b = 0; b < nb; b++) {
+                const int64_t c = h[(size_t)g * 64 + b];
+                cnt[x][b] += c;
+                ntl[x][b] += (c + Ta - 1) / Ta;
+            }
+        for (int b = 0; b < nb; b++) desc[x][b] = (const uint64_t *)ms->p1desc[x] + dbase[x][b];
+    }
+    *staged = true;
+    return SMJ_OK;
 }
 
 // Region capacities from the key sample (ms->h_samp: table x's sampled keys at
@@ -1360,17 +1491,22 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     // from its region to its place in the output), or -- when a region would
     // overflow, or SMJ_PART1=0 -- counted, then scattered straight into the
     // output buffer (smj_dev_partition; the parts are then sorted in place)
-    std::vector<int64_t> cnt[2], off[2], roff[2];
-    bool staged = false;
-    if (msd_part1_on(in, ntab)) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
+    std::vector<int64_t> cnt[2], off[2], roff[2], ntl[2];
+    std::vector<const uint64_t *> desc[2];
+    bool staged = false, chunked = false;
+    if (msd_part1_on(in, ntab)) {
+        SMJ_TRY(msd_part1c(ms, in, ntab, spl, cnt, desc, ntl, &chunked, s));
+        if (!chunked) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
+    }
     if (getenv("SMJ_DEBUG_PART1")) {
         fprintf(stderr, "smj: partitioned mode: %lld x %lld rows, %d parts (%zu weighted samples), %s; splitters", (long long)in[0].n,
-                (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, kw.size(), staged ? "one-pass regions" : "counting partition");
+                (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, kw.size(),
+                chunked ? "chunked one-pass" : staged ? "one-pass regions" : "counting partition");
         for (int64_t k : spl) fprintf(stderr, " %lld", (long long)k);
         fprintf(stderr, "\n");
     }
     for (int x = 0; x < ntab; x++) {
-        if (!staged) {
+        if (!staged && !chunked) {
             cnt[x].assign(nspl + 1, 0);
             if (in[x].n)
                 SMJ_TRY(smj_dev_partition(in[x].src, in[x].n, in[x].cols, in[x].use_sel, in[x].sel_col,
@@ -1389,6 +1525,11 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         for (int x = 0; x < ntab; x++) {
             if (cnt[x][p] == 0) continue;
             T *base = in[x].out + off[x][p] * in[x].cols;
+            if (chunked) {  // the part's tiles through its descriptors into the staging buffer
+                part[np++] = MsdIn{(const T *)ms->pst[x], cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base, desc[x][p],
+                                   ntl[x][p]};
+                continue;
+            }
             const T *src = staged ? (const T *)ms->pst[x] + roff[x][p] * in[x].cols : base;
             part[np++] = MsdIn{src, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
         }

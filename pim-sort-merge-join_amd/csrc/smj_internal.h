@@ -236,6 +236,9 @@ struct MsdTable {        // an input table as the sampler and part_a see it
     int64_t n;
     int cols, key_col, use_sel, sel_col;
     int64_t sel_val;
+    const uint64_t *desc = nullptr;  // a chunked part's tile descriptors (MsdPartAParams::desc), ntiles of tile rows
+    int64_t ntiles = 0;
+    int tile = 0;
 };
 struct MsdSampleParams {
     MsdTable tab[2];
@@ -252,6 +255,11 @@ struct MsdPartAParams {
     int64_t *out;        // tempA: tile t's rows at [t*T, t*T + m_t)
     uint32_t *offs;      // [tiles][kOffsARow]
     int64_t *tmm;        // [tiles][2] min / max selected key
+    // a part of the chunked partition (msd_part1c_kernel): tile t's rows are
+    // desc[t] >> 16 (a row of src) and the desc[t] & 0xffff rows after it, in
+    // order; ntiles tiles.  nullptr: tile t = rows [t T, t T + T) of src
+    const uint64_t *desc = nullptr;
+    int64_t ntiles = 0;
 };
 struct MsdPartA2 {       // one part_a launch over up to two tables
     MsdPartAParams t[2];
@@ -406,6 +414,34 @@ struct MsdPart1Params {
     int64_t ntiles;
 };
 hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s);
+// The chunked one-pass partition (msd_part1c_kernel): no look-back.  A
+// persistent grid of G workgroups; workgroup g takes the consecutive tiles
+// [g K, g K + K) in order and appends part b's rows to its own sub-region
+// [st[b] + g cap[b], + cap[b]) of the staging buffer, so part b = the G
+// sub-regions' filled prefixes in g order (input order).  cnt[g * 64 + b] =
+// the rows it wrote there; flags[1] = a sub-region overflowed.  The part's
+// tile descriptors for part_a then come from msd_p1c_desc_kernel.
+struct P1cWords {  // sub-region starts of part b [0, 64) and per-chunk capacities [64, 128), rows; splitters [128, 192)
+    int64_t v[192];
+};
+struct MsdPart1cParams {
+    const int64_t *src;
+    int64_t n;
+    int use_sel, sel_col, key_col, nspl;
+    int64_t sel_val;
+    int64_t *dst;
+    uint32_t *cnt;               // [G][64] rows per (chunk, part)
+    uint32_t *flags;             // [1]: a sub-region overflowed (zeroed by the caller)
+    int64_t ntiles, chunk;       // p1_tile rows per tile; tiles per workgroup
+};
+hipError_t launch_msd_part1c(const MsdPart1cParams &p, const P1cWords &w, int cols, int grid, hipStream_t s);
+int msd_part1c_grid(int cols);   // resident workgroups of the chunked partition (G)
+// part b's part_a tile descriptors at desc + dbase[b]: chunk g's rows in tiles
+// of tile rows (the last one partial), chunks in order
+struct P1cDesc {
+    int64_t st[64], cap[64], dbase[64];
+};
+hipError_t launch_p1c_desc(const uint32_t *cnt, int G, int nb, int tile, const P1cDesc &d, uint64_t *desc, hipStream_t s);
 struct P1Words {  // region starts [0, 64) and capacities [64, 128), rows; splitters [128, 192)
     int64_t v[192];
 };

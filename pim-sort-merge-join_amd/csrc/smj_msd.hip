@@ -258,10 +258,14 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
     uint32_t valid = 0;
     if (x < p.ntab && t.n > 0 && jj < min(t.n, (int64_t)kSampleMax)) {
         constexpr int kSampleRun = 16, kClusters = kSampleMax / kSampleRun;
-        const int64_t r = t.n <= kSampleMax
-                              ? jj
-                              : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
-                                                 jj % kSampleRun);
+        int64_t r = t.n <= kSampleMax
+                        ? jj
+                        : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
+                                           jj % kSampleRun);
+        if (t.desc) {  // a chunked part: row r of tile r / tile (clamped to the tile's rows) -- any row of it samples
+            const uint64_t d = t.desc[min(t.ntiles - 1, r / t.tile)];
+            r = (int64_t)(d >> 16) + min(r % t.tile, (int64_t)(d & 0xffffu) - 1);
+        }
         const int64_t *row = t.src + r * t.cols;
         const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
         if (!t.use_sel || sv > t.sel_val) {
@@ -361,7 +365,15 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t t = (int64_t)p.tile0 + bx, row0 = t * T;
-    const int nrows = (int)min((int64_t)T, p.n - row0);
+    int64_t rs = row0;  // first input row of the tile (a chunked part: its descriptor)
+    int nrows;
+    if (p.desc) {
+        const uint64_t d = p.desc[t];
+        rs = (int64_t)(d >> 16);
+        nrows = (int)(d & 0xffffu);
+    } else {
+        nrows = (int)min((int64_t)T, p.n - row0);
+    }
     uint32_t *wc = s_wcnt + wave * RADIX;
     if (tid < kSplA) s_spl[tid] = p.spl[tid];
     zero_counters<RADIX>(wc, lane);
@@ -369,8 +381,8 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
     int64_t rows[ITEMS][COLS];
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
-        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
-        else load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        else load_row<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
     __syncthreads();  // splitters
 
     uint32_t dig[ITEMS];
@@ -500,7 +512,7 @@ __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_
     if (wave == 0) {
         const uint32_t cnt = lane < nb ? s_bin[lane + 1] - s_bin[lane] : 0u;
         unsigned long long *st = p.status + t * nb;
-        if (t > 0 && !SMJ_P1_ABL) {  // (SMJ_P1_ABL: timing ablation, no look-back -- every tile at its part's start)
+        if (t > 0 && !SMJ_P1_ABL) {  // (SMJ_P1_ABL: timing ablation, no look-back -- tile t at t x its share of the region)
             if (lane < nb) atomicExch(&st[lane], kP1Agg | cnt);
             // (one predecessor per lane with all its part words -- 64 tiles per
             // round trip -- was slower: C4 partition 19.4 vs 14.4 ms, its 7x
@@ -542,6 +554,10 @@ __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_
                 if (__ballot(lv && !done) == 0ull) break;
             }
         }
+        if (SMJ_P1_ABL && lane < nb) {  // distinct rows per tile (its share of the region), clamped into it
+            const uint64_t cap = (uint64_t)p.oc[64 + lane], per = cap / (uint64_t)p.ntiles;
+            s_acc[lane] = min((uint64_t)t * per, cap - min(cap, (uint64_t)cnt));
+        }
         if (lane < nb) {
             const uint64_t ex = s_acc[lane];
             atomicExch(&st[lane], kP1Inc | (ex + cnt));
@@ -574,6 +590,141 @@ __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// part1c: the chunked one-pass partition (no look-back; smj_internal.h)
+// ---------------------------------------------------------------------------
+// The look-back of msd_part1_kernel costs ~1.9 ms per 1e9-row table
+// (tools/p1_probe.py: 7.2 ms with it, 5.3 ms for the same kernel writing each
+// tile at a fixed share of its region without it).  Here no tile waits on
+// another: workgroup g walks its own chunk of consecutive tiles in order and
+// keeps a running cursor per part, so its rows of part b land contiguous and
+// in input order in its sub-region; a part is the chunks' sub-regions in g
+// order.  The next tile's rows are loaded while the current one is ranked,
+// staged and stored.  Sub-regions are sized from the key sample (their
+// per-chunk share plus 8 sigma plus a tile); an overflow only sets flags[1]
+// (the caller then runs the look-back partition).
+#ifndef SMJ_P1C_PF
+#define SMJ_P1C_PF 0  // A/B switch: the next tile's rows loaded while this one is placed (+32 VGPRs: spills at 128)
+#endif
+template <int COLS>
+__global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1c_kernel(const MsdPart1cParams p,
+                                                                                        const P1cWords w) {
+    constexpr int ITEMS = p1_items(COLS), T = p1_tile(COLS), RADIX = 64;
+    constexpr int ROWB = T * COLS * 8, CNTB = kMsdWaves * RADIX * 4;
+    constexpr int UB = ROWB > CNTB ? ROWB : CNTB;
+    __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
+    __shared__ uint8_t s_pd[T];
+    __shared__ int64_t s_spl[RADIX];
+    __shared__ uint32_t s_bin[RADIX + 1];
+    __shared__ uint32_t s_wsum[kMsdWaves];
+    __shared__ int64_t s_gb[RADIX];   // output row of part b's tile-local slot 0
+    __shared__ uint32_t s_ok[RADIX];
+    __shared__ uint32_t s_cur[RADIX]; // rows of part b written so far by this workgroup
+    int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
+    uint32_t *s_wcnt = reinterpret_cast<uint32_t *>(s_u);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nb = p.nspl + 1;
+    const int64_t g = blockIdx.x, t0 = g * p.chunk, t1 = min(t0 + p.chunk, p.ntiles);
+    if (tid < RADIX) {
+        s_spl[tid] = tid < p.nspl ? w.v[128 + tid] : INT64_MAX;
+        s_cur[tid] = 0;
+    }
+    uint32_t *wc = s_wcnt + wave * RADIX;
+    const int lrow0 = wave * ITEMS * 64 + lane;
+    int64_t rows[ITEMS][COLS];
+    auto load_tile = [&](int64_t t, int64_t (&r)[ITEMS][COLS]) {
+        const int64_t row0 = t * T;
+        const int nrows = (int)min((int64_t)T, p.n - row0);
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) load_row<COLS>(p.src + (row0 + min(lrow0 + it * 64, nrows - 1)) * COLS, r[it]);
+    };
+    if (SMJ_P1C_PF && t0 < t1) load_tile(t0, rows);
+    for (int64_t t = t0; t < t1; t++) {
+        zero_counters<RADIX>(wc, lane);  // (the previous tile's last barrier freed the region)
+        int64_t nxt[ITEMS][COLS];
+        if (!SMJ_P1C_PF) load_tile(t, rows);
+        else if (t + 1 < t1) load_tile(t + 1, nxt);  // in flight while this tile is placed
+        __syncthreads();                              // counters zeroed (first tile: splitters, cursors)
+        const int nrows = (int)min((int64_t)T, p.n - t * T);
+        uint32_t dig[ITEMS];
+        uint32_t vmask = 0;
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const bool inb = lrow0 + it * 64 < nrows;
+            const bool pass = !p.use_sel | (pick<COLS>(rows[it], p.sel_col) > p.sel_val);
+            const bool v = inb & pass;
+            const int64_t k = pick<COLS>(rows[it], p.key_col);
+            uint32_t b = 0;
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1) b += s_spl[b + step - 1] < k ? step : 0u;
+            dig[it] = v ? b : 0u;
+            vmask |= v ? (1u << it) : 0u;
+        }
+        wave_rank<ITEMS, 6>(dig, vmask, wc, lane);
+        __syncthreads();
+        (void)tile_digit_starts<RADIX>(s_wcnt, s_bin, s_wsum);
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const uint32_t d = dig[it] & 0xffffu;
+            dig[it] = (d << 16) | (s_bin[d] + wc[d] + (dig[it] >> 16));  // part << 16 | staging slot
+        }
+        __syncthreads();  // counters read out: the region becomes the staging tile
+        if (tid < nb) {
+            const uint32_t c = s_bin[tid + 1] - s_bin[tid], cur = s_cur[tid];
+            const uint64_t cap = (uint64_t)w.v[64 + tid];
+            const bool ok = (uint64_t)cur + c <= cap;
+            if (!ok) atomicOr(&p.flags[1], 1u);
+            s_ok[tid] = ok ? 1u : 0u;
+            s_gb[tid] = w.v[tid] + g * (int64_t)cap + (int64_t)cur - (int64_t)s_bin[tid];
+            s_cur[tid] = ok ? cur + c : cur;
+        }
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if ((vmask >> it) & 1u) {
+                const uint32_t slot = dig[it] & 0xffffu;
+                store_row<COLS>(s_rows + (size_t)slot * COLS, rows[it]);
+                s_pd[slot] = (uint8_t)(dig[it] >> 16);
+            }
+        __syncthreads();  // staging tile and sub-region rows published
+        const uint32_t total = s_bin[nb];
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const uint32_t slot = (uint32_t)(tid + it * kMsdThreads);
+            if (slot < total) {
+                const uint32_t b = s_pd[slot];
+                if (s_ok[b]) {
+                    int64_t r[COLS];
+                    load_row<COLS>(s_rows + (size_t)slot * COLS, r);
+                    store_row<COLS>(p.dst + (s_gb[b] + (int64_t)slot) * COLS, r);
+                }
+            }
+        }
+        __syncthreads();  // staging tile read out
+        if (SMJ_P1C_PF)
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+#pragma unroll
+                for (int c = 0; c < COLS; c++) rows[it][c] = nxt[it][c];
+    }
+    if (tid < RADIX) p.cnt[g * RADIX + tid] = tid < nb ? s_cur[tid] : 0u;
+}
+
+// part b's tile descriptors (MsdPartAParams::desc): block b, thread g = chunk
+// g's rows of part b in ceil(rows / tile) tiles, the chunks in order
+__global__ __launch_bounds__(1024) void msd_p1c_desc_kernel(const uint32_t *cnt, int G, int tile, const P1cDesc d,
+                                                            uint64_t *desc) {
+    __shared__ uint32_t s_w[16];
+    const int b = blockIdx.x, g = threadIdx.x;
+    const uint32_t c = g < G ? cnt[(int64_t)g * 64 + b] : 0u;
+    const uint32_t nt = (c + tile - 1) / tile;
+    uint32_t tot;
+    uint32_t e = block_excl_scan<16>(nt, s_w, &tot);
+    uint64_t *o = desc + d.dbase[b] + e;
+    const int64_t r0 = d.st[b] + (int64_t)g * d.cap[b];
+    for (uint32_t i = 0; i < nt; i++)
+        o[i] = ((uint64_t)(r0 + (int64_t)i * tile) << 16) | (uint64_t)min((uint32_t)tile, c - i * (uint32_t)tile);
 }
 
 // ---------------------------------------------------------------------------
@@ -4266,9 +4417,36 @@ hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <class K>
+static int64_t resident_blocks(K kernel, int threads, size_t dyn_lds);
+
+int msd_part1c_grid(int cols) {
+    static int g[9] = {0};
+    if (cols < 1 || cols > 8) return 0;  // (SMJ_COLS_SWITCH)
+    if (!g[cols]) SMJ_COLS_SWITCH(cols, g[cols] = (int)std::min<int64_t>(1024, resident_blocks(msd_part1c_kernel<C>, kMsdThreads, 0)));
+    const char *e = getenv("SMJ_P1C_GRID");  // tests: fewer chunks of more tiles at small sizes
+    return e && atoi(e) > 0 ? std::min(g[cols], atoi(e)) : g[cols];
+}
+
+hipError_t launch_msd_part1c(const MsdPart1cParams &p, const P1cWords &w, int cols, int grid, hipStream_t s) {
+    if (p.ntiles <= 0) return hipSuccess;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part1c_kernel<C>), dim3((unsigned)grid), dim3(kMsdThreads), 0, s, p, w));
+    return hipGetLastError();
+}
+
+hipError_t launch_p1c_desc(const uint32_t *cnt, int G, int nb, int tile, const P1cDesc &d, uint64_t *desc, hipStream_t s) {
+    if (G > 1024 || nb > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(msd_p1c_desc_kernel, dim3((unsigned)nb), dim3(1024), 0, s, cnt, G, tile, d, desc);
+    return hipGetLastError();
+}
+
+static int64_t pa_tiles(const MsdPartAParams &p, int cols) {
+    return p.n <= 0 ? 0 : p.desc ? p.ntiles : (int64_t)blocks_for(p.n, msd_tile_a(cols));
+}
+
 hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
-    return launch_msd_part_a_tiles(p, cols, 0, blocks_for(p.n, msd_tile_a(cols)), s);
+    return launch_msd_part_a_tiles(p, cols, 0, pa_tiles(p, cols), s);
 }
 
 hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t t0, int64_t t1, hipStream_t s) {
@@ -4287,8 +4465,8 @@ hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, 
     q.t[0] = a;
     q.t[1] = b;
     q.t[0].tile0 = q.t[1].tile0 = 0;
-    q.tiles0 = a.n > 0 ? blocks_for(a.n, msd_tile_a(cols)) : 0u;
-    const unsigned tiles1 = b.n > 0 ? blocks_for(b.n, msd_tile_a(cols)) : 0u;
+    q.tiles0 = (unsigned)pa_tiles(a, cols);
+    const unsigned tiles1 = (unsigned)pa_tiles(b, cols);
     if (q.tiles0 + tiles1 == 0) return hipSuccess;
     SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(q.tiles0 + tiles1), dim3(pa_threads(C)), 0,
                                              s, q));

@@ -108,6 +108,50 @@ def test_partitioned_sorted_input_matches_oracle(gpu, oracle_built, parts):
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
 
 
+@pytest.mark.parametrize("case", [FORCED[1], FORCED[2], FORCED[3], FORCED[7], FORCED[4]])
+def test_chunked_partition_matches_oracle(gpu, oracle_built, parts, monkeypatch, capfd, case):
+    """The chunked one-pass partition (msd_part1c_kernel) with 3 chunks, so
+    that every chunk walks many tiles and its parts span several sub-regions
+    and partial part_a tiles: bit-exact, and the chunked path is the one taken."""
+    from smj import ops
+    nr, ns, c1, c2, k1, k2, kind, s1, s2, p = case
+    parts(p)
+    monkeypatch.setenv("SMJ_P1C_GRID", "3")
+    monkeypatch.setenv("SMJ_DEBUG_PART1", "1")
+    rng = np.random.default_rng(nr + 5 * ns + p)
+    R = table(rng, nr, c1, kind, k1, 0)
+    S = table(rng, ns, c2, kind, k2, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R).reshape(nr, c1), dev(S).reshape(ns, c2), k1, k2, s1, s2)
+    torch.cuda.synchronize()
+    assert "chunked one-pass" in capfd.readouterr().err
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, s2)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, c1))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, c2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
+
+
+def test_chunked_partition_overflow_falls_back(gpu, oracle_built, parts, monkeypatch, capfd):
+    """Input clustered by key (sorted R): every chunk's rows fall in a few
+    parts, its sub-regions overflow, and the call takes the look-back
+    partition instead -- still bit-exact."""
+    from smj import ops
+    parts(5)
+    monkeypatch.setenv("SMJ_P1C_GRID", "4")
+    monkeypatch.setenv("SMJ_DEBUG_PART1", "1")
+    rng = np.random.default_rng(23)
+    R = table(rng, 300_000, 2, "uniform", 0, 0)
+    S = table(rng, 200_000, 2, "uniform", 0, 10 ** 9)
+    R = np.ascontiguousarray(R[np.argsort(R[:, 0], kind="stable")])
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, (0, SEL), (0, SEL))
+    torch.cuda.synchronize()
+    err = capfd.readouterr().err
+    assert "chunked partition overflowed" in err and "one-pass regions" in err
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, (0, SEL), (0, SEL))
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
 def test_partitioned_select_sort_matches_oracle(gpu, oracle_built, parts):
     from smj import ops
     parts(5)

@@ -50,12 +50,16 @@ for s in $STEPS; do
     msd)   test_run msd 600 $PYT tests/test_gpu_msd.py ;;
     parity) test_run parity 600 $PYT tests/test_gpu_parity.py ;;
     large) test_run large 900 $PYT tests/test_gpu_large.py ;;
+    lsmall) test_run lsmall 600 $PYT tests/test_gpu_large.py -k "partition or chunked" ;;
+    lfull) test_run lfull 900 $PYT tests/test_gpu_large.py -k "full_size" ;;
     dist)  test_run dist 600 $PYT tests/test_dist_gloo.py -m gpu ;;
     multidev) test_run multidev 600 $PYT tests/test_gpu_multidev.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
     c5)    run c5 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c5.out" c5 ;;
+    c4old) SMJ_PART1C=0 run c4old 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4old.out" c4old ;;
+    c4pf)  SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/p1cpf/libsmj_hip.so run c4pf 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4pf.out" c4pf ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
