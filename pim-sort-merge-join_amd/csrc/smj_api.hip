@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <map>
 #include <mutex>
 #include <string>
@@ -72,6 +73,7 @@ std::vector<ProfRec> g_prof;
 std::map<int, std::vector<hipEvent_t>> g_event_pool;  // per device: an event records only on its own device's streams
 std::mutex g_mu;  // scratch maps and profiler records (the host API drives devices from worker threads)
 thread_local int t_slot = -1;  // smj::set_scratch_slot
+thread_local int t_msd_var = 0;  // msd_large: the MsdScratch set of the part in flight (0 / 1)
 
 hipEvent_t take_event(int dev) {
     std::vector<hipEvent_t> &pool = g_event_pool[dev];
@@ -541,8 +543,9 @@ MsdBgLimits msd_bg_limits() {  // read per call: a test may change them between 
 
 int msd_scratch(MsdScratch **out) {
     int dev = 0;
-    const int key = scratch_key(&dev);
-    if (key < 0) return SMJ_ERR_HIP;
+    const int base = scratch_key(&dev);
+    if (base < 0) return SMJ_ERR_HIP;
+    const int key = base + (t_msd_var << 20);
     std::lock_guard<std::mutex> lk(g_mu);
     MsdScratch &m = g_msd[key];
     if (m.dev < 0) {
@@ -891,8 +894,20 @@ int msd_combined(const MsdIn *in, int ntab) {
     return 2 * hi > 3 * lo ? 1 : 0;  // over 1.5 : 1
 }
 
-int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s,
-            const MsdStage *stg = nullptr) {
+// The pipeline in two phases: msd_front launches sample .. final (no host
+// wait), msd_back the count scan + compact, reads the plan back and runs the
+// fallback tiers.  msd_large overlaps part p's back (its host round trips)
+// with part p + 1's front on another stream and scratch set.
+struct MsdCtx {
+    MsdScratch *ms = nullptr;
+    MsdFinalParams fp{};
+    const MsdIn *in = nullptr;
+    int ntab = 0, join = 0, tc = 1;
+    size_t pa[2] = {(size_t)-1, (size_t)-1}, pb[2] = {(size_t)-1, (size_t)-1}, pf = (size_t)-1;
+    bool pa_fused = false;
+};
+
+int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, const MsdStage *stg, MsdCtx *cx) {
     for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
         SMJ_TRY(check_table(in[x].n, in[x].cols, in[x].use_sel ? in[x].sel_col : 0, in[x].key));
     if (join && (ntab != 2 || key2 != in[1].key)) return SMJ_ERR_INVALID;
@@ -1090,12 +1105,33 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     fp.combined = msd_combined(in, ntab);
     fp.key2 = key2;
     if (t_slot < 0) g_fin_last = fp;
-    size_t pf;
     {
         ProfScope ps("msd_final", 0, s);
         HIP_TRY(launch_msd_final(fp, s));
     }
-    pf = prof_last();
+    cx->ms = ms;
+    cx->fp = fp;
+    cx->in = in;
+    cx->ntab = ntab;
+    cx->join = join;
+    cx->tc = tc;
+    cx->pf = prof_last();
+    for (int x = 0; x < 2; x++) {
+        cx->pa[x] = pa[x];
+        cx->pb[x] = pb[x];
+    }
+    cx->pa_fused = pa_fused;
+    return SMJ_OK;
+}
+
+int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
+    MsdScratch *ms = cx.ms;
+    const MsdIn *in = cx.in;
+    const int ntab = cx.ntab, join = cx.join, tc = cx.tc;
+    const MsdFinalParams &fp = cx.fp;
+    const size_t pf = cx.pf;
+    const size_t *pa = cx.pa, *pb = cx.pb;
+    const bool pa_fused = cx.pa_fused;
     auto compact = [&](int after_fallback) -> int {
         {
             ProfScope ps("msd_count_scan", 0, s);
@@ -1163,6 +1199,13 @@ int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_
     prof_set_bytes(pc, 2.0 * Jb);
     if (join) h_rows[2] = pl.joined;
     return SMJ_OK;
+}
+
+int msd_run(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s,
+            const MsdStage *stg = nullptr) {
+    MsdCtx cx;
+    SMJ_TRY(msd_front(in, ntab, join, key2, s, stg, &cx));
+    return msd_back(cx, out_j, h_rows, s);
 }
 
 int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int key, const T *out) {
@@ -1439,6 +1482,34 @@ int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64
     return SMJ_OK;
 }
 
+// SMJ_PART_OVERLAP=0: the parts strictly in turn on the caller's stream (A/B)
+bool msd_overlap_on() {
+    static const bool on = [] {
+        const char *e = getenv("SMJ_PART_OVERLAP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// the partitioned mode's two part streams per scratch key (non-blocking: no
+// implicit ordering with the legacy default stream)
+int part_streams(hipStream_t out[2]) {
+    int dev = 0;
+    const int key = scratch_key(&dev);
+    if (key < 0) return SMJ_ERR_HIP;
+    std::lock_guard<std::mutex> lk(g_mu);
+    static std::map<int, std::array<hipStream_t, 2>> m;
+    auto it = m.find(key);
+    if (it == m.end()) {
+        std::array<hipStream_t, 2> a{};
+        for (auto &x : a) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        it = m.emplace(key, a).first;
+    }
+    out[0] = it->second[0];
+    out[1] = it->second[1];
+    return SMJ_OK;
+}
+
 int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
@@ -1519,9 +1590,12 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     // 4. the pipeline per part, in place
     int64_t J = 0;
     const int tc = ntab > 1 ? in[0].cols + in[1].cols - 1 : 1;
+    std::vector<MsdIn> parts(2 * (size_t)(nspl + 1));
+    std::vector<int> nps(nspl + 1, 0);
+    bool all_joined = join != 0;  // every part has rows of both tables
     for (int p = 0; p <= nspl; p++) {
-        MsdIn part[2];
-        int np = 0;
+        MsdIn *part = &parts[2 * (size_t)p];
+        int &np = nps[p];
         for (int x = 0; x < ntab; x++) {
             if (cnt[x][p] == 0) continue;
             T *base = in[x].out + off[x][p] * in[x].cols;
@@ -1533,6 +1607,49 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
             const T *src = staged ? (const T *)ms->pst[x] + roff[x][p] * in[x].cols : base;
             part[np++] = MsdIn{src, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
         }
+        all_joined &= np == 2;
+    }
+    if (all_joined && !g_prof_on && msd_overlap_on()) {
+        // part p's back phase (its host round trips: plan, fallback lists)
+        // overlaps part p + 1's front phase, which runs on the other stream
+        // with the other scratch set (part p - 1's, whose back has returned).
+        // Profiling steps run the parts in turn: their per-kernel times stay
+        // those of a kernel alone on the GPU.
+        hipStream_t ps[2];
+        SMJ_TRY(part_streams(ps));
+        struct Guard {  // on any exit: no part still in flight, scratch set 0 current
+            hipStream_t *ps;
+            ~Guard() {
+                hipStreamSynchronize(ps[0]);
+                hipStreamSynchronize(ps[1]);
+                t_msd_var = 0;
+            }
+        } guard{ps};
+        hipEvent_t ready;
+        HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        const hipError_t er = hipEventRecord(ready, s);  // the partition's output on s
+        for (int i = 0; i < 2 && er == hipSuccess; i++) HIP_TRY(hipStreamWaitEvent(ps[i], ready, 0));
+        hipEventDestroy(ready);
+        HIP_TRY(er);
+        std::vector<MsdCtx> cx(nspl + 1);
+        auto front = [&](int p) -> int {
+            t_msd_var = p & 1;
+            return msd_front(&parts[2 * (size_t)p], 2, 1, key2, ps[p & 1], nullptr, &cx[p]);
+        };
+        SMJ_TRY(front(0));
+        for (int p = 0; p <= nspl; p++) {
+            if (p < nspl) SMJ_TRY(front(p + 1));
+            t_msd_var = p & 1;
+            int64_t rows[3] = {0, 0, 0};
+            SMJ_TRY(msd_back(cx[p], out_j + J * tc, rows, ps[p & 1]));
+            J += rows[2];
+        }
+        h_rows[2] = J;
+        return SMJ_OK;
+    }
+    for (int p = 0; p <= nspl; p++) {
+        MsdIn *part = &parts[2 * (size_t)p];
+        const int np = nps[p];
         int64_t rows[3] = {0, 0, 0};
         if (np == 2 && join) {
             SMJ_TRY(msd_run(part, 2, 1, key2, out_j + J * tc, rows, s));
