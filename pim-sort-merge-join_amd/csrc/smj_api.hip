@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <string>
@@ -1482,6 +1483,30 @@ int msd_part1(MsdScratch *ms, const MsdIn *in, int ntab, const std::vector<int64
     return SMJ_OK;
 }
 
+// LSD radix sort of (key, weight) pairs by key, 8-bit digits, skipping the
+// digits every key shares: ~8k samples in tens of microseconds where
+// std::sort took ~0.3 ms of idle GPU per partitioned call (SMJ_DEBUG_HOST)
+void radix_sort_keys(std::vector<std::pair<int64_t, double>> &v) {
+    const size_t n = v.size();
+    if (n < 2) return;
+    std::vector<std::pair<int64_t, double>> tmp(n);
+    auto ukey = [](int64_t k) { return (uint64_t)k ^ (1ull << 63); };  // signed order as unsigned
+    uint64_t all_or = 0, all_and = ~0ull;
+    for (const auto &e : v) {
+        all_or |= ukey(e.first);
+        all_and &= ukey(e.first);
+    }
+    const uint64_t varying = all_or ^ all_and;
+    for (int sh = 0; sh < 64; sh += 8) {
+        if (((varying >> sh) & 0xffu) == 0) continue;
+        size_t c[257] = {0};
+        for (const auto &e : v) c[((ukey(e.first) >> sh) & 0xffu) + 1]++;
+        for (int d = 0; d < 256; d++) c[d + 1] += c[d];
+        for (const auto &e : v) tmp[c[(ukey(e.first) >> sh) & 0xffu]++] = e;
+        v.swap(tmp);
+    }
+}
+
 // SMJ_PART_OVERLAP=0: the parts strictly in turn on the caller's stream (A/B)
 bool msd_overlap_on() {
     static const bool on = [] {
@@ -1510,7 +1535,35 @@ int part_streams(hipStream_t out[2]) {
     return SMJ_OK;
 }
 
+// SMJ_DEBUG_HOST=1: the partitioned mode's host timeline per call (us since
+// entry at each phase, and the host time since the previous call returned)
+struct HostMarks {
+    using clk = std::chrono::steady_clock;
+    bool on = getenv("SMJ_DEBUG_HOST") != nullptr;
+    clk::time_point t0 = clk::now();
+    std::string log;
+    static clk::time_point &last_exit() {
+        static clk::time_point t = clk::time_point{};
+        return t;
+    }
+    void mark(const char *what) {
+        if (!on) return;
+        char b[96];
+        snprintf(b, sizeof b, " %s %.0f", what, std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+        log += b;
+    }
+    ~HostMarks() {
+        if (!on) return;
+        mark("exit");
+        const double gap = last_exit() == clk::time_point{} ? 0.0
+                                                             : std::chrono::duration<double, std::micro>(t0 - last_exit()).count();
+        fprintf(stderr, "smj host: since last call %.0f us |%s\n", gap, log.c_str());
+        last_exit() = clk::now();
+    }
+};
+
 int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *h_rows, hipStream_t s) {
+    HostMarks hm;
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
     const int64_t P = msd_large_parts(in, ntab);
@@ -1528,6 +1581,7 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
     HIP_TRY(hipMemcpyAsync(ms->h_samp, ms->samp, sizeof(int64_t) * (2 * kSampleMax + kSampleGatherBlocksH),
                            hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    hm.mark("sample");
     // 2. P - 1 splitters: weighted quantiles (a sample of table x stands for
     // n_x / (its sample count) input rows; dropped rows are not samples)
     std::vector<std::pair<int64_t, double>> kw;
@@ -1543,7 +1597,7 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
             W += w;
         }
     }
-    std::sort(kw.begin(), kw.end());
+    radix_sort_keys(kw);  // by key (the order among equal keys does not change which key a quantile picks)
     std::vector<int64_t> spl;
     {
         double acc = 0;
@@ -1556,6 +1610,7 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         }
     }
     const int nspl = (int)spl.size();
+    hm.mark("splitters");
     if (nspl) HIP_TRY(hipMemcpyAsync(ms->lspl, spl.data(), sizeof(int64_t) * nspl, hipMemcpyHostToDevice, s));
     // 3. select + stable partition of every table: in one pass into part
     // regions sized from the sample (msd_part1_kernel; each part is then sorted
@@ -1569,6 +1624,7 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         SMJ_TRY(msd_part1c(ms, in, ntab, spl, cnt, desc, ntl, &chunked, s));
         if (!chunked) SMJ_TRY(msd_part1(ms, in, ntab, spl, cnt, roff, &staged, s));
     }
+    hm.mark("partition");
     if (getenv("SMJ_DEBUG_PART1")) {
         fprintf(stderr, "smj: partitioned mode: %lld x %lld rows, %d parts (%zu weighted samples), %s; splitters", (long long)in[0].n,
                 (long long)(ntab > 1 ? in[1].n : 0), nspl + 1, kw.size(),
@@ -1637,12 +1693,14 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
             return msd_front(&parts[2 * (size_t)p], 2, 1, key2, ps[p & 1], nullptr, &cx[p]);
         };
         SMJ_TRY(front(0));
+        hm.mark("f0");
         for (int p = 0; p <= nspl; p++) {
             if (p < nspl) SMJ_TRY(front(p + 1));
             t_msd_var = p & 1;
             int64_t rows[3] = {0, 0, 0};
             SMJ_TRY(msd_back(cx[p], out_j + J * tc, rows, ps[p & 1]));
             J += rows[2];
+            hm.mark("b");
         }
         h_rows[2] = J;
         return SMJ_OK;

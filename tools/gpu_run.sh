@@ -62,6 +62,8 @@ for s in $STEPS; do
     c4pf)  SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/p1cpf/libsmj_hip.so run c4pf 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4pf.out" c4pf ;;
     c4nov) SMJ_PART_OVERLAP=0 run c4nov 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4nov.out" c4nov ;;
     c5nov) SMJ_PART_OVERLAP=0 run c5nov 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c5nov.out" c5nov ;;
+    hostc4) SMJ_DEBUG_HOST=1 run hostc4 600 python bench.py --workload c4 --steps 3 --warmup 1 $NOCPU ;;
+    hostc5) SMJ_DEBUG_HOST=1 run hostc5 600 python bench.py --workload c5 --steps 3 --warmup 1 $NOCPU ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
