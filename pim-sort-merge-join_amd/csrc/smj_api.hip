@@ -1673,14 +1673,19 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         // those of a kernel alone on the GPU.
         hipStream_t ps[2];
         SMJ_TRY(part_streams(ps));
+        hipEvent_t fe[2] = {nullptr, nullptr};  // front p launched: front p + 1 starts behind it
         struct Guard {  // on any exit: no part still in flight, scratch set 0 current
             hipStream_t *ps;
+            hipEvent_t *fe;
             ~Guard() {
                 hipStreamSynchronize(ps[0]);
                 hipStreamSynchronize(ps[1]);
+                for (int i = 0; i < 2; i++)
+                    if (fe[i]) hipEventDestroy(fe[i]);
                 t_msd_var = 0;
             }
-        } guard{ps};
+        } guard{ps, fe};
+        for (int i = 0; i < 2; i++) HIP_TRY(hipEventCreateWithFlags(&fe[i], hipEventDisableTiming));
         hipEvent_t ready;
         HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         const hipError_t er = hipEventRecord(ready, s);  // the partition's output on s
@@ -1688,9 +1693,15 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         hipEventDestroy(ready);
         HIP_TRY(er);
         std::vector<MsdCtx> cx(nspl + 1);
+        // SMJ_PART_CHAIN=1: front p + 1 waits for front p's kernels, so that it
+        // shares the GPU with part p's back phase rather than with front p
+        static const bool chain = getenv("SMJ_PART_CHAIN") && getenv("SMJ_PART_CHAIN")[0] == '1';
         auto front = [&](int p) -> int {
             t_msd_var = p & 1;
-            return msd_front(&parts[2 * (size_t)p], 2, 1, key2, ps[p & 1], nullptr, &cx[p]);
+            if (p > 0 && chain) HIP_TRY(hipStreamWaitEvent(ps[p & 1], fe[(p - 1) & 1], 0));
+            SMJ_TRY(msd_front(&parts[2 * (size_t)p], 2, 1, key2, ps[p & 1], nullptr, &cx[p]));
+            HIP_TRY(hipEventRecord(fe[p & 1], ps[p & 1]));
+            return SMJ_OK;
         };
         SMJ_TRY(front(0));
         hm.mark("f0");

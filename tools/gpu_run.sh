@@ -64,6 +64,12 @@ for s in $STEPS; do
     c5nov) SMJ_PART_OVERLAP=0 run c5nov 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c5nov.out" c5nov ;;
     hostc4) SMJ_DEBUG_HOST=1 run hostc4 600 python bench.py --workload c4 --steps 3 --warmup 1 $NOCPU ;;
     hostc5) SMJ_DEBUG_HOST=1 run hostc5 600 python bench.py --workload c5 --steps 3 --warmup 1 $NOCPU ;;
+    abov)  # same-box A/B/C of the partitioned mode's part overlap: on / chained / off, twice, C4 and C5
+           for w in c4 c5; do for r in 1 2; do
+             run ab_${w}_on_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_on_$r.out" ${w}_on
+             SMJ_PART_CHAIN=1 run ab_${w}_ch_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_ch_$r.out" ${w}_chain
+             SMJ_PART_OVERLAP=0 run ab_${w}_off_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_off_$r.out" ${w}_off
+           done; done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
