@@ -25,7 +25,9 @@
  *     part regions of ~1.3x the table of library scratch when the device
  *     has room, else counted and scattered in place; the regions stay
  *     allocated for the next call until smj_finalize, and are released
- *     when they cannot all be had), tables over 8 columns
+ *     when they cannot all be had; two parts are in flight at once, on two
+ *     library streams with two sets of per-part scratch, both kept until
+ *     smj_finalize -- ~12 GB each at 1e9 x 1e9), tables over 8 columns
  *     are sorted as (key, row id) pairs and gathered; the
  *     LSD and partition entry points take 1..8 columns (else
  *     SMJ_ERR_UNSUPPORTED).

@@ -577,7 +577,12 @@ int msd_scratch(MsdScratch **out) {
     return SMJ_OK;
 }
 
+std::map<int, std::array<hipStream_t, 2>> g_part_streams;  // msd_large's part streams per scratch key
+
 void msd_free_all() {
+    for (auto &kv : g_part_streams)
+        for (hipStream_t st : kv.second) hipStreamDestroy(st);
+    g_part_streams.clear();
     for (auto &kv : g_msd) {
         MsdScratch &m = kv.second;
         if (m.dev < 0) continue;
@@ -1523,7 +1528,7 @@ int part_streams(hipStream_t out[2]) {
     const int key = scratch_key(&dev);
     if (key < 0) return SMJ_ERR_HIP;
     std::lock_guard<std::mutex> lk(g_mu);
-    static std::map<int, std::array<hipStream_t, 2>> m;
+    auto &m = g_part_streams;
     auto it = m.find(key);
     if (it == m.end()) {
         std::array<hipStream_t, 2> a{};
