@@ -97,6 +97,12 @@ for s in $STEPS; do
                python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmcw)  run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
                python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
+    pmc45) for w in c4 c5; do
+             run pmc_fetch_$w 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$w" -o run -- \
+               python3 "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 $NOCPU
+             run pmc_write_$w 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$w" -o run -- \
+               python3 "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 $NOCPU
+           done ;;
     pmcsq) run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
                --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmcsq2) run pmc_sq2 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES \

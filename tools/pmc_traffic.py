@@ -40,7 +40,8 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_compact_kernel", "msd_compact", True),
     (r"gen_uniform_kernel", "gen_uniform", True),
     (r"gen_zipf_kernel", "gen_zipf", True),
-    (r"msd_part1_kernel", "partition_1pass", True),
+    (r"msd_part1c?_kernel", "partition_1pass", True),
+    (r"msd_p1c_desc_kernel", "partition_1pass", False),
     (r"msd_big_stage_kernel", "msd_big_dev", True),
     (r"msd_giant_\w+_kernel", "msd_big_dev", False),
     (r"msd_single_kernel", "msd_single", True),
