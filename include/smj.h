@@ -186,6 +186,25 @@ int smj_dev_sort_merge_join(const int64_t *R, int64_t nr, int c1, int use_sel1, 
                             const int64_t *S, int64_t ns, int c2, int use_sel2, int sel_col2, int64_t sel_val2, int key2,
                             int64_t *R_sorted, int64_t *S_sorted, int64_t *out, int64_t *h_rows, void *stream);
 
+/* smj_dev_sort_merge_join in two halves.  _begin validates the arguments,
+ * enqueues the pipeline up to its sort/join kernel on `stream` and returns at
+ * once with *job; _end enqueues the compaction of the joined rows into `out`,
+ * waits, and fills h_rows exactly as smj_dev_sort_merge_join does (the job is
+ * released whatever it returns).  Between the two the calling thread may do
+ * anything but start another smj_dev_* pipeline call (the job holds the
+ * thread's scratch; a second _begin returns SMJ_ERR_INVALID): the multi-GPU
+ * driver posts its next stage's transfers there, and `out`'s place may be
+ * chosen only then.  Inputs and R_sorted / S_sorted must stay valid until _end
+ * returns.  Tables over 1.6e8 rows, over 8 columns or empty run whole inside
+ * _end.  (Replaces nothing in the reference: app.c's DPU launches are
+ * synchronous, app.c:247; this is the asynchronous form a device-resident
+ * caller needs.) */
+int smj_dev_sort_merge_join_begin(const int64_t *R, int64_t nr, int c1, int use_sel1, int sel_col1, int64_t sel_val1,
+                                  int key1, const int64_t *S, int64_t ns, int c2, int use_sel2, int sel_col2,
+                                  int64_t sel_val2, int key2, int64_t *R_sorted, int64_t *S_sorted, void *stream,
+                                  void **job);
+int smj_dev_sort_merge_join_end(void *job, int64_t *out, int64_t *h_rows);
+
 /* Stable select alone (a stable compaction). *out_rows is written after a
  * stream synchronisation. */
 int smj_dev_select(const int64_t *in, int64_t n_rows, int col_num, int select_col, int64_t select_val, int64_t *out,

@@ -15,6 +15,8 @@
 #include <array>
 #include <chrono>
 #include <map>
+#include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1970,6 +1972,76 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
                         {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
     if (c1 > kDirectCols || c2 > kDirectCols) return msd_indexed(t, 2, 1, key2, SMJ_KEY_INT64, out, h_rows, s);
     return msd_any(t, 2, 1, key2, out, h_rows, s);
+}
+
+// The fused call in two halves (smj.h): _begin launches the pipeline up to
+// its final kernel and returns; _end runs the count scan and compaction into
+// out, reads the plan back and runs the fallback tiers.  Between them the
+// caller's host thread is free -- the multi-GPU driver posts the next stage's
+// transfers there -- but must not start another pipeline call (the job owns
+// the thread's scratch).  Shapes the split does not cover (partitioned
+// sizes, wide rows, an empty table) run whole inside _end.
+struct SmjJob {
+    MsdIn in[2];
+    MsdCtx cx;
+    hipStream_t s = nullptr;
+    bool whole = false;
+    const T *R = nullptr, *S = nullptr;
+    int64_t nr = 0, ns = 0;
+    int c1 = 0, c2 = 0, use_sel1 = 0, sel_col1 = 0, key1 = 0, use_sel2 = 0, sel_col2 = 0, key2 = 0;
+    T sel_val1 = 0, sel_val2 = 0;
+    T *R_sorted = nullptr, *S_sorted = nullptr;
+};
+thread_local SmjJob *t_job = nullptr;  // the thread's job between _begin and _end
+
+extern "C" int smj_dev_sort_merge_join_begin(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
+                                             int key1, const T *S, int64_t ns, int c2, int use_sel2, int sel_col2,
+                                             T sel_val2, int key2, T *R_sorted, T *S_sorted, void *stream,
+                                             void **job) {
+    if (!job) return SMJ_ERR_INVALID;
+    *job = nullptr;
+    if (t_job) return SMJ_ERR_INVALID;  // an earlier _begin has not been ended
+    SMJ_TRY(msd_check(R, nr, c1, use_sel1, sel_col1, key1, R_sorted));
+    SMJ_TRY(msd_check(S, ns, c2, use_sel2, sel_col2, key2, S_sorted));
+    SmjJob *j = new (std::nothrow) SmjJob;
+    if (!j) return SMJ_ERR_NOMEM;
+    *j = SmjJob{};
+    j->s = (hipStream_t)stream;
+    j->R = R, j->S = S, j->nr = nr, j->ns = ns, j->c1 = c1, j->c2 = c2;
+    j->use_sel1 = use_sel1, j->sel_col1 = sel_col1, j->sel_val1 = sel_val1, j->key1 = key1;
+    j->use_sel2 = use_sel2, j->sel_col2 = sel_col2, j->sel_val2 = sel_val2, j->key2 = key2;
+    j->R_sorted = R_sorted, j->S_sorted = S_sorted;
+    j->whole = nr == 0 || ns == 0 || c1 > kDirectCols || c2 > kDirectCols || g_force_parts > 0 ||
+               nr > kMsdSingleMax || ns > kMsdSingleMax;
+    if (!j->whole) {
+        j->in[0] = MsdIn{R, nr, c1, use_sel1, sel_col1, key1, sel_val1, R_sorted};
+        j->in[1] = MsdIn{S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted};
+        const int rc = msd_front(j->in, 2, 1, key2, j->s, nullptr, &j->cx);
+        if (rc != SMJ_OK) {
+            delete j;
+            return rc;
+        }
+    }
+    t_job = j;
+    *job = j;
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
+    SmjJob *j = (SmjJob *)job;
+    if (!j || j != t_job || !h_rows) return SMJ_ERR_INVALID;
+    t_job = nullptr;
+    std::unique_ptr<SmjJob> own(j);
+    h_rows[0] = h_rows[1] = h_rows[2] = 0;
+    if (j->whole)
+        return smj_dev_sort_merge_join(j->R, j->nr, j->c1, j->use_sel1, j->sel_col1, j->sel_val1, j->key1, j->S,
+                                       j->ns, j->c2, j->use_sel2, j->sel_col2, j->sel_val2, j->key2, j->R_sorted,
+                                       j->S_sorted, out, h_rows, j->s);
+    if (!out) {  // the launched half still has to drain before its scratch is reused
+        hipStreamSynchronize(j->s);
+        return SMJ_ERR_INVALID;
+    }
+    return msd_back(j->cx, out, h_rows, j->s);
 }
 
 // The host-pointer path with staged input (smj_host.hip): R and S are

@@ -46,6 +46,9 @@ SIGNATURES = {
     "smj_dev_select_sort": (_I, [_P, _L, _I, _I, _I, _L, _I, _U, _P, _PL, _P]),
     "smj_dev_select_sort_lsd": (_I, [_P, _L, _I, _I, _I, _L, _I, _U, _P, _PL, _P]),
     "smj_dev_sort_merge_join": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _L, _I, _I, _I, _L, _I, _P, _P, _P, _PL, _P]),
+    "smj_dev_sort_merge_join_begin": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _L, _I, _I, _I, _L, _I, _P, _P, _P,
+                                           ctypes.POINTER(ctypes.c_void_p)]),
+    "smj_dev_sort_merge_join_end": (_I, [_P, _P, _PL]),
     "smj_dev_sort_merge_join_typed": (_I, [_I, _P, _L, _I, _I, _I, ctypes.c_uint64, _I, _P, _L, _I, _I, _I,
                                            ctypes.c_uint64, _I, _P, _P, _P, _PL, _P]),
     "smj_sort_merge_join_typed": (_I, [_I, _P, _P, _P, _P, _I, ctypes.c_uint64, _I, ctypes.c_uint64, _I, _I,

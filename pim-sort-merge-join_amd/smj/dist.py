@@ -112,6 +112,20 @@ class _Tracer:
         self.t = t
 
 
+# the per-stage pipelines in two halves on a side stream (SMJ_DIST_SPLIT=0:
+# one blocking call per stage on the current stream, after the next stage's
+# transfers are posted)
+SPLIT_STAGES = os.environ.get("SMJ_DIST_SPLIT", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(str(device))
+    if s is None:
+        s = _SIDE[str(device)] = torch.cuda.Stream(device=device)
+    return s
+
+
 class HipOps:
     """The product operators: HIP kernels behind libsmj_hip.so."""
     sort_merge_join = staticmethod(hip_ops.sort_merge_join)
@@ -120,6 +134,7 @@ class HipOps:
     partition_plan = staticmethod(hip_ops.partition_plan)    # asynchronous: counts stay on the device
     partition_apply = staticmethod(hip_ops.partition_apply)
     partition_regions = staticmethod(hip_ops.partition_regions)  # one read of the table (msd_part1_kernel)
+    sort_merge_join_begin = staticmethod(hip_ops.sort_merge_join_begin)  # the pipeline enqueued; job.end(out) finishes it
     region_capacities = staticmethod(hip_ops.region_capacities)
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
@@ -626,14 +641,36 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     J = torch.empty((max(bound, 1), ncols), dtype=R.dtype, device=R.device) if into else None
     parts, at = [], 0
     tr("stage 0 posted")
+    begin = getattr(ops, "sort_merge_join_begin", None) if into and R.is_cuda and SPLIT_STAGES else None
+    side = _side_stream(R.device) if begin else None
     for k in range(K):
         Rk, Sk = _wait_all(pending)
         tr(f"stage {k} received")
+        job = None
+        if begin and Rk.shape[0] and Sk.shape[0]:
+            # this stage's pipeline is enqueued before the next stage's
+            # transfers are posted -- posting costs ~0.3 ms of host time per
+            # stage (profiles/r04/r04y), which the GPU now spends sorting --
+            # on a side stream: the process group orders its transfers after
+            # the current stream's work, and they must not wait for the sort
+            side.wait_stream(torch.cuda.current_stream())
+            job = begin(Rk, Sk, k1, k2, None, None, stream=side)
         if k + 1 < K:
-            pending = [post_stage(k + 1, K, sends, regs, sl, rank, world, R.device, group, loopback)]
+            try:
+                pending = [post_stage(k + 1, K, sends, regs, sl, rank, world, R.device, group, loopback)]
+            except BaseException:
+                if job is not None:  # the thread's pipeline scratch is the job's until it ends
+                    job.end()
+                raise
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
             continue
-        if into:
+        if job is not None:
+            b = min(Rk.shape[0], Sk.shape[0])
+            got = job.end(out=J[at: at + b])[2]  # waits for the side stream
+            torch.cuda.current_stream().wait_stream(side)
+            at += got.shape[0]
+            del job
+        elif into:
             b = min(Rk.shape[0], Sk.shape[0])
             got = ops.sort_merge_join(Rk, Sk, k1, k2, None, None, out=J[at: at + b])[2]
             at += got.shape[0]

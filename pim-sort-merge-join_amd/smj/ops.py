@@ -123,6 +123,58 @@ def sort_merge_join(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=N
     return R_sorted[: rows[0]], S_sorted[: rows[1]], out[: rows[2]]
 
 
+class SortMergeJoinJob:
+    """sort_merge_join in two halves (smj_dev_sort_merge_join_begin / _end):
+    the pipeline is enqueued by sort_merge_join_begin, and end(out) compacts
+    the joined rows into out (allocated if None), waits and returns what
+    sort_merge_join returns.  Until end() the thread must not start another
+    pipeline call; the tables and the job must stay alive."""
+
+    def __init__(self, lib, handle, R, S, R_sorted, S_sorted, stream):
+        self._lib, self._h = lib, handle
+        self._keep = (R, S)
+        self.R_sorted, self.S_sorted, self._stream = R_sorted, S_sorted, stream
+
+    def end(self, out=None):
+        if self._h is None:
+            raise RuntimeError("job already ended")
+        R, S = self._keep
+        nr, c1 = R.shape
+        ns, c2 = S.shape
+        if out is None:
+            out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=torch.int64, device=R.device)
+        else:
+            _out(out, "out", min(nr, ns), c1 + c2 - 1, R)
+        rows = (ctypes.c_int64 * 3)()
+        h, self._h = self._h, None
+        _lib.check(self._lib.smj_dev_sort_merge_join_end(h, _ptr(out), rows), "smj_dev_sort_merge_join_end")
+        self._keep = None
+        return self.R_sorted[: rows[0]], self.S_sorted[: rows[1]], out[: rows[2]]
+
+
+def sort_merge_join_begin(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=None, S_sorted=None,
+                          stream=None):
+    """Enqueue sort_merge_join up to its sort/join kernel and return a
+    SortMergeJoinJob at once (int64 tables); job.end(out) finishes it."""
+    lib = _lib.load()
+    _table(R, "R")
+    _table(S, "S")
+    nr, c1 = R.shape
+    ns, c2 = S.shape
+    if S.device != R.device:
+        raise ValueError("R and S must be on the same device")
+    R_sorted = torch.empty_like(R) if R_sorted is None else _out(R_sorted, "R_sorted", nr, c1, R)
+    S_sorted = torch.empty_like(S) if S_sorted is None else _out(S_sorted, "S_sorted", ns, c2, R)
+    s1 = select1 or (0, 0)
+    s2 = select2 or (0, 0)
+    h = ctypes.c_void_p()
+    _lib.check(lib.smj_dev_sort_merge_join_begin(_ptr(R), nr, c1, int(select1 is not None), s1[0], int(s1[1]), key1,
+                                                 _ptr(S), ns, c2, int(select2 is not None), s2[0], int(s2[1]), key2,
+                                                 _ptr(R_sorted), _ptr(S_sorted), _stream(stream), ctypes.byref(h)),
+               "smj_dev_sort_merge_join_begin")
+    return SortMergeJoinJob(lib, h, R, S, R_sorted, S_sorted, stream)
+
+
 def _sort_merge_join_typed(lib, R, S, key1, key2, select1, select2, R_sorted, S_sorted, out, stream, key_type):
     for name, t in (("R", R), ("S", S)):
         if not (t.is_cuda and t.dim() == 2 and t.is_contiguous() and t.element_size() == 8):

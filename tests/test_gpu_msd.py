@@ -138,6 +138,48 @@ def test_forced_timeout_is_fault_safe(gpu, oracle_built, nr, ns, kind, parts):
     np.testing.assert_array_equal(host(gJ), J)
 
 
+@pytest.mark.parametrize("nr,ns,kind,parts", [
+    (300_000, 250_000, "uniform", 0),   # the split path: front enqueued, back in end()
+    (40_000, 400_000, "zipf", 0),       # oversized groups: the fallback tiers run in end()
+    (200_000, 150_000, "dups", 3),      # partitioned: the whole call runs inside end()
+    (0, 50_000, "uniform", 0),          # an empty table: whole inside end()
+])
+def test_begin_end_matches_oracle(gpu, oracle_built, nr, ns, kind, parts):
+    """smj_dev_sort_merge_join_begin / _end (the multi-GPU driver's per-stage
+    call): between the halves the host thread may run other GPU work -- a
+    torch kernel on another stream here -- and out is chosen only at end();
+    the result is the oracle's.  A second begin before end is refused."""
+    from smj import _lib, ops
+    rng = np.random.default_rng(nr * 7 + ns)
+    R = table(rng, nr, 2, kind, 0, 0)
+    S = table(rng, ns, 2, kind, 0, 10 ** 9)
+    dR, dS = dev(R).reshape(nr, 2), dev(S).reshape(ns, 2)
+    side = torch.cuda.Stream()
+    ops.force_parts(parts)
+    try:
+        side.wait_stream(torch.cuda.current_stream())
+        job = ops.sort_merge_join_begin(dR, dS, 0, 0, (0, 5000), None, stream=side)
+        with pytest.raises(_lib.SmjError):
+            ops.sort_merge_join_begin(dR, dS, 0, 0, (0, 5000), None, stream=side)
+        busy = torch.randn(1 << 20, device="cuda").sum()  # unrelated work while the job is in flight
+        out = torch.empty((max(min(nr, ns), 1) + 7, 3), dtype=torch.int64, device="cuda")
+        gR, gS, gJ = job.end(out=out[5:])
+        torch.cuda.current_stream().wait_stream(side)
+        assert bool(torch.isfinite(busy))
+        with pytest.raises(RuntimeError):
+            job.end()
+    finally:
+        ops.force_parts(0)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, (0, 5000), None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    if nr and ns:
+        np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    # the thread is free again: a plain call works and agrees
+    g2 = ops.sort_merge_join(dR, dS, 0, 0, (0, 5000), None)
+    np.testing.assert_array_equal(host(g2[2]), host(gJ))
+
+
 def test_single_key_groups_stream(gpu, oracle_built):
     """Heavy keys (over the LDS group capacity) take the no-sort streaming path."""
     from smj import ops

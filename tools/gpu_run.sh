@@ -71,6 +71,11 @@ for s in $STEPS; do
              SMJ_PART_OVERLAP=0 run ab_${w}_off_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_off_$r.out" ${w}_off
            done; done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
+    loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
+    loopab) for r in 1 2 3; do
+              run loop_s$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_s$r.out" loop_split
+              SMJ_DIST_SPLIT=0 run loop_n$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_n$r.out" loop_nosplit
+            done ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
@@ -91,6 +96,9 @@ for s in $STEPS; do
     tr4)   run tr4 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr4" -o c4 -- \
                python3 "$ROOT/bench.py" --workload c4 --steps 2 --warmup 1 $NOCPU
            python3 tools/trace_gaps.py "$OUT/tr4/c4_kernel_trace.csv" --from-kernel msd_sample --top 30 --per msd_part_sample > "$OUT/tr4_gaps.txt" ;;
+    trlp)  run trlp 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trlp" -o loop -- \
+               python3 "$ROOT/bench.py" --loopback --steps 3 --warmup 1 $NOCPU
+           python3 tools/trace_gaps.py "$OUT/trlp/loop_kernel_trace.csv" --from-kernel msd_sample --top 30 --per p1_set_words > "$OUT/trlp_gaps.txt" ;;
     p1)    run p1_base 300 python tools/p1_probe.py && \
            SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/p1abl/libsmj_hip.so run p1_abl 300 python tools/p1_probe.py ;;
     pmcf)  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
