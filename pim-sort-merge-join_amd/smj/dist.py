@@ -122,7 +122,7 @@ _SIDE = {}
 def _side_stream(device):
     s = _SIDE.get(str(device))
     if s is None:
-        s = _SIDE[str(device)] = torch.cuda.Stream(device=device)
+        s = _SIDE[str(device)] = torch.cuda.Stream(device=device, priority=-1)  # like the compute stream
     return s
 
 
