@@ -915,7 +915,10 @@ struct MsdCtx {
     bool pa_fused = false;
 };
 
+thread_local bool t_job_open = false;  // smj_dev_sort_merge_join_begin's job, until its _end
+
 int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, const MsdStage *stg, MsdCtx *cx) {
+    if (t_job_open) return SMJ_ERR_INVALID;  // a begun job owns this thread's scratch until its _end
     for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
         SMJ_TRY(check_table(in[x].n, in[x].cols, in[x].use_sel ? in[x].sel_col : 0, in[x].key));
     if (join && (ntab != 2 || key2 != in[1].key)) return SMJ_ERR_INVALID;
@@ -2023,6 +2026,7 @@ extern "C" int smj_dev_sort_merge_join_begin(const T *R, int64_t nr, int c1, int
         }
     }
     t_job = j;
+    t_job_open = true;
     *job = j;
     return SMJ_OK;
 }
@@ -2031,6 +2035,7 @@ extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
     SmjJob *j = (SmjJob *)job;
     if (!j || j != t_job || !h_rows) return SMJ_ERR_INVALID;
     t_job = nullptr;
+    t_job_open = false;
     std::unique_ptr<SmjJob> own(j);
     h_rows[0] = h_rows[1] = h_rows[2] = 0;
     if (j->whole)

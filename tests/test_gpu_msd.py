@@ -148,7 +148,8 @@ def test_begin_end_matches_oracle(gpu, oracle_built, nr, ns, kind, parts):
     """smj_dev_sort_merge_join_begin / _end (the multi-GPU driver's per-stage
     call): between the halves the host thread may run other GPU work -- a
     torch kernel on another stream here -- and out is chosen only at end();
-    the result is the oracle's.  A second begin before end is refused."""
+    the result is the oracle's.  A second begin, or any other pipeline call,
+    before end is refused."""
     from smj import _lib, ops
     rng = np.random.default_rng(nr * 7 + ns)
     R = table(rng, nr, 2, kind, 0, 0)
@@ -161,6 +162,8 @@ def test_begin_end_matches_oracle(gpu, oracle_built, nr, ns, kind, parts):
         job = ops.sort_merge_join_begin(dR, dS, 0, 0, (0, 5000), None, stream=side)
         with pytest.raises(_lib.SmjError):
             ops.sort_merge_join_begin(dR, dS, 0, 0, (0, 5000), None, stream=side)
+        with pytest.raises(_lib.SmjError):  # the job owns the thread's pipeline scratch until end()
+            ops.sort_merge_join(dR, dS, 0, 0, (0, 5000), None)
         busy = torch.randn(1 << 20, device="cuda").sum()  # unrelated work while the job is in flight
         out = torch.empty((max(min(nr, ns), 1) + 7, 3), dtype=torch.int64, device="cuda")
         gR, gS, gJ = job.end(out=out[5:])
