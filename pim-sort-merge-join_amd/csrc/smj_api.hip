@@ -1239,7 +1239,15 @@ int msd_check(const T *src, int64_t n, int cols, int use_sel, int sel_col, int k
 // key sample of both tables (a key never spans two parts).
 // ---------------------------------------------------------------------------
 constexpr int64_t kMsdSingleMax = 160000000;  // rows per table of one pipeline call (<= 256 pass-B tiles per bucket)
-constexpr int64_t kMsdPartRows = 150000000;          // target rows per table and part
+// Target rows per part of the larger table.  Smaller parts mean fewer pass-B
+// tiles per bucket, i.e. fewer and longer runs per final group (msd_final
+// 17.6 -> 16.0 ms at C4 with 14 parts instead of 7), against a fixed cost per
+// part that the skewed tables' fallback tiers make larger (host round
+// trips, oversized groups).  Same-box sweeps (profiles/r04/r04ze): C4 (equal
+// sizes) 7 parts 61.2-62.2 ms, 14: 58.3-60.4, 20: 58.8, 28: 59.4-59.7; C5
+// (1:10 sizes, Zipf) 7 parts 43.0-43.5, 10: 42.8, 14: 45.0.
+constexpr int64_t kMsdPartRows = 50000000;         // tables of similar size
+constexpr int64_t kMsdPartRowsSkewed = 100000000;  // one table over 1.5x the other (msd_combined's test)
 
 int g_force_parts = 0;  // smj_debug_force_parts: the partitioned mode at any size (tests)
 
@@ -1250,9 +1258,15 @@ int64_t msd_large_parts(const MsdIn *in, int ntab) {
     static const int64_t rows = [] {  // SMJ_PART_ROWS: A/B of the part size
         const char *e = getenv("SMJ_PART_ROWS");
         const int64_t v = e ? (int64_t)atof(e) : 0;
-        return v >= 1000000 && v <= kMsdSingleMax ? v : kMsdPartRows;
+        return v >= 1000000 && v <= kMsdSingleMax ? v : 0;
     }();
-    return std::min<int64_t>(64, (mx + rows - 1) / rows);
+    int64_t lo = in[0].n, hi = in[0].n;
+    for (int x = 1; x < ntab; x++) {
+        lo = std::min(lo, in[x].n);
+        hi = std::max(hi, in[x].n);
+    }
+    const int64_t per = rows ? rows : (ntab > 1 && 2 * hi > 3 * lo) ? kMsdPartRowsSkewed : kMsdPartRows;
+    return std::min<int64_t>(64, (mx + per - 1) / per);
 }
 
 // The one-pass partition (msd_part1_kernel) for tables of up to 8 columns;

@@ -70,6 +70,18 @@ for s in $STEPS; do
              SMJ_PART_CHAIN=1 run ab_${w}_ch_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_ch_$r.out" ${w}_chain
              SMJ_PART_OVERLAP=0 run ab_${w}_off_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/ab_${w}_off_$r.out" ${w}_off
            done; done ;;
+    abparts) for r in 1 2 3 4; do
+             run pr7_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/pr7_$r.out" c4_p7
+             SMJ_PART_ROWS=72000000 run pr14_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/pr14_$r.out" c4_p14
+           done ;;
+    abparts2) for r in 1 2; do
+             for pr in 72000000 50000000 36000000; do
+               SMJ_PART_ROWS=$pr run c4r${pr}_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4r${pr}_$r.out" c4_rows$pr
+             done
+             for pr in 150000000 100000000; do
+               SMJ_PART_ROWS=$pr run c5r${pr}_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5r${pr}_$r.out" c5_rows$pr
+             done
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
