@@ -22,12 +22,12 @@
  *   - row counts must be < 2^31 per table (dpu_block_t.row_num is an int,
  *     common.h:17) and col_num in [1, 1024].  Tables over 1.6e8 rows are
  *     range-partitioned on the key inside the library (in one pass into
- *     part regions of ~1.3x the table of library scratch when the device
+ *     part regions of ~1.3-1.6x the table of library scratch when the device
  *     has room, else counted and scattered in place; the regions stay
  *     allocated for the next call until smj_finalize, and are released
  *     when they cannot all be had; two parts are in flight at once, on two
  *     library streams with two sets of per-part scratch, both kept until
- *     smj_finalize -- ~12 GB each at 1e9 x 1e9), tables over 8 columns
+ *     smj_finalize -- ~5 GB each at 1e9 x 1e9), tables over 8 columns
  *     are sorted as (key, row id) pairs and gathered; the
  *     LSD and partition entry points take 1..8 columns (else
  *     SMJ_ERR_UNSUPPORTED).
