@@ -82,6 +82,18 @@ for s in $STEPS; do
                SMJ_PART_ROWS=$pr run c5r${pr}_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5r${pr}_$r.out" c5_rows$pr
              done
            done ;;
+    c5knobs) for r in 1 2; do
+             for pr in 80000000 100000000 125000000; do
+               SMJ_PART_ROWS=$pr run c5p${pr}_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5p${pr}_$r.out" c5_rows$pr
+             done
+             SMJ_BG_SEG=16384 run c5seg16k_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5seg16k_$r.out" c5_seg16k
+             SMJ_BG_MAX_ROWS=32768 run c5bg32k_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5bg32k_$r.out" c5_bgmax32k
+           done ;;
+    loopk) for r in 1 2; do
+             for k in 2 3 4; do
+               SMJ_DIST_STAGES=$k run loopk${k}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/loopk${k}_$r.out" loop_k$k
+             done
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
