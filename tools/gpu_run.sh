@@ -94,6 +94,14 @@ for s in $STEPS; do
                SMJ_DIST_STAGES=$k run loopk${k}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/loopk${k}_$r.out" loop_k$k
              done
            done ;;
+    abpa)  for r in 1 2 3; do
+             run c3pa0_$r 300 python bench.py $NOCPU && summ "$OUT/c3pa0_$r.out" c3_pa_tile
+             SMJ_PA_PERSIST=1 run c3pa1_$r 300 python bench.py $NOCPU && summ "$OUT/c3pa1_$r.out" c3_pa_persist
+           done
+           for r in 1 2; do
+             run c4pa0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pa0_$r.out" c4_pa_tile
+             SMJ_PA_PERSIST=1 run c4pa1_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pa1_$r.out" c4_pa_persist
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
