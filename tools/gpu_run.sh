@@ -102,6 +102,12 @@ for s in $STEPS; do
              run c4pa0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pa0_$r.out" c4_pa_tile
              SMJ_PA_PERSIST=1 run c4pa1_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pa1_$r.out" c4_pa_persist
            done ;;
+    abp1i) V=$ROOT/pim-sort-merge-join_amd/lib/variants
+           for r in 1 2; do
+             run c4i8_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i8_$r.out" c4_p1items8
+             SMJ_LIB=$V/p1i4/libsmj_hip.so run c4i4_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i4_$r.out" c4_p1items4
+             SMJ_LIB=$V/p1i6/libsmj_hip.so run c4i6_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i6_$r.out" c4_p1items6
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
