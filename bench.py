@@ -233,6 +233,16 @@ def main():
             pmc = json.load(f)
         if pmc.get("rows_per_table") != n or pmc.get("workload", "c3") != a.workload:
             pmc = None
+    if pmc and pmc.get("runs"):
+        # ... and with the same launches per step (the partitioned mode's part
+        # count changes them): a summary of other launches is not attached
+        for name, d in prof.items():
+            k = pmc.get("kernels", {}).get(name)
+            if k and d["launches"] and k["launches"] * psteps != d["launches"] * pmc["runs"]:
+                log(f"PMC summary {a.pmc}: {name} {k['launches']} launches in {pmc['runs']} steps, "
+                    f"this run {d['launches']} in {psteps}: not attached")
+                pmc = None
+                break
     if dom[0]:
         name, d = dom
         ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9

@@ -93,6 +93,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--workload", default="c3", help="bench.py --workload the runs timed (c3 / c4 / c5)")
+    ap.add_argument("--runs", type=int, default=5,
+                    help="bench.py steps the PMC runs executed: warmup + steps + profiling steps (1 + 2 + 2)")
     ap.add_argument("-o", "--out", default="profiles/pmc_traffic.json")
     a = ap.parse_args()
     base = os.path.splitext(a.out)[0]
@@ -106,7 +108,7 @@ def main():
         w = write.get(t, 0.0) / max(nw.get(t, 0), 1)
         kernels[t] = {"launches": nf.get(t, 0), "fetch_kib_raw": round(f, 1),
                       "write_kib": round(w, 1), "hbm_bytes_per_launch": round((2 * f + w) * 1024)}
-    out = {"rows_per_table": a.rows, "workload": a.workload, "source": [fcsv, wcsv],
+    out = {"rows_per_table": a.rows, "workload": a.workload, "runs": a.runs, "source": [fcsv, wcsv],
            "raw_runs": [a.fetch_dir, a.write_dir],
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB per scope launch (gfx950: FETCH_SIZE "
                          "counts half of a wide coalesced read; MI355X_MICROARCH.md, HBM)",
