@@ -956,10 +956,18 @@ __device__ __forceinline__ void runs_apply_body(const uint32_t *__restrict__ off
                                                              const MsdBucket *__restrict__ bk,
                                                              uint2 *__restrict__ list, uint2 *__restrict__ tinfo) {
     const int lane = threadIdx.x & 63;
-    const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // XCD-aware block order: the eight workgroups whose bucket quads share
+    // one 128-B offsA line (quads 8j .. 8j + 7 of one segment) get linear ids
+    // p = 64 m + 8 r + x -- the same x, i.e. the same XCD (workgroups are
+    // dealt round-robin over the 8 XCDs), one after another -- so the line
+    // is fetched into one L2 once instead of into eight
+    const uint32_t p = blockIdx.x + blockIdx.y * gridDim.x;
+    const uint32_t x = p & 7u, r = (p >> 3) & 7u, sj = (p >> 6) * 8u + x;
+    const uint32_t seg = sj >> 3, quad = (sj & 7u) * 8u + r;
+    const int a = (int)quad * 4 + (threadIdx.x >> 6);
     const int64_t Ls = (ntiles + kMsdSegs - 1) / kMsdSegs;
-    const int64_t c0 = min((int64_t)blockIdx.y * Ls, ntiles), c1 = min(c0 + Ls, ntiles);
-    uint32_t P = segL[blockIdx.y * kOffsA + a], Q = segC[blockIdx.y * kOffsA + a];  // exclusive prefixes
+    const int64_t c0 = min((int64_t)seg * Ls, ntiles), c1 = min(c0 + Ls, ntiles);
+    uint32_t P = segL[seg * kOffsA + a], Q = segC[seg * kOffsA + a];  // exclusive prefixes
     const uint32_t lbase = uni32(bk[a].list_base), tbase = uni32(bk[a].tile_base);
     const uint32_t uT = (uint32_t)TB;  // pass-B tile rows (T: pass-A tile rows)
     for (int64_t t0 = c0; t0 < c1; t0 += 64) {
@@ -4501,6 +4509,7 @@ hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
 
 hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s) {
     static_assert(kBucketsA % 4 == 0, "four buckets (waves) per workgroup");
+    static_assert(kBucketsA / 4 == 64 && kMsdSegs % 8 == 0, "runs_apply_body's XCD-aware block order");
     const dim3 grid(kBucketsA / 4, kMsdSegs, a.ntab);
     hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();

@@ -108,6 +108,15 @@ for s in $STEPS; do
              SMJ_LIB=$V/p1i4/libsmj_hip.so run c4i4_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i4_$r.out" c4_p1items4
              SMJ_LIB=$V/p1i6/libsmj_hip.so run c4i6_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i6_$r.out" c4_p1items6
            done ;;
+    abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
+           for r in 1 2 3; do
+             run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
+             SMJ_LIB=$V run c3base_$r 300 python bench.py $NOCPU && summ "$OUT/c3base_$r.out" c3_base
+           done
+           for r in 1 2; do
+             run c4new_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4new_$r.out" c4_new
+             SMJ_LIB=$V run c4base_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4base_$r.out" c4_base
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
