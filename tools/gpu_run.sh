@@ -117,6 +117,14 @@ for s in $STEPS; do
              run c4new_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4new_$r.out" c4_new
              SMJ_LIB=$V run c4base_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4base_$r.out" c4_base
            done ;;
+    abpbo) for r in 1 2 3; do
+             run c3o1_$r 300 python bench.py $NOCPU && summ "$OUT/c3o1_$r.out" c3_order
+             SMJ_PB_ORDER=0 run c3o0_$r 300 python bench.py $NOCPU && summ "$OUT/c3o0_$r.out" c3_plain
+           done
+           for r in 1 2; do
+             run c4o1_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4o1_$r.out" c4_order
+             SMJ_PB_ORDER=0 run c4o0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4o0_$r.out" c4_plain
+           done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
