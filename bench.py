@@ -24,6 +24,14 @@ they run through the library's partitioned mode; under torchrun (or
 generates its contiguous slice, global rows [r n / W, (r + 1) n / W) (row0 =
 r n / W: the generators are functions of the global row, so the tables do not
 depend on W), then the range partition + RCCL exchange of smj/dist.py.
+
+Every line carries "verified" (after the timed steps, outside them): under
+torchrun / --loopback each rank digests its slice of the joined rows at its
+global position (smj_dev_digest, order-sensitive) and rank 0 compares them with
+the single-GPU call on the whole job's tables; at N = 1 the timed step's sorted
+tables and joined rows are compared with the CPU port's (oracle/cpu_mt.cpp, the
+cpu_baseline_mt leg).  A mismatch prints the line with "verified": false and
+exits 3 on every rank.
 """
 import argparse
 import json
@@ -84,6 +92,10 @@ def parse():
     p.add_argument("--loopback", action="store_true",
                    help="N = 1 through the distributed path (smj.dist, RCCL process group of one rank, "
                         "own segments sent to itself): the multi-GPU pipeline's cost without cross-GPU traffic")
+    p.add_argument("--verify", type=int, default=1,
+                   help="after the timed steps, check the result: distributed / --loopback against the single-GPU "
+                        "call on the whole job's tables (rank 0), N = 1 against the CPU port (--cpu-mt); "
+                        "a mismatch exits 3 (0 = skip)")
     p.add_argument("--pmc", default=None,
                    help="committed rocprofv3 PMC traffic summary for the roofline 'traffic' field "
                         "(default: profiles/pmc_traffic.json for c3, profiles/pmc_traffic_<workload>.json otherwise)")
@@ -109,9 +121,57 @@ def workload_name(w, world, distributed):
 def step_single(R, S, bufs):
     """One pass of the hot path: the fused MSD pipeline (select + stable sort of
     R and S, 1:1 zip join; sorted tables and joined rows all written)."""
-    _, _, J = ops.sort_merge_join(R, S, KEYS[0], KEYS[1], (SELECT[0], SELECT[1]), (SELECT[2], SELECT[3]),
-                                  R_sorted=bufs["R"], S_sorted=bufs["S"], out=bufs["J"])
-    return J.shape[0]
+    Rs, Ss, J = ops.sort_merge_join(R, S, KEYS[0], KEYS[1], (SELECT[0], SELECT[1]), (SELECT[2], SELECT[3]),
+                                    R_sorted=bufs["R"], S_sorted=bufs["S"], out=bufs["J"])
+    return (Rs.shape[0], Ss.shape[0], J.shape[0])
+
+
+MASK64 = (1 << 64) - 1
+
+
+def verify_distributed(J, rank, world, dev, full_tables):
+    """Self-check of a distributed (or --loopback) result, after the timed
+    steps: every rank digests its slice of the joined rows at its global
+    position (smj_dev_digest: order-sensitive, position-mixed), the digests
+    and row counts are gathered, and rank 0 runs the single-GPU call
+    (smj_dev_sort_merge_join, the partitioned mode above 1.6e8 rows) on the
+    whole job's tables -- full_tables() makes them -- and digests the same
+    slices of its result.  Returns (ok on every rank, details on rank 0).
+    The reference order is the one the reference's host builds by
+    concatenating DPU outputs in DPU order (app.c:585-692)."""
+    t0 = time.perf_counter()
+    cnt = torch.tensor([J.shape[0]], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(allc, cnt)
+    counts = [int(c.item()) for c in allc]
+    offs = [sum(counts[:r]) for r in range(world)]
+    d = ops.digest_async(J, offs[rank])
+    alld = [torch.zeros_like(d) for _ in range(world)]
+    dist.all_gather(alld, d)
+    got = [int(x.item()) & MASK64 for x in alld]
+    flag = torch.zeros(1, dtype=torch.int64, device=dev)
+    info = None
+    if rank == 0:
+        torch.cuda.empty_cache()  # the distributed path's cached blocks, for the library's own allocations
+        Rf, Sf = full_tables()
+        _, _, Jf = ops.sort_merge_join(Rf, Sf, KEYS[0], KEYS[1], (SELECT[0], SELECT[1]), (SELECT[2], SELECT[3]))
+        total = Jf.shape[0]
+        ref = [ops.digest(Jf[offs[r]: offs[r] + counts[r]], offs[r]) if offs[r] + counts[r] <= total else None
+               for r in range(world)]
+        whole = ops.digest(Jf)
+        bad = [r for r in range(world) if ref[r] != got[r]]
+        ok = not bad and sum(counts) == total and (sum(got) & MASK64) == whole
+        flag.fill_(1 if ok else 0)
+        info = {"ok": ok, "against": "single-GPU smj_dev_sort_merge_join on the whole job's tables (rank 0)",
+                "joined_rows": sum(counts), "reference_joined_rows": total, "digest": "%016x" % (sum(got) & MASK64),
+                "reference_digest": "%016x" % whole, "mismatched_ranks": bad,
+                "seconds": None}
+        del Rf, Sf, Jf
+        torch.cuda.empty_cache()
+    dist.broadcast(flag, 0)
+    if info is not None:
+        info["seconds"] = round(time.perf_counter() - t0, 2)
+    return bool(flag.item()), info
 
 
 def main():
@@ -203,7 +263,22 @@ def main():
         log(f"msd stats (single-key groups, LSD-fallback groups, mR, mS): {ops.msd_stats()}; "
             f"(groups, radix-tier, wide-tier, in-LDS LSD): {ops.msd_groups()}")
 
-    joined = int(res) if not distributed else int(res.shape[0])
+    joined = int(res[2]) if not distributed else int(res.shape[0])
+
+    def full_tables():  # the whole job's tables (rank 0's verification call)
+        if world == 1:
+            return R, S
+        if a.workload == "c5":
+            return (ops.gen_zipf(NR, row0=0, seed=3, domain=100_000_000, theta=0.9, device=dev),
+                    ops.gen_zipf(NS, row0=0, seed=4, domain=100_000_000, theta=0.9, device=dev))
+        return (ops.gen_uniform(NR, row0=0, seed=1, key_range=key_range, device=dev),
+                ops.gen_uniform(NS, row0=0, seed=2, key_range=key_range, device=dev))
+
+    verified, verification = None, None
+    if distributed and a.verify:
+        verified, verification = verify_distributed(res, rank, world, dev, full_tables)
+        if rank == 0:
+            log(f"verification: {verification}")
     rank_rows = [nr + ns]  # every rank's generated input rows (R + S), rank order
     if world > 1:
         got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
@@ -308,13 +383,28 @@ def main():
         # (OMP_NUM_THREADS on the GPU box), else every core the process is affine to
         usable = len(os.sched_getaffinity(0))
         threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or usable, usable)
-        secs, rows = oracle.mt_pipeline(R.cpu().numpy(), S.cpu().numpy(), SELECT, KEYS, threads)
-        assert rows[2] == joined, "CPU port disagrees with the GPU join count"
+        secs, rows, outs = oracle.mt_pipeline(R.cpu().numpy(), S.cpu().numpy(), SELECT, KEYS, threads,
+                                              outputs=True)
         cpu_mt = {"value": round(2 * n / secs, 1), "unit": "rows/s", "cores": threads, "kind": "port",
                   "sample": f"the full workload ({n} x {n} rows): oracle/cpu_mt.cpp, cpu_app.c's select + "
                             f"stable sort + zip join on {threads} threads (the host cores granted to this GPU's "
                             f"job; {usable} usable, {os.cpu_count()} in the node) (chunk sort + merge rounds), g++ -O3; "
-                            f"{secs:.2f} s, {rows[2]} joined rows (equal to the GPU's)"}
+                            f"{secs:.2f} s, {rows[2]} joined rows"}
+        # the timed GPU step's outputs (last step: the same deterministic result)
+        # against the CPU port's, by the order-sensitive digest (smj_dev_digest
+        # on the device, its C restatement oracle.digest on the host)
+        if a.verify:
+            gpu_out = (bufs["R"][: res[0]], bufs["S"][: res[1]], bufs["J"][: res[2]])
+            dg = [ops.digest(t) for t in gpu_out]
+            dc = [oracle.digest(t) for t in outs]
+            ok = tuple(res) == tuple(rows) and dg == dc
+            verified = ok
+            verification = {"ok": ok, "against": "oracle/cpu_mt.cpp on the full workload (sorted R, sorted S, "
+                                                 "joined rows: row counts + order-sensitive digests)",
+                            "rows": list(res), "cpu_rows": list(rows),
+                            "digests": ["%016x" % x for x in dg], "cpu_digests": ["%016x" % x for x in dc]}
+            log(f"verification: {verification}")
+        del outs
 
     if rank == 0:
         line = {
@@ -339,10 +429,15 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_mt": cpu_mt,
             "sort_passes": sort_passes,
+            "verified": verified,
+            "verification": verification,
         }
         emit(line)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
+    if verified is False:
+        log("VERIFICATION FAILED: the result differs from the reference call")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

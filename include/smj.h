@@ -298,6 +298,19 @@ int smj_dev_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, in
 /* sum_{i=1..n} i^-theta (host). */
 double smj_zipf_zeta(int64_t n, double theta);
 
+/* Order-sensitive digest of a row-major table slice whose first row sits at
+ * global position pos0:
+ *   *d_digest (DEVICE uint64) = sum_i h(pos0 + i, row i) mod 2^64, with
+ *   h(p, r) = f(... f(f(mix(p ^ 0x5851F42D4C957F2D) + r[0]) + r[1]) ... + r[c-1])
+ * and mix = splitmix64's finaliser (x += 0x9E3779B97F4A7C15 then the two
+ * xor-shift-multiply rounds).  Digests of consecutive slices at their global
+ * positions sum to the digest of the whole, so a distributed result (one slice
+ * per rank, rank order) is checked against a single call by adding numbers.
+ * Async.  (The reference has no result checker at all -- SURVEY 4: no tests;
+ * this is the verification the multi-GPU bench line carries.) */
+int smj_dev_digest(const int64_t *rows, int64_t n_rows, int col_num, int64_t pos0, uint64_t *d_digest,
+                   void *stream);
+
 /* ---- T = UINT64 / DOUBLE (common.h:3-9) ------------- */
 /* The fused pipeline with keys and select values compared as key_type
  * (uint64 or IEEE double, as cpu_app.c compiled with that T): tables are

@@ -288,6 +288,18 @@ uint64_t smj_ref_splitmix64(uint64_t x)
     return x ^ (x >> 31);
 }
 
+uint64_t smj_ref_digest(const void *rows, int64_t row_num, int col_num, int64_t pos0)
+{
+    const uint64_t *r = (const uint64_t *)rows;
+    uint64_t acc = 0;
+    for (int64_t i = 0; i < row_num; i++) {
+        uint64_t h = smj_ref_splitmix64((uint64_t)(pos0 + i) ^ 0x5851F42D4C957F2DULL);
+        for (int c = 0; c < col_num; c++) h = smj_ref_splitmix64(h + r[i * col_num + c]);
+        acc += h;
+    }
+    return acc;
+}
+
 void smj_ref_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t key_range)
 {
     const uint64_t salt = seed * 0xD1B54A32D192ED03ULL;

@@ -83,6 +83,12 @@ void smj_ref_gen_uniform(T *out, int64_t row0, int64_t rows, uint64_t seed, uint
  * device generator's restatement; zetan = sum_{i<=n} i^-theta). */
 void smj_ref_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t n, double theta, double zetan);
 
+/* The checker's side of smj_dev_digest (include/smj.h): sum over rows i of
+ * h(pos0 + i, row i) mod 2^64, h(p, r) = f(..f(f(m(p ^ 0x5851F42D4C957F2D) +
+ * r[0]) + r[1]).. + r[c-1]), f = m = splitmix64 (cells as their 64-bit
+ * patterns).  Not part of cpu_app.c: the reference has no result checker. */
+uint64_t smj_ref_digest(const void *rows, int64_t row_num, int col_num, int64_t pos0);
+
 #ifdef __cplusplus
 }
 #endif

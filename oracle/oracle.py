@@ -67,6 +67,8 @@ def _bind(l, ktype):
     l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
     l.smj_ref_gen_zipf.restype = None
     l.smj_ref_gen_zipf.argtypes = [_P, _L, _L, ctypes.c_uint64, _L, ctypes.c_double, ctypes.c_double]
+    l.smj_ref_digest.restype = ctypes.c_uint64
+    l.smj_ref_digest.argtypes = [_P, _L, ctypes.c_int, _L]
     l.smj_ref_csv_size.restype = ctypes.c_int
     l.smj_ref_csv_size.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     l.smj_ref_load_csv.restype = ctypes.c_int
@@ -142,6 +144,33 @@ def gen_uniform(rows, row0=0, seed=1, key_range=None):
     out = np.empty((rows, 2), dtype=np.int64)
     lib().smj_ref_gen_uniform(out.ctypes.data_as(_P), row0, rows, seed, key_range)
     return out
+
+
+def digest(table, pos0=0):
+    """The checker's restatement of smj_dev_digest (include/smj.h): an
+    order-sensitive sum of per-row hashes of (global position, cells)."""
+    t = np.ascontiguousarray(table)
+    if t.dtype.itemsize != 8 or t.ndim != 2:
+        raise ValueError("digest: 2-D table of 8-byte cells")
+    return int(lib().smj_ref_digest(t.ctypes.data_as(_P), t.shape[0], max(t.shape[1], 1), int(pos0)))
+
+
+def digest_np(table, pos0=0):
+    """The same digest in numpy (an independent restatement for the tests)."""
+    t = np.ascontiguousarray(table).view(np.uint64)
+    M = np.uint64
+
+    def mix(x):
+        x = x + M(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> M(30))) * M(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> M(27))) * M(0x94D049BB133111EB)
+        return x ^ (x >> M(31))
+
+    with np.errstate(over="ignore"):
+        h = mix(np.arange(pos0, pos0 + t.shape[0], dtype=np.int64).view(np.uint64) ^ M(0x5851F42D4C957F2D))
+        for c in range(t.shape[1]):
+            h = mix(h + t[:, c])
+        return int(h.sum(dtype=np.uint64))
 
 
 def zipf_zeta(n, theta):

@@ -581,30 +581,46 @@ int msd_scratch(MsdScratch **out) {
 
 std::map<int, std::array<hipStream_t, 2>> g_part_streams;  // msd_large's part streams per scratch key
 
+void msd_free_one(MsdScratch &m) {  // also a set whose creation failed half-way (dev still -1)
+    if (m.dev >= 0) hipSetDevice(m.dev);
+    for (auto &t : m.t)
+        for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb, t.fb2})
+            hipFree(p);
+    for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
+                    (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
+                    (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
+                    (void *)m.p1c, m.p1desc[0], m.p1desc[1]})
+        hipFree(p);
+    hipHostFree(m.p1h);
+    hipHostFree(m.h_p1c);
+    hipHostFree(m.h_pick);
+    hipHostFree(m.h_work);
+    hipHostFree(m.h_plan);
+    hipHostFree(m.h_samp);
+    m = MsdScratch{};
+}
+
 void msd_free_all() {
     for (auto &kv : g_part_streams)
         for (hipStream_t st : kv.second) hipStreamDestroy(st);
     g_part_streams.clear();
-    for (auto &kv : g_msd) {
-        MsdScratch &m = kv.second;
-        if (m.dev < 0) continue;
-        hipSetDevice(m.dev);
-        for (auto &t : m.t)
-            for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb, t.fb2})
-                hipFree(p);
-        for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
-                        (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
-                        (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
-                        (void *)m.p1c, m.p1desc[0], m.p1desc[1]})
-            hipFree(p);
-        hipHostFree(m.p1h);
-        hipHostFree(m.h_p1c);
-        hipHostFree(m.h_pick);
-        hipHostFree(m.h_work);
-        hipHostFree(m.h_plan);
-        hipHostFree(m.h_samp);
-    }
+    for (auto &kv : g_msd) msd_free_one(kv.second);
     g_msd.clear();
+}
+
+// Releases this thread's scratch set `var` on the current device (nothing of
+// it may be in flight): the partitioned mode's second set when it could not
+// all be had.
+void msd_release_var(int var) {
+    int dev = 0;
+    const int base = scratch_key(&dev);
+    if (base < 0) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_msd.find(base + (var << 20));
+    if (it == g_msd.end()) return;
+    msd_free_one(it->second);
+    g_msd.erase(it);
+    hipSetDevice(dev);
 }
 
 struct MsdIn {            // one input table of the pipeline
@@ -1729,13 +1745,37 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         };
         SMJ_TRY(front(0));
         hm.mark("f0");
+        // seq: the second scratch set could not be allocated (its front
+        // returned SMJ_ERR_NOMEM before the part was fully launched): the part
+        // whose back is due still finishes on its own set, set 1 is released,
+        // and the remaining parts run one after another on set 0 -- the memory
+        // the sequential path needs
+        bool seq = false;
         for (int p = 0; p <= nspl; p++) {
-            if (p < nspl) SMJ_TRY(front(p + 1));
-            t_msd_var = p & 1;
             int64_t rows[3] = {0, 0, 0};
+            if (seq) {
+                t_msd_var = 0;
+                SMJ_TRY(msd_run(&parts[2 * (size_t)p], 2, 1, key2, out_j + J * tc, rows, ps[0]));
+                J += rows[2];
+                continue;
+            }
+            if (p < nspl) {
+                const int rc = front(p + 1);
+                if (rc == SMJ_ERR_NOMEM) seq = true;
+                else SMJ_TRY(rc);
+            }
+            t_msd_var = p & 1;
             SMJ_TRY(msd_back(cx[p], out_j + J * tc, rows, ps[p & 1]));
             J += rows[2];
             hm.mark("b");
+            if (seq) {
+                HIP_TRY(hipStreamSynchronize(ps[0]));
+                HIP_TRY(hipStreamSynchronize(ps[1]));
+                t_msd_var = 0;
+                msd_release_var(1);
+                if (getenv("SMJ_DEBUG_PART1"))
+                    fprintf(stderr, "smj: partitioned mode: no room for a second scratch set; parts %d.. in turn\n", p + 1);
+            }
         }
         h_rows[2] = J;
         return SMJ_OK;
@@ -2493,6 +2533,14 @@ extern "C" int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t see
     if (rows < 0 || (rows && !out) || domain < 2 || !(theta > 0 && theta < 1)) return SMJ_ERR_INVALID;
     if (rows == 0) return SMJ_OK;
     HIP_TRY(launch_gen_zipf(out, row0, rows, seed, domain, theta, zeta_n, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_digest(const T *rows, int64_t n_rows, int col_num, int64_t pos0, uint64_t *d_digest,
+                              void *stream) {
+    if (n_rows < 0 || (n_rows && !rows) || !d_digest || col_num < 1 || col_num > SMJ_MAX_COLS || pos0 < 0)
+        return SMJ_ERR_INVALID;
+    HIP_TRY(launch_digest(rows, n_rows, col_num, pos0, d_digest, (hipStream_t)stream));
     return SMJ_OK;
 }
 

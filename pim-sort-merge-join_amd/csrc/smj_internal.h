@@ -143,6 +143,8 @@ hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t
                               uint64_t key_range, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
                            double theta, double zeta_n, hipStream_t s);
+// *out = sum over rows i of hash(pos0 + i, row i) mod 2^64 (smj_dev_digest)
+hipError_t launch_digest(const int64_t *rows, int64_t n, int cols, int64_t pos0, uint64_t *out, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // MSD sample-sort pipeline (smj_msd.hip): sample -> part_a -> runs -> part_b

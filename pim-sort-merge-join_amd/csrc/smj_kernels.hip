@@ -1047,8 +1047,41 @@ __global__ void gen_zipf_kernel(int64_t *out, int64_t row0, int64_t rows, uint64
 }
 
 // ---------------------------------------------------------------------------
+// order-sensitive table digest (smj_dev_digest): sum over rows of a hash of
+// (global position, every cell), mod 2^64.  Sums of slices at their global
+// positions add up to the digest of the whole, so per-rank digests of a
+// distributed result can be checked against one single-GPU call.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t digest_row(uint64_t pos, const int64_t *r, int cols) {
+    uint64_t h = splitmix64(pos ^ 0x5851F42D4C957F2Dull);
+    for (int c = 0; c < cols; c++) h = splitmix64(h + (uint64_t)r[c]);
+    return h;
+}
+
+__global__ __launch_bounds__(256) void digest_kernel(const int64_t *__restrict__ rows, int64_t n, int cols,
+                                                     int64_t pos0, unsigned long long *out) {
+    uint64_t acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        acc += digest_row((uint64_t)(pos0 + i), rows + i * cols, cols);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    __shared__ uint64_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+
+hipError_t launch_digest(const int64_t *rows, int64_t n, int cols, int64_t pos0, uint64_t *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), s);
+    if (e != hipSuccess || n <= 0) return e;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(n, 256), 4096));
+    hipLaunchKernelGGL(digest_kernel, dim3(grid), dim3(256), 0, s, rows, n, cols, pos0, (unsigned long long *)out);
+    return hipGetLastError();
+}
 
 // Ablation switches for profiling builds of the bench tools only (unset in
 // production): SMJ_DEBUG_PASS bit0 = no look-back, bit1 = no HBM stores,

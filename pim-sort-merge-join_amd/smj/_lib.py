@@ -66,6 +66,7 @@ SIGNATURES = {
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),
+    "smj_dev_digest": (_I, [_P, _L, _I, _L, _P, _P]),
     "smj_debug_msd_stats": (None, [_PL]),
     "smj_debug_msd_groups": (None, [_PL]),
     "smj_debug_msd_tiers": (None, [_PL]),

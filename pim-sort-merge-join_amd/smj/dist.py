@@ -30,8 +30,9 @@ point-to-point sends / receives (RCCL group over xGMI; received chunks
 placed in source-rank order) while the local pipeline sorts and joins stage
 k - 1's sub-range: sort and zip join are per-key operations, so the stage
 outputs concatenated in stage order are the rank's slice of the result.
-S is counted first (a read-only pass), so the cuts are known once R is
-partitioned and R's stage-0 rows travel while S is being partitioned.
+The cuts use R's exact counts and S's sample estimate, so they are known once
+R is partitioned, and R's stage-0 rows travel while S is being partitioned (on
+a side stream, so the transfers are not ordered behind it).
 
 Concatenating the per-rank outputs in rank order is exactly cpu_app.c's
 result (stable sort + zip join are per-key operations on disjoint key ranges).
@@ -116,13 +117,13 @@ class _Tracer:
 # one blocking call per stage on the current stream, after the next stage's
 # transfers are posted)
 SPLIT_STAGES = os.environ.get("SMJ_DIST_SPLIT", "1") != "0"
-_SIDE = {}
+_SPLIT_SIDE = {}  # device -> the stage pipelines' side stream
 
 
 def _side_stream(device):
-    s = _SIDE.get(str(device))
+    s = _SPLIT_SIDE.get(str(device))
     if s is None:
-        s = _SIDE[str(device)] = torch.cuda.Stream(device=device, priority=-1)  # like the compute stream
+        s = _SPLIT_SIDE[str(device)] = torch.cuda.Stream(device=device, priority=-1)  # like the compute stream
     return s
 
 
@@ -466,7 +467,9 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     (optional dict) gets the rows this rank received per table and the
     max / mean load over ranks (load-balance report).  stages: key sub-ranges
     per rank whose exchange overlaps the previous one's sort + join
-    (default SMJ_DIST_STAGES or 2; 1 = exchange everything, then compute).
+    (default SMJ_DIST_STAGES, else default_stages(W): 3 on one rank, 4 at
+    W > 1, lowered by stage_count to what the partition fits; 1 = exchange
+    everything, then compute).
     loopback (default SMJ_DIST_LOOPBACK=1): the rank's own segments also go
     through send / receive to itself, and a single rank takes the whole
     distributed path (exercises the RCCL transport on one GPU).
@@ -543,7 +546,16 @@ def _repartition(ops, T, bounds, k, sc, sv):
     return ops.partition_apply(T, bounds, plan, k, sc, sv)
 
 
-_SIDE = {}
+_GATHER_SIDE = {}  # device -> the count gathers' host-copy stream
+S_SIDE = os.environ.get("SMJ_DIST_S_SIDE", "1") != "0"
+_S_SIDE = {}  # device -> the stream S's partition runs on
+
+
+def _s_stream(device):
+    s = _S_SIDE.get(str(device))
+    if s is None:
+        s = _S_SIDE[str(device)] = torch.cuda.Stream(device=device, priority=-1)
+    return s
 
 
 class _HostGather:
@@ -560,9 +572,9 @@ class _HostGather:
             return
         self.outs = [torch.empty_like(t) for _ in range(world)]
         work = dist.all_gather(self.outs, t, group=group, async_op=True)  # ordered after t's producer
-        side = _SIDE.get(t.device)
+        side = _GATHER_SIDE.get(str(t.device))
         if side is None:
-            side = _SIDE[t.device] = torch.cuda.Stream(device=t.device)
+            side = _GATHER_SIDE[str(t.device)] = torch.cuda.Stream(device=t.device)
         with torch.cuda.stream(side):
             work.wait()
             self.host = torch.empty((world, t.numel()), dtype=t.dtype, pin_memory=True)
@@ -593,23 +605,44 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     nb = len(bounds) + 1
     tabs = [(R, k1, sc1, sv1), (S, k2, sc2, sv2)]
     wire = _wire_device(R, group)
-    # R partitioned (one read), its counts gathered -- the host copy waits for
-    # that gather only -- while S is partitioned behind it on the compute
-    # stream; the cuts come from R's exact counts and S's sample estimate (any
-    # (bucket, occurrence) cut is valid: R and S apply the same one), so R's
-    # first stage leaves before S's partition has finished (round 4; before,
-    # nothing left until both tables were counted)
+    # R partitioned (one read) on the compute stream and its counts gathered
+    # -- the host copy waits for that gather only.  S is partitioned on a side
+    # stream (S_SIDE), so that R's stage-0 transfers, posted as soon as R's
+    # counts are known, do not wait for it: the process group orders its
+    # work after the CURRENT stream (R's partition only), and S's count gather
+    # is issued after R's stage 0 from the side stream (waiting for S's
+    # partition only).  The cuts come from R's exact counts and S's sample
+    # estimate (any (bucket, occurrence) cut is valid: R and S apply the same
+    # one).  Round 4 issued both partitions and both gathers on the compute
+    # stream first, so the stage-0 transfers queued behind S's partition and
+    # only the host's wait was removed; SMJ_DIST_S_SIDE=0 keeps
+    # that order.
     cnt = [torch.empty(nb + 1, dtype=torch.int64, device=R.device) for _ in range(2)]
+    cur = torch.cuda.current_stream(R.device) if R.is_cuda else None
+    sside = _s_stream(R.device) if (R.is_cuda and S_SIDE) else None
+    if sside is not None:
+        sside.wait_stream(cur)  # everything before this step (buffers it may reuse) first
     part = [_partition(ops, R, bounds, cnt[0], own[0], k1, sc1, sv1)]
     gR = _HostGather(cnt[0], world, group)
-    part.append(_partition(ops, S, bounds, cnt[1], own[1], k2, sc2, sv2))
-    gS = _HostGather(cnt[1], world, group)
+    if sside is not None:
+        with torch.cuda.stream(sside):
+            part.append(_partition(ops, S, bounds, cnt[1], own[1], k2, sc2, sv2))
+        gS = None
+    else:
+        part.append(_partition(ops, S, bounds, cnt[1], own[1], k2, sc2, sv2))
+        gS = _HostGather(cnt[1], world, group)
     counts, sends, regs, sl = [None, None], [None, None], [None, None], [None, None]
 
     def finish(t, allc):  # this table's exact counts: overflow fix-up, send buffer, row ranges
+        # flag word bit 1: a look-back timed out on that rank (a bug; its
+        # prefixes, and with them every rank's cuts, would be wrong) -- every
+        # rank sees every flag, so all raise together instead of hanging
+        late = [r for r in range(world) if allc[r][nb] & 2]
+        if late:
+            raise RuntimeError(f"smj.dist: the partition's look-back timed out on rank(s) {late} (table {t})")
         counts[t] = [allc[r][:nb] for r in range(world)]
         buf, reg = part[t]
-        if reg is not None and allc[rank][nb]:  # a region overflowed: the counting partition
+        if reg is not None and allc[rank][nb] & 1:  # a region overflowed: the counting partition
             T, k, sc, sv = tabs[t]
             buf, reg = _repartition(ops, T, bounds, k, sc, sv), None
         if reg is None:  # bucket-contiguous
@@ -628,7 +661,13 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     cuts = choose_cuts(GR, GSe, single, nseg, fracs)
     finish(0, allcR)
     pending = [post_stage(0, K, [sends[0], None], regs, sl, rank, world, R.device, group, loopback)]  # R's stage 0
-    finish(1, gS.result())  # host sync 3 (S's counts)
+    if gS is None:
+        with torch.cuda.stream(sside):
+            gS = _HostGather(cnt[1], world, group)
+    allcS = gS.result()  # host sync 3 (S's counts)
+    if sside is not None:
+        cur.wait_stream(sside)  # S's partition before anything that reads its buffer on the compute stream
+    finish(1, allcS)
     tr("partition S + counts; R stage 0 posted")
     pending.append(post_stage(0, K, [None, sends[1]], regs, sl, rank, world, R.device, group, loopback))
     seg = [[[sum(hi - lo for (_, lo, hi) in sl[t][r][j]) for j in range(nseg)] for r in range(world)]

@@ -136,20 +136,51 @@ class SortMergeJoinJob:
         self.R_sorted, self.S_sorted, self._stream = R_sorted, S_sorted, stream
 
     def end(self, out=None):
+        """Finish the job.  The C job is released whatever happens here: an
+        unusable `out` still ends it (the C call drains the stream and frees
+        the thread's pipeline) before the error is raised."""
         if self._h is None:
             raise RuntimeError("job already ended")
         R, S = self._keep
         nr, c1 = R.shape
         ns, c2 = S.shape
-        if out is None:
-            out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=torch.int64, device=R.device)
-        else:
-            _out(out, "out", min(nr, ns), c1 + c2 - 1, R)
-        rows = (ctypes.c_int64 * 3)()
         h, self._h = self._h, None
-        _lib.check(self._lib.smj_dev_sort_merge_join_end(h, _ptr(out), rows), "smj_dev_sort_merge_join_end")
+        rows = (ctypes.c_int64 * 3)()
+        try:
+            if out is None:
+                out = torch.empty((max(min(nr, ns), 1), c1 + c2 - 1), dtype=torch.int64, device=R.device)
+            else:
+                _out(out, "out", min(nr, ns), c1 + c2 - 1, R)
+        except BaseException:
+            self._lib.smj_dev_sort_merge_join_end(h, None, rows)  # returns SMJ_ERR_INVALID, job released
+            self._keep = None
+            raise
+        rc = self._lib.smj_dev_sort_merge_join_end(h, _ptr(out), rows)
         self._keep = None
+        _lib.check(rc, "smj_dev_sort_merge_join_end")
         return self.R_sorted[: rows[0]], self.S_sorted[: rows[1]], out[: rows[2]]
+
+    def abandon(self):
+        """End a job whose result is not wanted (waits for its kernels)."""
+        if self._h is not None:
+            h, self._h = self._h, None
+            self._lib.smj_dev_sort_merge_join_end(h, None, (ctypes.c_int64 * 3)())
+            self._keep = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.abandon()  # a job not ended inside the block
+        return False
+
+    def __del__(self):
+        # a job dropped without end() would keep its thread's pipeline scratch
+        # (every later pipeline call on the thread returns SMJ_ERR_INVALID)
+        try:
+            self.abandon()
+        except Exception:
+            pass
 
 
 def sort_merge_join_begin(R, S, key1=0, key2=0, select1=None, select2=None, R_sorted=None, S_sorted=None,
@@ -467,6 +498,32 @@ def gen_zipf(rows, row0=0, seed=3, domain=100_000_000, theta=0.9, device="cuda",
     _lib.check(lib.smj_dev_gen_zipf(_ptr(out), row0, rows, seed, domain, theta, zeta, _stream(stream)),
                "smj_dev_gen_zipf")
     return out
+
+
+MASK64 = (1 << 64) - 1
+
+
+def digest_async(table, pos0=0, out=None, stream=None):
+    """smj_dev_digest of `table` (rows at global positions pos0, pos0 + 1, ...)
+    into out (a 1-element int64 CUDA tensor holding the uint64 bits;
+    allocated if None), without a host synchronisation.  Returns out."""
+    lib = _lib.load()
+    if not (isinstance(table, torch.Tensor) and table.is_cuda and table.element_size() == 8 and table.dim() == 2
+            and table.is_contiguous()):
+        raise ValueError("table must be a contiguous 2-D 8-byte CUDA tensor")
+    if out is None:
+        out = torch.empty(1, dtype=torch.int64, device=table.device)
+    _lib.check(lib.smj_dev_digest(_ptr(table), table.shape[0], max(table.shape[1], 1), int(pos0),
+                                  ctypes.c_void_p(out.data_ptr()), _stream(stream)), "smj_dev_digest")
+    return out
+
+
+def digest(table, pos0=0, stream=None):
+    """The order-sensitive digest of `table` as a Python int in [0, 2^64):
+    digests of consecutive slices at their global positions add up (mod 2^64)
+    to the digest of the whole table (smj.h smj_dev_digest)."""
+    d = digest_async(table, pos0, stream=stream)
+    return int(d.item()) & MASK64
 
 
 def prof_enable(on=True):

@@ -265,15 +265,16 @@ def test_c4_full_size_one_gpu(gpu, oracle_built):
     assert rows > 500_000 and j > 0
 
 
-@pytest.mark.parametrize("workload,stages", [("c3", 1), ("c5", 2)])
+@pytest.mark.parametrize("workload,stages", [("c3", 1), ("c5", 2), ("c4", 3)])
 def test_loopback_full_size_equals_single_call(gpu, workload, stages):
     """The distributed path at BASELINE sizes on one GPU (RCCL loopback,
     tools/loop_check.py): C3 with one stage sends 1.6 GB per table, C5 ~7 GB
-    of S per stage -- messages past RCCL's ~1 GiB point-to-point limit
-    (profiles/r04/r04f/rccl_big.txt), so this exercises the piece cutting of
-    smj/dist.py (before it, C4 / C5 loopback joins were wrong).  The joined
-    rows of every step equal the single call's bit for bit (the single call
-    is oracle-checked at these sizes above and in test_gpu_msd.py)."""
+    of S per stage, C4 5-9 GB per table and stage -- messages past RCCL's
+    ~1 GiB point-to-point limit (profiles/r04/r04f/rccl_big.txt), so this
+    exercises the piece cutting of smj/dist.py (before it, the C4 loopback
+    join had 999,910,439 rows instead of 247,122,870).  The joined rows of
+    every step equal the single call's bit for bit (the single call is
+    oracle-checked at these sizes above and in test_gpu_msd.py)."""
     import subprocess
     import sys
     from smj import _lib

@@ -393,3 +393,17 @@ def test_smj_app_typed_result_csv(gpu, oracle_built, manifest, golden_dir, tmp_p
     subprocess.run(cmd, check=True, capture_output=True, timeout=120)
     oracle.pipeline_csv(ins[0], ins[1], ref, sel, keys, ktype=ktype)
     assert sha(out) == sha(ref), case
+
+
+@pytest.mark.parametrize("n,cols", [(0, 2), (1, 1), (4097, 2), (1_000_003, 3), (65_536, 9)])
+def test_digest_matches_oracle(gpu, oracle_built, n, cols):
+    """smj_dev_digest (bench.py's distributed self-check) against its C
+    restatement, whole and in slices at their global positions."""
+    from smj import ops
+    rng = np.random.default_rng(7 * n + cols)
+    t = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, size=(n, cols), dtype=np.int64, endpoint=True)
+    d = dev(t).reshape(n, cols)
+    assert ops.digest(d) == oracle.digest(t)
+    a, b = n // 4, n // 2
+    assert ops.digest(d[a:b], a) == oracle.digest(t[a:b], a)
+    assert (ops.digest(d[:a]) + ops.digest(d[a:], a)) % (1 << 64) == oracle.digest(t)

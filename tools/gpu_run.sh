@@ -41,7 +41,7 @@ test_run() {  # a pytest step: stop on any failure
   run "$@" || { tail -30 "$OUT/$1.out"; echo "stopping after $1 (tests failed)" | tee -a "$OUT/steps.log"; exit 1; }
 }
 summ() {  # one-line summary of a bench JSON
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline') or {}; print(sys.argv[2], d['ms_per_step'], 'ms/step', d['value'], r.get('kernel'), r.get('frac'), {k: v['ms_per_step'] for k, v in d['kernels'].items() if v['ms_per_step'] > 0.1})" "$1" "$2" | tee -a "$OUT/steps.log"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline') or {}; print(sys.argv[2], d['ms_per_step'], 'ms/step', d['value'], 'verified', d.get('verified'), r.get('kernel'), r.get('frac'), {k: v['ms_per_step'] for k, v in d['kernels'].items() if v['ms_per_step'] > 0.1})" "$1" "$2" | tee -a "$OUT/steps.log"
 }
 for s in $STEPS; do
   case $s in
@@ -174,6 +174,14 @@ for s in $STEPS; do
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
+    t:*)   # t:FILE[:KEXPR] -- one test file, optionally filtered by -k (underscores kept, '+' = space)
+           spec=${s#t:}; f=${spec%%:*}; k=""; [ "$spec" != "$f" ] && k=${spec#*:}
+           n=$(basename "$f" .py)_$(echo "$k" | tr -c 'a-zA-Z0-9' '_' | cut -c1-30)
+           if [ -n "$k" ]; then test_run "$n" 1200 $PYT "$f" -m gpu -k "${k//+/ }"
+           else test_run "$n" 1200 $PYT "$f" -m gpu; fi ;;
+    loopv) for w in c3 c4 c5; do
+             run loopv_$w 900 python bench.py --loopback --workload $w --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loopv_$w.out" loop_$w
+           done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
