@@ -2245,6 +2245,12 @@ static_assert(kGroupCap == (1 << kFinIdxBits), "sort word = residual << 10 | gro
 
 constexpr int kCountRange = 4096;  // counting-sort residual range (packed u16 bins)
 constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re-orders
+#ifndef SMJ_ST_FOLDSCAN
+#define SMJ_ST_FOLDSCAN 1  // the staged kernel's join-row scan shares the st_issue_lists barrier
+#endif
+#ifndef SMJ_ST_RUNFIX
+#define SMJ_ST_RUNFIX 8  // the staged kernel: groups whose longest equal-key run is <= this sort runs in one pass
+#endif
 #ifndef SMJ_ST_MAXRUN
 #define SMJ_ST_MAXRUN kMaxDupRun  // the staged kernel: longer runs take the in-LDS LSD (<= kMaxDupRun)
 #endif
@@ -3025,7 +3031,7 @@ template <bool COMB>
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
-                                        uint32_t &nex) {
+                                        uint32_t &nex, uint32_t &mex) {
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const StSplit<COMB> L(p, g);
@@ -3135,7 +3141,48 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // run, r01k; the run's first thread insertion-sorting the run, r01ah:
     // 2.81 vs 2.32 ms.)
     static_assert(kStRows / 2 == 2 * kStThreads, "two compare-exchanges per thread and round");
-    for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd) ? 0u : fl); rd++) {
+    // Runs of at most SMJ_ST_RUNFIX rows (block-uniform fl: the longest run):
+    // one pass instead of fl rounds -- the thread holding a run's first
+    // position (read off the histogram starts) sorts the run by group row on
+    // its own (a compare-exchange for two rows, an insertion sort for more),
+    // then one barrier.  C3's longest run per group is ~4 (Poisson(1/3) keys
+    // per table): 1 barrier instead of ~4.
+    const bool runfix = SMJ_ST_RUNFIX > 1 && !lsd && !ST_ABL(16) && fl > 1u && fl <= (uint32_t)SMJ_ST_RUNFIX;
+    if (runfix) {
+#pragma unroll
+        for (int k = 0; k < kStIt; k++) {
+            const uint32_t q = (uint32_t)tid + (uint32_t)k * kStThreads;
+            if (!L.valid_pos(q)) continue;
+            const uint32_t x = q >= sp ? 1u : 0u, pq = q - (x ? sp : 0u);
+            const uint32_t w0 = sm.key[q], res = w0 >> kStIdx, sh = 16u * (res & 1u);
+            const uint32_t hw = sm.hist[x][res >> 1];
+            if (((hw >> sh) & 0xffffu) != pq) continue;  // not the first position of its run
+            const uint32_t nx = x ? nS : nR;
+            const uint32_t end = (res & 1u) ? ((res + 1u < (uint32_t)kStRange) ? (sm.hist[x][(res + 1) >> 1] & 0xffffu) : nx)
+                                            : (hw >> 16);
+            const uint32_t len = end - pq;
+            if (len < 2) continue;
+            if (len == 2) {
+                const uint32_t b = sm.key[q + 1];
+                if (w0 > b) {
+                    sm.key[q] = b;
+                    sm.key[q + 1] = w0;
+                }
+            } else {
+                for (uint32_t i = 1; i < len; i++) {
+                    const uint32_t v = sm.key[q + i];
+                    uint32_t j = i;
+                    while (j > 0 && sm.key[q + j - 1] > v) {
+                        sm.key[q + j] = sm.key[q + j - 1];
+                        j--;
+                    }
+                    sm.key[q + j] = v;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd || runfix) ? 0u : fl); rd++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint32_t q = 2u * (uint32_t)(tid + h * kStThreads) + (rd & 1u);
@@ -3178,6 +3225,15 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             }
         }
     }
+    if (SMJ_ST_FOLDSCAN) {
+        // the join rows' block scan, first half: wave totals published here,
+        // read by st_emit after the barrier that separates the two (in
+        // st_issue_lists, or the kernel's own when there is no next group) --
+        // one barrier per group less than a scan of its own
+        const uint32_t c = (uint32_t)__popc(mmask), inc = wave_incl_scan(c, lane);
+        if (lane == 63) sm.wsum[wsb][wave] = inc;
+        mex = inc - c;
+    }
     return true;
 }
 
@@ -3185,7 +3241,7 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
 // is zeroed for the next group here (no one reads it after the lookups)
 template <bool COMB>
 __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, StSmem &sm,
-                                        int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt]) {
+                                        int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt], uint32_t mex) {
     const int tid = opaque_tid();
     const StSplit<COMB> L(p, g);
     {
@@ -3211,8 +3267,21 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     }
     if (!p.join || ST_ABL(8)) return;
     const uint32_t *kS = sm.key + L.sp;
-    uint32_t total;
-    uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
+    uint32_t total, o;
+    if (SMJ_ST_FOLDSCAN) {  // the wave totals st_sort published (a barrier ago)
+        const int wave = tid >> 6;
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int u = 0; u < kStWaves; u++) {
+            const uint32_t x = sm.wsum[wsb][u];
+            before += u < wave ? x : 0u;
+            all += x;
+        }
+        total = all;
+        o = before + mex;
+    } else {
+        o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
+    }
     wsb ^= 1;
     if (tid == 0) p.counts[gi] = total;
     if (total == 0) return;
@@ -3334,7 +3403,8 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         FIN_STAMP(1);
         uint32_t mmask = 0, part[kStIt];
         uint32_t nex;  // the next group's run-length prefix, scanned with this group's bins
-        const bool ok = st_sort<COMB>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex);  // cur is staged in LDS here
+        uint32_t mex = 0;  // this thread's exclusive prefix of join rows within its wave (SMJ_ST_FOLDSCAN)
+        const bool ok = st_sort<COMB>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex, mex);  // cur is staged in LDS here
         FIN_STAMP(2);
         // st_issue_lists writes only the list region (unused by the sort; its
         // start bitmap was zeroed, and its run lengths scanned, inside
@@ -3349,7 +3419,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
             __syncthreads();
         FIN_STAMP(3);
         if (ok) {
-            st_emit<COMB>(p, g, gi, sm, wsb, mmask, part);
+            st_emit<COMB>(p, g, gi, sm, wsb, mmask, part, mex);
         } else {  // hand-over: the histogram still needs zeroing
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
             for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);

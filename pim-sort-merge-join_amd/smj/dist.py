@@ -620,11 +620,15 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     cnt = [torch.empty(nb + 1, dtype=torch.int64, device=R.device) for _ in range(2)]
     cur = torch.cuda.current_stream(R.device) if R.is_cuda else None
     sside = _s_stream(R.device) if (R.is_cuda and S_SIDE) else None
-    if sside is not None:
-        sside.wait_stream(cur)  # everything before this step (buffers it may reuse) first
     part = [_partition(ops, R, bounds, cnt[0], own[0], k1, sc1, sv1)]
     gR = _HostGather(cnt[0], world, group)
     if sside is not None:
+        # after R's partition: the two calls share the library's partition
+        # scratch (region words, look-back status words), so they must not run
+        # at once -- only the process group's work is kept off S's partition
+        # (r05a: concurrent partitions corrupted R's look-back, an illegal
+        # address at C3); also orders everything before this step first
+        sside.wait_stream(cur)
         with torch.cuda.stream(sside):
             part.append(_partition(ops, S, bounds, cnt[1], own[1], k2, sc2, sv2))
         gS = None
