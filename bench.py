@@ -154,7 +154,10 @@ def verify_distributed(J, rank, world, dev, full_tables):
     if rank == 0:
         torch.cuda.empty_cache()  # the distributed path's cached blocks, for the library's own allocations
         Rf, Sf = full_tables()
+        log(f"[verify] reference call on {Rf.shape[0]} x {Sf.shape[0]} rows "
+            f"(free {torch.cuda.mem_get_info()[0] / 2**30:.1f} GiB)")
         _, _, Jf = ops.sort_merge_join(Rf, Sf, KEYS[0], KEYS[1], (SELECT[0], SELECT[1]), (SELECT[2], SELECT[3]))
+        log(f"[verify] reference call done: {Jf.shape[0]} joined rows")
         total = Jf.shape[0]
         ref = [ops.digest(Jf[offs[r]: offs[r] + counts[r]], offs[r]) if offs[r] + counts[r] <= total else None
                for r in range(world)]
@@ -231,8 +234,17 @@ def main():
             return step_single(R, S, bufs)
         return sdist.sort_merge_join(R, S, select=SELECT, keys=KEYS, stats=lb, loopback=a.loopback)
 
-    for _ in range(a.warmup):
+    t_start = time.perf_counter()
+
+    def progress(what):  # one stderr line per phase (rank 0): a long run shows where it is
+        if rank == 0:
+            log(f"[bench {time.perf_counter() - t_start:7.1f} s] {what}")
+
+    progress(f"inputs ready ({nr} + {ns} rows on this rank)")
+    for i in range(a.warmup):
         step()
+        torch.cuda.synchronize()
+        progress(f"warmup step {i + 1}/{a.warmup} done")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -258,6 +270,7 @@ def main():
         step()
     torch.cuda.synchronize()
     ops.prof_enable(False)
+    progress(f"{a.steps} timed + {psteps} profiled steps done ({dt / a.steps * 1e3:.3f} ms/step)")
     prof = ops.prof_report()
     if world == 1:
         log(f"msd stats (single-key groups, LSD-fallback groups, mR, mS): {ops.msd_stats()}; "
@@ -276,6 +289,7 @@ def main():
 
     verified, verification = None, None
     if distributed and a.verify:
+        progress("verification: digests of every rank's slice, then the single-GPU call on rank 0")
         verified, verification = verify_distributed(res, rank, world, dev, full_tables)
         if rank == 0:
             log(f"verification: {verification}")

@@ -514,6 +514,8 @@ struct MsdScratch {
     size_t c_p1st = 0;
     int64_t *p1d = nullptr;             // device [2][kP1Words]: oc[128], tot[64], flags[4] (u32 x 8) per table
     int64_t *p1h = nullptr;             // pinned twin
+    int64_t *heavy = nullptr;           // [kBucketsA][kHeavyMax] heavy keys per bucket (msd_heavy_kernel)
+    uint32_t *nheavy = nullptr;         // [kBucketsA] their count
     uint32_t *p1c = nullptr;            // chunked partition: device [2][kP1cWords]: rows per (chunk, part), flags
     uint32_t *h_p1c = nullptr;          // pinned twin
     void *p1desc[2] = {nullptr, nullptr};  // its parts' part_a tile descriptors per table
@@ -570,6 +572,8 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(hipMalloc(&m.p1d, sizeof(int64_t) * 2 * kP1Words));
         HIP_TRY(hipHostMalloc(&m.p1h, sizeof(int64_t) * 2 * kP1Words, hipHostMallocDefault));
         HIP_TRY(hipMalloc(&m.p1c, sizeof(uint32_t) * 2 * kP1cWords));
+        HIP_TRY(hipMalloc(&m.heavy, sizeof(int64_t) * kBucketsA * kHeavyMax));
+        HIP_TRY(hipMalloc(&m.nheavy, sizeof(uint32_t) * kBucketsA));
         HIP_TRY(hipHostMalloc(&m.h_p1c, sizeof(uint32_t) * 2 * kP1cWords, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
@@ -589,7 +593,7 @@ void msd_free_one(MsdScratch &m) {  // also a set whose creation failed half-way
     for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                     (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                     (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
-                    (void *)m.p1c, m.p1desc[0], m.p1desc[1]})
+                    (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy})
         hipFree(p);
     hipHostFree(m.p1h);
     hipHostFree(m.h_p1c);
@@ -1057,7 +1061,29 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
             ta[2 * x + 1] = segT(x, 1);
         }
         HIP_TRY(launch_msd_seg_scan(sa, ta, 2 * ntab, s));
+        // heavy keys per bucket (a skewed sample only; SMJ_HEAVY=0 turns it off)
+        const bool heavy_on = !(getenv("SMJ_HEAVY") && atoi(getenv("SMJ_HEAVY")) == 0) && in[0].cols <= kDirectCols &&
+                              (ntab < 2 || in[1].cols <= kDirectCols);
+        if (heavy_on) {
+            MsdHeavyParams hp{};
+            for (int x = 0; x < ntab; x++) {
+                hp.tempA[x] = (const int64_t *)ms->t[x].tempA;
+                hp.offs[x] = (const uint32_t *)ms->t[x].offsA;
+                hp.ntiles[x] = tilesA[x];
+                hp.tile[x] = T_[x];
+                hp.cols[x] = in[x].cols;
+                hp.key[x] = in[x].key;
+                hp.totL[x] = segT(x, 0);
+            }
+            hp.spl = ms->spl;
+            hp.ntab = ntab;
+            hp.heavy = ms->heavy;
+            hp.nheavy = ms->nheavy;
+            ProfScope ps("msd_heavy", 0, s);
+            HIP_TRY(launch_msd_heavy(hp, s));
+        }
         MsdBasesParams bp{};
+        bp.nheavy = heavy_on ? ms->nheavy : nullptr;
         for (int x = 0; x < ntab; x++) {
             bp.totL[x] = segT(x, 0);
             bp.totC[x] = segT(x, 1);
@@ -1079,6 +1105,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         MsdPartBParams p{(const int64_t *)ms->t[x].tempA, (int64_t *)ms->t[x].tempB, (const uint2 *)ms->t[x].list,
                          (const uint2 *)ms->t[x].tinfo, (const MsdBucket *)ms->t[x].bk, ms->plan,
                          (uint16_t *)ms->t[x].offsB, in[x].key, x};
+        p.heavy = ms->heavy;
         {
             ProfScope ps("msd_part_b", 0, s);
             HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s));
@@ -1106,6 +1133,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         gp.single_list = ms->single_list;
         gp.big_list = ms->big_list;
         gp.spin_limit = g_spin_limit;
+        gp.heavy = ms->heavy;
         ProfScope ps("msd_group", 0, s);
         HIP_TRY(launch_msd_group(gp, s));
     }

@@ -277,8 +277,31 @@ struct MsdBucket {       // per pass-A bucket and table
     uint32_t list_base;  // first run-list entry
     uint32_t nruns;      // run-list entries
     uint32_t tile_base;  // first pass-B tile
-    uint32_t one_key;    // the bucket's interval is a single key value (a heavy key's bucket)
+    uint32_t one_key;    // bit 0: the bucket's interval is a single key value (a heavy key's bucket);
+                         // bits 8..15: m, the bucket's heavy keys (msd_heavy_kernel): the pass-B digit
+                         // is then d = lin(r) + 2 c + e over D - 2 m linear sub-buckets, c = heavy keys
+                         // below the key, e = the key is one -- every heavy key a sub-bucket of its own
     uint32_t s32;        // != 0 (interval < 2^32 keys): the digit is mulhi32(r, s32) instead
+};
+// Heavy keys of a multi-key pass-A bucket (C5's Zipf tables: keys with
+// thousands of rows next to light ones, which made oversized sub-buckets for
+// msd_big_stage / msd_giant_*): found from a sample of the bucket's rows,
+// <= kHeavyMax per bucket, each given a sub-bucket of its own by the pass-B
+// digit -- a single-key group, streamed in stable order by msd_single_kernel
+constexpr int kHeavyMax = 64;
+constexpr int kHeavySamples = 2048;   // sampled rows per bucket (both tables)
+constexpr uint32_t kHeavyRows = 768;  // a key is heavy from ~this many rows (sample hits scaled)
+__host__ __device__ inline uint32_t msd_heavy_count(uint32_t one_key_word) { return (one_key_word >> 8) & 0xffu; }
+struct MsdHeavyParams {
+    const int64_t *tempA[2];   // pass-A tiles (msd_part_a)
+    const uint32_t *offs[2];   // [tiles][kOffsARow] bucket starts
+    int64_t ntiles[2];
+    int tile[2], cols[2], key[2];  // pass-A tile rows, columns, key column
+    const uint32_t *totL[2];   // rows per bucket (msd_seg_scan_kernel)
+    const int64_t *spl;        // pass-A splitters
+    int ntab;
+    int64_t *heavy;            // out: [kBucketsA][kHeavyMax] ascending heavy keys
+    uint32_t *nheavy;          // out: [kBucketsA] their count
 };
 struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t m[2];       // selected rows per table
@@ -320,6 +343,7 @@ struct MsdBasesParams {
     const int64_t *spl;
     MsdBucket *bk[2];
     MsdPlan *plan;
+    const uint32_t *nheavy;    // [kBucketsA] heavy keys per bucket (msd_heavy_kernel), nullptr = none
 };
 struct MsdPartBParams {
     const int64_t *srcA;
@@ -331,6 +355,7 @@ struct MsdPartBParams {
     uint16_t *offs;      // [tilesB][kOffsB] tile-local sub-bucket starts
     int key_col, x;
     int dbg;             // SMJ_DEBUG_MSD: phase stamps (tools/msd_phases.py)
+    const int64_t *heavy;  // [kBucketsA][kHeavyMax] heavy keys (MsdBucket::one_key bits 8..15: how many)
 };
 struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
     uint16_t a, flags, b0, b1;
@@ -354,6 +379,7 @@ struct MsdGroupParams {
     uint32_t *single_list, *big_list;  // dense group indices
     int combined;           // as MsdBasesParams::combined
     uint32_t spin_limit;    // polls of the look-back before it gives up (kMsdSpinLimit; 0 in the forced-timeout test)
+    const int64_t *heavy;   // as MsdPartBParams::heavy
 };
 struct MsdTab {          // a table as the final kernels see it
     const int64_t *tempB;
@@ -478,6 +504,7 @@ struct MsdRunsArgs {     // msd_runs_seg / msd_runs_apply over both tables (bloc
 hipError_t launch_msd_runs_seg(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int narr, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
+hipError_t launch_msd_heavy(const MsdHeavyParams &p, hipStream_t s);
 hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);

@@ -825,6 +825,105 @@ __global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanPara
     if (w == 0) p.tot[blockIdx.y][a] = tot;
 }
 
+// Heavy keys of bucket a = blockIdx.x (1024 threads): kHeavySamples rows of
+// the bucket, both tables in proportion to their rows, each one row of an
+// evenly spaced pass-A tile's run of the bucket, sorted in LDS (bitonic); a
+// key sampled at least thr times -- ~kHeavyRows rows of the bucket's L --
+// is heavy (the kHeavyMax most sampled when more qualify).  Runs only when the
+// pass-A sample already shows skew (a repeated splitter) and for multi-key
+// buckets over 8 kGroupCap rows; elsewhere the bucket gets none.  A missed
+// heavy key only costs speed (its sub-bucket takes the oversized-group path),
+// a light key taken for heavy only a single-key group of its own: the sort
+// and join never depend on the sample.
+constexpr int kHeavyThreads = 1024;
+__global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavyParams p) {
+    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads;
+    static_assert(kHeavySamples == 2 * kHeavyThreads, "two sampled rows per thread");
+    __shared__ int64_t s_k[kHeavySamples];
+    __shared__ uint32_t s_wsum[NW], s_skew, s_cnt;
+    const int a = blockIdx.x, t = threadIdx.x;
+    if (t == 0) s_skew = 0;
+    __syncthreads();
+    if (t + 1 < kSplA && p.spl[t] == p.spl[t + 1]) s_skew = 1;  // benign race: all write 1
+    __syncthreads();
+    const int64_t *spl = p.spl;
+    const bool own = a >= 1 && a < kSplA && spl[a] == spl[a - 1] && (a == 1 || spl[a - 2] != spl[a - 1]);
+    const uint32_t L0 = p.totL[0][a], L1 = p.ntab > 1 ? p.totL[1][a] : 0u, L = L0 + L1;
+    if (!s_skew || own || L < 8u * kGroupCap) {
+        if (t == 0) p.nheavy[a] = 0;
+        return;
+    }
+    const uint32_t n0 = p.ntab > 1 ? (uint32_t)(((uint64_t)kHeavySamples * L0 + L / 2) / L) : (uint32_t)kHeavySamples;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t i = (uint32_t)t + (uint32_t)k * kHeavyThreads;
+        const int x = i < n0 ? 0 : 1;
+        const uint32_t j = x ? i - n0 : i, nx = x ? kHeavySamples - n0 : n0;
+        int64_t key = INT64_MAX;  // no sample
+        if (j < nx && p.ntiles[x] > 0) {
+            const int64_t tile = (int64_t)(((unsigned __int128)j * (uint64_t)p.ntiles[x]) / nx);
+            const uint32_t *o = p.offs[x] + tile * kOffsARow;
+            const uint32_t s0 = o[a], s1 = o[a + 1];  // o[kBucketsA] = the tile's rows
+            if (s1 > s0) {
+                const uint32_t r = s0 + (uint32_t)(((uint64_t)(j * 0x9E3779B9u) * (s1 - s0)) >> 32);
+                key = p.tempA[x][((int64_t)tile * p.tile[x] + r) * p.cols[x] + p.key[x]];
+            }
+        }
+        s_k[i] = key;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= (uint32_t)kHeavySamples; k <<= 1)  // bitonic sort, ascending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t i = (((uint32_t)t & ~(j - 1u)) << 1) | ((uint32_t)t & (j - 1u)), l = i + j;
+            const int64_t u = s_k[i], v = s_k[l];
+            if ((u > v) == ((i & k) == 0)) {
+                s_k[i] = v;
+                s_k[l] = u;
+            }
+            __syncthreads();
+        }
+    // runs of equal sampled keys: this thread's positions q = t, t + 1024
+    uint32_t len[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t q = (uint32_t)t + (uint32_t)k * kHeavyThreads;
+        const int64_t v = s_k[q];
+        len[k] = 0;
+        if (v != INT64_MAX && (q == 0 || s_k[q - 1] != v)) {  // a run starts at q: its end by binary search
+            uint32_t lo = q, n = (uint32_t)kHeavySamples - q;
+            while (n) {
+                const uint32_t h = n >> 1;
+                if (s_k[lo + h] <= v) { lo += h + 1; n -= h + 1; } else n = h;
+            }
+            len[k] = lo - q;
+        }
+    }
+    // hits for ~kHeavyRows rows of the bucket; raised until <= kHeavyMax keys qualify
+    uint32_t thr = max(3u, (uint32_t)(((uint64_t)kHeavySamples * kHeavyRows + L - 1) / L));
+    for (int round = 0; round < 16; round++) {
+        if (t == 0) s_cnt = 0;
+        __syncthreads();
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) c += len[k] >= thr ? 1u : 0u;
+        if (c) atomicAdd(&s_cnt, c);
+        __syncthreads();
+        const uint32_t tot = s_cnt;
+        __syncthreads();
+        if (tot <= (uint32_t)kHeavyMax) break;
+        thr = thr + thr / 2 + 1;
+    }
+    // the qualifying keys in ascending order: positions q = t (first half), then t + 1024
+    uint32_t tot0, tot1;
+    const uint32_t f0 = len[0] >= thr ? 1u : 0u, f1 = len[1] >= thr ? 1u : 0u;
+    const uint32_t e0 = block_excl_scan<NW>(f0, s_wsum, &tot0);
+    const uint32_t e1 = block_excl_scan<NW>(f1, s_wsum, &tot1);
+    int64_t *hv = p.heavy + (int64_t)a * kHeavyMax;
+    if (f0 && e0 < (uint32_t)kHeavyMax) hv[e0] = s_k[t];
+    if (f1 && tot0 + e1 < (uint32_t)kHeavyMax) hv[tot0 + e1] = s_k[t + kHeavyThreads];
+    if (t == 0) p.nheavy[a] = min(tot0 + tot1, (uint32_t)kHeavyMax);
+}
+
 // one workgroup of kOffsA threads: thread = bucket.  Bucket sizes / bases of
 // both tables, the global key range, and the pass-B digit of every bucket.
 constexpr int kBasesWaves = kOffsA / 64;
@@ -864,7 +963,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     // 2 x 448 = 896 of 1024 rows instead of 2 x 381 = 762 with D = kRadB.
     int64_t lo = 0;
     uint64_t scale = 0;
-    uint32_t maxspan = kRadB, s32 = 0;
+    uint32_t maxspan = kRadB, s32 = 0, heavy = 0;
     bool one_key = false;
     if (a < kBucketsA) {
         // bucket a = (spl[a-1], spl[a]] (open ends: the global min / max),
@@ -894,6 +993,12 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
                 const uint64_t k = (uint64_t)kRadB * kFill / Lm;
                 D = k >= 2 ? (Lm * k + kFill - 1) / kFill : (Lm + kOne - 1) / kOne;
                 D = min<uint64_t>(kRadB, max<uint64_t>(kRadB / 2, D));
+            }
+            // the bucket's heavy keys take two sub-buckets each (their own and
+            // the split of their linear sub-bucket's other keys): D - 2 m linear ones
+            if (p.nheavy) {
+                heavy = min(p.nheavy[a], (uint32_t)kHeavyMax);
+                D = min<uint64_t>(D, (uint64_t)kRadB - 2u * heavy);
             }
             const unsigned __int128 q = ((unsigned __int128)D << 64) / ((unsigned __int128)range + 1u);
             scale = q >> 64 ? ~0ull : (uint64_t)q;
@@ -928,7 +1033,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             b.list_base = lb;
             b.nruns = C;
             b.tile_base = tb;
-            b.one_key = one_key ? 1u : 0u;
+            b.one_key = (one_key ? 1u : 0u) | (heavy << 8);
             b.s32 = s32;
             p.bk[x][a] = b;
         }
@@ -1055,7 +1160,34 @@ __device__ __forceinline__ MsdBucket uni_bucket(const MsdBucket *bk, uint32_t a)
     r.list_base = uni32(v.list_base);
     r.nruns = uni32(v.nruns);
     r.tile_base = uni32(v.tile_base);
+    r.one_key = uni32(v.one_key);
     return r;
+}
+
+// ---------------------------------------------------------------------------
+// the pass-B digit (part_b computes it, the group kernel inverts it)
+// ---------------------------------------------------------------------------
+// linear sub-bucket of residual r = key - lo
+__device__ __forceinline__ uint32_t pb_lin(const MsdBucket &b, uint64_t r) {
+    return b.s32 ? __umulhi((uint32_t)r, b.s32)  // < D: r < 2^32 in such a bucket
+                 : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(kRadB - 1)) : (uint32_t)r;
+}
+// heavy keys below `key` in the bucket's sorted list hv[0, m) (m <= kHeavyMax;
+// a fixed 7-step search), and whether key is one of them
+__device__ __forceinline__ uint32_t heavy_rank(const int64_t *hv, uint32_t m, int64_t key, bool &eq) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t st = kHeavyMax; st >= 1; st >>= 1)
+        if (pos + st <= m && hv[pos + st - 1] < key) pos += st;
+    eq = pos < m && hv[pos] == key;
+    return pos;
+}
+// the digit with m heavy keys: lin + 2 c + e (order-preserving; heavy key j --
+// 0-based -- alone in sub-bucket lin(h_j) + 2 j + 1)
+__device__ __forceinline__ uint32_t pb_digit_heavy(uint32_t lin, const int64_t *hv, uint32_t m, int64_t key) {
+    bool eq;
+    const uint32_t c = heavy_rank(hv, m, key, eq);
+    return lin + 2u * c + (eq ? 1u : 0u);
 }
 
 // Diagnostic phase stamps of part_b (SMJ_DEBUG_MSD=1; off in production):
@@ -1107,6 +1239,7 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
     __shared__ __attribute__((aligned(16))) unsigned char s_u[UB];
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint32_t s_slow;
+    __shared__ int64_t s_hv[kHeavyMax];  // the tile's bucket's heavy keys (MsdBucket::one_key bits 8..15)
     uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_u);
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_u + PERMB);
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
@@ -1152,6 +1285,8 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         const uint32_t q0 = ti.y;
         const int J = (int)runs_of(ti, b, g);
         for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
+        if (msd_heavy_count(b.one_key) && (uint32_t)tid < msd_heavy_count(b.one_key))  // read after two barriers
+            s_hv[tid] = p.heavy[(int64_t)ti.x * kHeavyMax + tid];
         if (p.dbg & 32) goto lookups_done;
         if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
         for (int j = tid + NT; j < J; j += NT)  // > NT runs: rare
@@ -1194,13 +1329,13 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 
         uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
         uint32_t vmask = 0;
+        const uint32_t hm = msd_heavy_count(b.one_key);  // block-uniform
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const bool v = lrow0 + it * 64 < nrows;
-            const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
-            const uint32_t d = b.s32     ? __umulhi((uint32_t)r, b.s32)  // < D: r < 2^32 in such a bucket
-                               : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1))
-                                         : (uint32_t)r;
+            const int64_t key = pick<COLS>(rows[it], p.key_col);
+            uint32_t d = pb_lin(b, (uint64_t)key - (uint64_t)b.lo);
+            if (hm) d = pb_digit_heavy(d, s_hv, hm, key);
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
@@ -1402,6 +1537,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
     __shared__ uint16_t s_nbt[T / 64];  // its 64-row block table
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint32_t s_slow;
+    __shared__ int64_t s_hv[kHeavyMax];  // the tile's bucket's heavy keys (MsdBucket::one_key bits 8..15)
     uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_u);
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_u + PERMB);
     int64_t *s_rows = reinterpret_cast<int64_t *>(s_u);
@@ -1467,6 +1603,9 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // or after the next tile's gathers as before, is waited with vmcnt(0),
         // which also retires the gathers and the previous tile's stores)
         const uint2 tn2 = sc_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
+        // the tile's bucket's heavy keys (C5; block-uniform: no load, no wait elsewhere)
+        const uint32_t hm = msd_heavy_count(b.one_key);
+        if (hm && (uint32_t)tid < hm) s_hv[tid] = p.heavy[(int64_t)ti.x * kHeavyMax + tid];
         __syncthreads();
 
         uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
@@ -1474,10 +1613,9 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const bool v = lrow0 + it * 64 < nrows;
-            const uint64_t r = (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo;
-            const uint32_t d = b.s32     ? __umulhi((uint32_t)r, b.s32)
-                               : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(RADIX - 1))
-                                         : (uint32_t)r;
+            const int64_t key = pick<COLS>(rows[it], p.key_col);
+            uint32_t d = pb_lin(b, (uint64_t)key - (uint64_t)b.lo);
+            if (hm) d = pb_digit_heavy(d, s_hv, hm, key);
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
         }
@@ -1485,7 +1623,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // sub-bucket 0 and the tile's gather order is already its stable
         // order -- no counting atomics (all on one LDS word) and no ranking
         // (cmax > SMJ_PB_FASTMAX would take the slow wave-by-wave path)
-        const bool one_key = SMJ_PB_ONEKEY && b.one_key != 0u;  // block-uniform (SMEM)
+        const bool one_key = SMJ_PB_ONEKEY && (b.one_key & 1u) != 0u;  // block-uniform (SMEM)
         if (!one_key) {
             const uint32_t quad = quad_of(), qsh = 16u * (quad & 1u), qrow = (quad >> 1) * RADIX;
 #pragma unroll
@@ -1686,7 +1824,7 @@ __global__ __launch_bounds__(256) void msd_group_sum_kernel(const MsdGroupParams
         const uint32_t k0 = (uint32_t)(((uint64_t)K * sl) / kGroupSlices), k1 = (uint32_t)(((uint64_t)K * (sl + 1)) / kGroupSlices);
         const uint16_t *o = p.offs[x] + (int64_t)bk.tile_base * kOffsB + t * SB;
         static_assert(SB == 8 && kOffsB % 8 == 0, "one 16-B load of 8 starts per row (rows 16-B aligned)");
-        if (bk.one_key) {  // a heavy key's bucket: every row is in sub-bucket 0 (C5: thousands of tiles)
+        if (bk.one_key & 1u) {  // a heavy key's bucket: every row is in sub-bucket 0 (C5: thousands of tiles)
             if (sl == 0 && t == 0) tot[0] = bk.L;
         } else
 #pragma unroll 4
@@ -1723,6 +1861,8 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     __shared__ uint32_t s_wsum[NW];
     __shared__ uint16_t s_g0[kRadB], s_g1[kRadB];   // groups: sub-buckets [b0, b1)
     __shared__ int s_ng, s_a;
+    __shared__ int64_t s_hk[kHeavyMax];             // the bucket's heavy keys (ascending)
+    __shared__ uint16_t s_hs[kHeavyMax], s_hl[kHeavyMax];  // heavy key j's sub-bucket, and its linear sub-bucket
     // The bucket is a ticket, not blockIdx.x: dispatch order (and which XCD
     // gets a workgroup when) is undefined, so a workgroup waiting on a lower
     // blockIdx could wait on one that is not resident yet -- and with other
@@ -1777,6 +1917,29 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     }
     __syncthreads();
     const bool single_sub = p.bk[0][a].scale == 0;  // every sub-bucket holds one key value
+    // heavy keys (msd_heavy_kernel): heavy key j alone in sub-bucket
+    // s_hs[j] = lin(h_j) + 2 j + 1 -- a group of its own, flagged single-key
+    // (streamed in stable order); the others' linear sub-bucket of a digit d
+    // is d - 2 #{heavy sub-buckets < d}
+    const uint32_t hm = msd_heavy_count(p.bk[0][a].one_key);
+    if ((uint32_t)t < hm) {
+        const MsdBucket &bb = p.bk[0][a];
+        const int64_t h = p.heavy[(int64_t)a * kHeavyMax + t];
+        const uint32_t l = pb_lin(bb, (uint64_t)h - (uint64_t)bb.lo);
+        s_hk[t] = h;
+        s_hl[t] = (uint16_t)l;
+        s_hs[t] = (uint16_t)(l + 2u * (uint32_t)t + 1u);
+    }
+    __syncthreads();
+    // heavy sub-buckets below d, and whether d is one
+    auto heavy_below = [&](uint32_t d, bool &is) -> uint32_t {
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t st = kHeavyMax; st >= 1; st >>= 1)
+            if (pos + st <= hm && s_hs[pos + st - 1] < d) pos += st;
+        is = pos < hm && s_hs[pos] == d;
+        return pos;
+    };
     // a group spans < 2^48 key values, so that (residual << idx | index) fits one
     // word in the final kernel's LDS sort
     const int maxspan = (int)p.bk[0][a].maxspan;
@@ -1828,6 +1991,12 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
                     if (lo <= kRadB) lim = min(lim, lo - 1);
                     else if (i + 1 <= kRadB && s_P[x][i + 1] > cap) lim = min(lim, i + 1);
                 }
+            }
+            if (hm) {  // a heavy sub-bucket is a group of its own: stop before the next one
+                bool is;
+                const uint32_t c = heavy_below((uint32_t)i, is);
+                if (is) lim = i + 1;
+                else if (c < hm) lim = min(lim, (int)s_hs[c]);
             }
             f = next_nz(max(lim, i + 1));
         }
@@ -1919,7 +2088,12 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.outR = p.bk[0][a].row_start + s_P[0][b0];
         gr.outS = p.ntab > 1 ? p.bk[1][a].row_start + s_P[1][b0] : 0u;
         gr.flags = 0;
-        if (comb ? gr.nR + gr.nS > (uint32_t)kStRows : (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap))
+        bool hv_only = false;  // the group is one heavy key's sub-bucket
+        uint32_t hj = 0;
+        if (hm && b1 == b0 + 1) hj = heavy_below(b0, hv_only);
+        if (hv_only)
+            gr.flags = kGroupSingle;  // whatever its size: streamed in stable order, no sort
+        else if (comb ? gr.nR + gr.nS > (uint32_t)kStRows : (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap))
             gr.flags = single_sub ? kGroupSingle : kGroupBig;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
@@ -1930,19 +2104,33 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         // digit(r) = floor(r * scale / 2^64) in [b0, b1) satisfy rmin(b0) <= r < rmin(b1),
         // rmin(b) = ceil(b * 2^64 / scale) (2^32 and s32 for a 32-bit digit);
         // with scale == 0 the digit is r itself
+        // (with heavy keys: over the linear sub-buckets [lin(b0), lin(b1 - 1) + 1)
+        // -- a superset of the group's keys -- and a heavy key's group is the key)
         const uint64_t sc = p.bk[0][a].scale;
         const uint32_t s32 = p.bk[0][a].s32;
-        unsigned __int128 r0 = b0, r1 = b1;
+        uint32_t l0 = b0, l1 = b1;
+        if (hm) {
+            bool is;
+            uint32_t c = heavy_below(b0, is);
+            l0 = is ? (uint32_t)s_hl[c] : b0 - 2u * c;
+            c = heavy_below(b1 - 1u, is);
+            l1 = (is ? (uint32_t)s_hl[c] : b1 - 1u - 2u * c) + 1u;
+        }
+        unsigned __int128 r0 = l0, r1 = l1;
         if (s32) {
-            r0 = (((uint64_t)b0 << 32) + s32 - 1u) / s32;
-            r1 = (((uint64_t)b1 << 32) + s32 - 1u) / s32;
+            r0 = (((uint64_t)l0 << 32) + s32 - 1u) / s32;
+            r1 = (((uint64_t)l1 << 32) + s32 - 1u) / s32;
         } else if (sc) {
-            r0 = (((unsigned __int128)b0 << 64) + sc - 1) / sc;
-            r1 = (((unsigned __int128)b1 << 64) + sc - 1) / sc;
+            r0 = (((unsigned __int128)l0 << 64) + sc - 1) / sc;
+            r1 = (((unsigned __int128)l1 << 64) + sc - 1) / sc;
         }
         gr.base = (int64_t)((uint64_t)p.bk[0][a].lo + (uint64_t)r0);
         const unsigned __int128 sp = r1 - r0;
         gr.span = sp > 0xffffffffu ? 0xffffffffu : (uint32_t)sp;
+        if (hv_only) {
+            gr.base = s_hk[hj];
+            gr.span = 1;
+        }
         // dense, key-ordered index; the streamed / oversized lists
         const uint32_t gi = base + (uint32_t)j;
         if (gi >= (uint32_t)kSlots) {  // the group array's capacity (a wrong base: never stored past it)
@@ -1986,7 +2174,7 @@ __device__ __forceinline__ void group_gather(const MsdTab &tb, const MsdGroup &g
     const int tid = threadIdx.x;
     const MsdBucket bk = tb.bk[g.a];
     const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
-    if (bk.one_key && g.b0 == 0) {  // single-key bucket: its tiles are full and hold only sub-bucket 0
+    if ((bk.one_key & 1u) && g.b0 == 0) {  // single-key bucket: its tiles are full and hold only sub-bucket 0
         const uint32_t base = bk.tile_base * (uint32_t)tb.tile;
         for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads) fn(v, base + v);
         return;
@@ -4574,6 +4762,11 @@ hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int n
 
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s) {
     hipLaunchKernelGGL(msd_bases_kernel, dim3(1), dim3(kOffsA), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_heavy(const MsdHeavyParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(msd_heavy_kernel, dim3(kBucketsA), dim3(kHeavyThreads), 0, s, p);
     return hipGetLastError();
 }
 

@@ -200,10 +200,12 @@ def test_single_key_groups_stream(gpu, oracle_built):
     np.testing.assert_array_equal(host(gJ), J)
 
 
-def test_multi_key_oversized_group_falls_back(gpu, oracle_built):
+def test_multi_key_oversized_group_falls_back(gpu, oracle_built, monkeypatch):
     """A far outlier stretches the first bucket's key interval, so thousands of
-    distinct keys share one sub-bucket: the LSD fallback sorts and joins it."""
+    distinct keys share one sub-bucket: the LSD fallback sorts and joins it
+    (heavy-key sub-buckets off: this test is about the fallback tier)."""
     from smj import ops
+    monkeypatch.setenv("SMJ_HEAVY", "0")
     rng = np.random.default_rng(2)
     n = 1_000_000
     keys = rng.integers(10, 10 ** 6, size=n)
@@ -247,12 +249,14 @@ def test_long_equal_key_runs_in_lds(gpu, oracle_built, nkeys, n, cols):
 
 
 @pytest.mark.parametrize("c1,c2,sel", [(2, 2, None), (3, 4, (2, -(1 << 62) + (1 << 58)))])
-def test_many_oversized_groups_batched(gpu, oracle_built, c1, c2, sel):
+def test_many_oversized_groups_batched(gpu, oracle_built, monkeypatch, c1, c2, sel):
     """Hundreds of oversized multi-key groups (the shape Zipf tables produce
     at C5's size: two neighbouring keys with ~600 rows each share one
     sub-bucket of a wide bucket), some present in one table only: all of them
-    go through the one batched gather / sort / join of the fallback."""
+    go through the one batched gather / sort / join of the fallback (heavy-key
+    sub-buckets off: this test is about the fallback tier)."""
     from smj import ops
+    monkeypatch.setenv("SMJ_HEAVY", "0")
     rng = np.random.default_rng(c1 + c2)
     heavy = rng.choice(1 << 40, 600, replace=False) * 4
 
@@ -288,8 +292,11 @@ def test_small_span_oversized_groups_on_device(gpu, oracle_built, monkeypatch, k
     sub-bucket, a group of several chunks, the key in column 1 and a WHERE.
     giant: the groups over the one-workgroup limit (lowered here from 65536
     to 2048 rows) go through the job split (msd_giant_*: per-job counts,
-    scatter and join launches; jobs of 2048 rows)."""
+    scatter and join launches; jobs of 2048 rows).  Heavy-key sub-buckets are
+    turned off here (SMJ_HEAVY=0): with them most of these groups would not
+    exist (test_heavy_keys_get_own_sub_buckets)."""
     from smj import ops
+    monkeypatch.setenv("SMJ_HEAVY", "0")
     if giant:
         monkeypatch.setenv("SMJ_BG_MAX_ROWS", "2048")
         monkeypatch.setenv("SMJ_BG_SEG", "2048")
@@ -331,8 +338,10 @@ def test_oversized_groups_many_distinct_keys(gpu, oracle_built, monkeypatch, gia
     the parallel ranking's 256 compact ids (dense clusters: ~3,000 rows over
     ~2,000 consecutive key values inside a sparse 2^31 key range) take the
     wave-serial ranking; clusters of < 256 distinct keys take the compact-id
-    one -- both in one call, bit-exact against the oracle."""
+    one -- both in one call, bit-exact against the oracle (heavy-key
+    sub-buckets off: this test is about the big-group tiers)."""
     from smj import ops
+    monkeypatch.setenv("SMJ_HEAVY", "0")
     if giant:
         monkeypatch.setenv("SMJ_BG_MAX_ROWS", "2048")
         monkeypatch.setenv("SMJ_BG_SEG", "2048")
@@ -557,3 +566,59 @@ def test_random_shapes_match_oracle(gpu, oracle_built, seed):
     np.testing.assert_array_equal(host(gS), Ss.reshape(-1, c2))
     if nr and ns:
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
+
+
+@pytest.mark.parametrize("kc,sel,skew", [(0, None, 1100), (1, (1, 1 << 22), 1100), (0, None, 400)])
+def test_heavy_keys_get_own_sub_buckets(gpu, oracle_built, monkeypatch, kc, sel, skew):
+    """The Zipf shape of C5 -- keys with thousands of rows among light keys in
+    the same narrow sub-buckets -- with heavy-key sub-buckets on (the
+    default): msd_heavy_kernel finds the heavy keys from a sample of every
+    bucket, the pass-B digit gives each a sub-bucket of its own (lin + 2 c +
+    e, order-preserving), and they stream as single-key groups instead of
+    oversized multi-key groups.  Bit-exact against the oracle, keys heavy in
+    one table only, adjacent heavy keys, the key in column 1, a WHERE; and
+    fewer device-sorted oversized groups than with the feature off."""
+    from smj import ops
+    rng = np.random.default_rng(29 + kc + skew)
+    span = 1 << 24
+    heavy = rng.choice(span - 2, 240, replace=False)
+
+    def make(n, pay0, drop):
+        keys = [rng.integers(0, span, n)]
+        for i, v in enumerate(heavy):
+            if i % 9 == drop:  # heavy in the other table only
+                continue
+            keys.append(np.full(skew + (i * 37) % 2400, v))
+            if i % 5 == 0:  # a second heavy key next to it
+                keys.append(np.full(skew - 50 + (i * 53) % 900, v + 1))
+        keys.append(np.full(9000, heavy[7]))
+        k = rng.permutation(np.concatenate(keys))
+        t = np.empty((len(k), 2), dtype=np.int64)
+        t[:, kc] = k
+        t[:, 1 - kc] = pay0 + np.arange(len(k))
+        return t
+
+    R, S = make(3_000_000, 0, 2), make(2_500_000, 10 ** 9, 4)
+    Rs, Ss, J = ref_pipeline(R, S, kc, kc, sel, sel)
+    monkeypatch.setenv("SMJ_HEAVY", "0")
+    ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, sel)
+    big_off = ops.msd_stats()[1]
+    monkeypatch.setenv("SMJ_HEAVY", "1")
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, sel)
+    single_on, big_on = ops.msd_stats()[0], ops.msd_stats()[1]
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    assert single_on > 100 and big_on < big_off / 4, (single_on, big_on, big_off)
+    # one table alone (smj_dev_select_sort)
+    gS1 = ops.select_sort(dev(S), kc, *(sel if sel else (0, None)))
+    np.testing.assert_array_equal(host(gS1), Ss.reshape(-1, 2))
+    # partitioned mode (the parts' pipelines each find their own heavy keys)
+    ops.force_parts(3)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, sel)
+    finally:
+        ops.force_parts(0)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
