@@ -981,6 +981,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         sp.ntab = ntab;
         sp.spl = ms->spl;
         sp.samp = ms->samp;
+        sp.plan = ms->plan;
         ProfScope ps("msd_sample", 0, s);
         if (stg) {
             host_sample(in, *stg, ntab, ms->h_samp);
@@ -1079,6 +1080,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
             hp.ntab = ntab;
             hp.heavy = ms->heavy;
             hp.nheavy = ms->nheavy;
+            hp.plan = ms->plan;
             ProfScope ps("msd_heavy", 0, s);
             HIP_TRY(launch_msd_heavy(hp, s));
         }

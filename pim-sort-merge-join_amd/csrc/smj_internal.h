@@ -247,6 +247,7 @@ struct MsdSampleParams {
     int ntab;
     int64_t *spl;        // out: kSplA splitters
     int64_t *samp;       // scratch: 2 kSampleMax samples + per-block valid counts
+    struct MsdPlan *plan;  // out (select kernel): plan->skew, sampled keys with an equal partner (nullptr: not counted)
 };
 struct MsdPartAParams {
     const int64_t *src;
@@ -302,6 +303,7 @@ struct MsdHeavyParams {
     int ntab;
     int64_t *heavy;            // out: [kBucketsA][kHeavyMax] ascending heavy keys
     uint32_t *nheavy;          // out: [kBucketsA] their count
+    const struct MsdPlan *plan;  // plan->skew (msd_sample_select)
 };
 struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t m[2];       // selected rows per table
@@ -324,6 +326,7 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
                          // Every kernel after msd_group_kernel returns at entry once err != 0
                          // (msd_plan_failed), so a failed plan never drives a gather or a store.
     uint32_t gticket;    // msd_group_kernel: bucket tickets, taken in the order workgroups start
+    uint32_t skew;       // msd_sample_select: sampled keys that another sample repeats (skew: msd_heavy_kernel runs)
 };
 // A kernel launched after msd_group_kernel reads the plan's error word first:
 // a set bit means the dense group array may hold slots this call never wrote.

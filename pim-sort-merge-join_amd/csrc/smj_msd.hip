@@ -294,6 +294,7 @@ constexpr int kSelSamples = 32, kSelSlices = 32;
 __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSampleParams p) {
     __shared__ int64_t s_key[kSampleN];
     __shared__ uint32_t s_rank[kSelSlices][kSelSamples];
+    __shared__ uint32_t s_eq[kSelSlices][kSelSamples];
     __shared__ uint32_t s_m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     {
@@ -312,21 +313,30 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
     const uint32_t M = s_m;
     const int li = lane & 31, i = blockIdx.x * kSelSamples + li, part = 2 * w + (lane >> 5);
     const int64_t my = s_key[i];
-    uint32_t r = 0;
+    uint32_t r = 0, eq = 0;
     constexpr int SL = kSampleN / kSelSlices;
     const int j0 = part * SL;
 #pragma unroll 8
     for (int j = j0; j < j0 + SL; j++) {
         const int64_t o = s_key[j];
         r += (o < my || (o == my && j < i)) ? 1u : 0u;
+        eq += (o == my) ? 1u : 0u;  // itself included
     }
     s_rank[part][li] = r;
+    s_eq[part][li] = eq;
     __syncthreads();
     if (tid < kSelSamples) {
-        uint32_t rank = 0;
+        uint32_t rank = 0, e = 0;
 #pragma unroll
-        for (int q = 0; q < kSelSlices; q++) rank += s_rank[q][tid];
+        for (int q = 0; q < kSelSlices; q++) {
+            rank += s_rank[q][tid];
+            e += s_eq[q][tid];
+        }
         const int64_t key = s_key[blockIdx.x * kSelSamples + tid];
+        // skew signal: sampled keys some other sample repeats (uniform keys
+        // over a range >> the sample: ~0 of them; Zipf: thousands)
+        const uint64_t rep = __ballot(e > 1u && key != INT64_MAX && rank < M);
+        if (tid == 0 && rep && p.plan) atomicAdd(&p.plan->skew, (uint32_t)__popcll(rep));
         if (M > 0 && rank < M)
             for (int q = 0; q < kSplA; q++)
                 if (min(M - 1, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))) == rank) p.spl[q] = key;
@@ -830,19 +840,20 @@ __global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanPara
 // evenly spaced pass-A tile's run of the bucket, sorted in LDS (bitonic); a
 // key sampled at least thr times -- ~kHeavyRows rows of the bucket's L --
 // is heavy (the kHeavyMax most sampled when more qualify).  Runs only when the
-// pass-A sample already shows skew (a repeated splitter) and for multi-key
+// pass-A sample already shows skew (kHeavySkew of its keys repeated, or a
+// repeated splitter) and for multi-key
 // buckets over 8 kGroupCap rows; elsewhere the bucket gets none.  A missed
 // heavy key only costs speed (its sub-bucket takes the oversized-group path),
 // a light key taken for heavy only a single-key group of its own: the sort
 // and join never depend on the sample.
-constexpr int kHeavyThreads = 1024;
+constexpr int kHeavyThreads = 256;  // small: on unskewed tables every workgroup only reads the gate and exits
+constexpr uint32_t kHeavySkew = 8;  // sampled keys repeated within the pass-A sample that open the gate
 __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavyParams p) {
-    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads;
-    static_assert(kHeavySamples == 2 * kHeavyThreads, "two sampled rows per thread");
+    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads, PAIRS = kHeavySamples / 2;
     __shared__ int64_t s_k[kHeavySamples];
     __shared__ uint32_t s_wsum[NW], s_skew, s_cnt;
     const int a = blockIdx.x, t = threadIdx.x;
-    if (t == 0) s_skew = 0;
+    if (t == 0) s_skew = p.plan->skew >= kHeavySkew ? 1u : 0u;
     __syncthreads();
     if (t + 1 < kSplA && p.spl[t] == p.spl[t + 1]) s_skew = 1;  // benign race: all write 1
     __syncthreads();
@@ -874,26 +885,35 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
     __syncthreads();
     for (uint32_t k = 2; k <= (uint32_t)kHeavySamples; k <<= 1)  // bitonic sort, ascending
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t i = (((uint32_t)t & ~(j - 1u)) << 1) | ((uint32_t)t & (j - 1u)), l = i + j;
-            const int64_t u = s_k[i], v = s_k[l];
-            if ((u > v) == ((i & k) == 0)) {
-                s_k[i] = v;
-                s_k[l] = u;
+#pragma unroll
+            for (int q = 0; q < PAIRS / kHeavyThreads; q++) {
+                const uint32_t pr = (uint32_t)t + (uint32_t)q * kHeavyThreads;
+                const uint32_t i = ((pr & ~(j - 1u)) << 1) | (pr & (j - 1u)), l = i + j;
+                const int64_t u = s_k[i], v = s_k[l];
+                if ((u > v) == ((i & k) == 0)) {
+                    s_k[i] = v;
+                    s_k[l] = u;
+                }
             }
             __syncthreads();
         }
-    // runs of equal sampled keys: this thread's positions q = t, t + 1024
+    // runs of equal sampled keys over this thread's positions [PER t, PER t + PER)
     uint32_t len[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        const uint32_t q = (uint32_t)t + (uint32_t)k * kHeavyThreads;
+        const uint32_t q = (uint32_t)t * PER + (uint32_t)k;
         const int64_t v = s_k[q];
         len[k] = 0;
         if (v != INT64_MAX && (q == 0 || s_k[q - 1] != v)) {  // a run starts at q: its end by binary search
             uint32_t lo = q, n = (uint32_t)kHeavySamples - q;
             while (n) {
                 const uint32_t h = n >> 1;
-                if (s_k[lo + h] <= v) { lo += h + 1; n -= h + 1; } else n = h;
+                if (s_k[lo + h] <= v) {
+                    lo += h + 1;
+                    n -= h + 1;
+                } else {
+                    n = h;
+                }
             }
             len[k] = lo - q;
         }
@@ -913,15 +933,20 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
         if (tot <= (uint32_t)kHeavyMax) break;
         thr = thr + thr / 2 + 1;
     }
-    // the qualifying keys in ascending order: positions q = t (first half), then t + 1024
-    uint32_t tot0, tot1;
-    const uint32_t f0 = len[0] >= thr ? 1u : 0u, f1 = len[1] >= thr ? 1u : 0u;
-    const uint32_t e0 = block_excl_scan<NW>(f0, s_wsum, &tot0);
-    const uint32_t e1 = block_excl_scan<NW>(f1, s_wsum, &tot1);
+    // the qualifying keys, ascending (positions are contiguous per thread)
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) c += len[k] >= thr ? 1u : 0u;
+    uint32_t tot;
+    uint32_t e = block_excl_scan<NW>(c, s_wsum, &tot);
     int64_t *hv = p.heavy + (int64_t)a * kHeavyMax;
-    if (f0 && e0 < (uint32_t)kHeavyMax) hv[e0] = s_k[t];
-    if (f1 && tot0 + e1 < (uint32_t)kHeavyMax) hv[tot0 + e1] = s_k[t + kHeavyThreads];
-    if (t == 0) p.nheavy[a] = min(tot0 + tot1, (uint32_t)kHeavyMax);
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+        if (len[k] >= thr) {
+            if (e < (uint32_t)kHeavyMax) hv[e] = s_k[(uint32_t)t * PER + (uint32_t)k];
+            e++;
+        }
+    if (t == 0) p.nheavy[a] = min(tot, (uint32_t)kHeavyMax);
 }
 
 // one workgroup of kOffsA threads: thread = bucket.  Bucket sizes / bases of
@@ -1333,11 +1358,15 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const bool v = lrow0 + it * 64 < nrows;
-            const int64_t key = pick<COLS>(rows[it], p.key_col);
-            uint32_t d = pb_lin(b, (uint64_t)key - (uint64_t)b.lo);
-            if (hm) d = pb_digit_heavy(d, s_hv, hm, key);
+            const uint32_t d = pb_lin(b, (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo);
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
+        }
+        if (__builtin_expect(hm != 0u, 0)) {  // heavy keys in the bucket (C5): lin + 2 c + e
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u)
+                    dig[it] = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
         }
         // Atomic path: per quad of waves one u16 count per sub-bucket, ranks in
         // atomic order.  Stability is restored per row below among the rows
@@ -1613,11 +1642,15 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const bool v = lrow0 + it * 64 < nrows;
-            const int64_t key = pick<COLS>(rows[it], p.key_col);
-            uint32_t d = pb_lin(b, (uint64_t)key - (uint64_t)b.lo);
-            if (hm) d = pb_digit_heavy(d, s_hv, hm, key);
+            const uint32_t d = pb_lin(b, (uint64_t)pick<COLS>(rows[it], p.key_col) - (uint64_t)b.lo);
             dig[it] = v ? d & (RADIX - 1) : 0u;
             vmask |= v ? (1u << it) : 0u;
+        }
+        if (__builtin_expect(hm != 0u, 0)) {  // heavy keys in the bucket (C5): lin + 2 c + e
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u)
+                    dig[it] = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
         }
         // a heavy key's own bucket (one key value): every row falls in
         // sub-bucket 0 and the tile's gather order is already its stable
@@ -2437,7 +2470,8 @@ constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re
 #define SMJ_ST_FOLDSCAN 1  // the staged kernel's join-row scan shares the st_issue_lists barrier
 #endif
 #ifndef SMJ_ST_RUNFIX
-#define SMJ_ST_RUNFIX 8  // the staged kernel: groups whose longest equal-key run is <= this sort runs in one pass
+#define SMJ_ST_RUNFIX 0  // the staged kernel: groups whose longest equal-key run is <= this sort runs in one pass
+                         // (off: r05d same-box A/B, msd_final 1.78 -> 1.86 ms at 8 -- one lane holding its wave)
 #endif
 #ifndef SMJ_ST_MAXRUN
 #define SMJ_ST_MAXRUN kMaxDupRun  // the staged kernel: longer runs take the in-LDS LSD (<= kMaxDupRun)
