@@ -835,10 +835,10 @@ __global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanPara
     if (w == 0) p.tot[blockIdx.y][a] = tot;
 }
 
-// Heavy keys of bucket a = blockIdx.x (1024 threads): kHeavySamples rows of
-// the bucket, both tables in proportion to their rows, each one row of an
-// evenly spaced pass-A tile's run of the bucket, sorted in LDS (bitonic); a
-// key sampled at least thr times -- ~kHeavyRows rows of the bucket's L --
+// Heavy keys of bucket a = blockIdx.x: kHeavySamples rows of the bucket, both
+// tables in proportion to their rows, each one row of an evenly spaced pass-A
+// tile's run of the bucket, counted in an LDS hash table; a key sampled at
+// least thr times -- ~kHeavyRows rows of the bucket's L --
 // is heavy (the kHeavyMax most sampled when more qualify).  Runs only when the
 // pass-A sample already shows skew (kHeavySkew of its keys repeated, or a
 // repeated splitter) and for multi-key
@@ -848,10 +848,14 @@ __global__ __launch_bounds__(1024) void msd_seg_scan_kernel(const MsdSegScanPara
 // and join never depend on the sample.
 constexpr int kHeavyThreads = 256;  // small: on unskewed tables every workgroup only reads the gate and exits
 constexpr uint32_t kHeavySkew = 8;  // sampled keys repeated within the pass-A sample that open the gate
+constexpr int kHeavySlots = 2 * kHeavySamples;  // LDS hash table of the sampled keys (load <= 1/2)
 __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavyParams p) {
-    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads, PAIRS = kHeavySamples / 2;
-    __shared__ int64_t s_k[kHeavySamples];
-    __shared__ uint32_t s_wsum[NW], s_skew, s_cnt;
+    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads, SPT = kHeavySlots / kHeavyThreads;
+    constexpr unsigned long long kEmpty = (unsigned long long)INT64_MAX;  // (an INT64_MAX key is never counted)
+    __shared__ unsigned long long s_hk[kHeavySlots];
+    __shared__ uint32_t s_hc[kHeavySlots];
+    __shared__ int64_t s_cand[kHeavyMax];
+    __shared__ uint32_t s_skew, s_cnt;
     const int a = blockIdx.x, t = threadIdx.x;
     if (t == 0) s_skew = p.plan->skew >= kHeavySkew ? 1u : 0u;
     __syncthreads();
@@ -864,60 +868,47 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
         if (t == 0) p.nheavy[a] = 0;
         return;
     }
+#pragma unroll
+    for (int k = 0; k < SPT; k++) {
+        s_hk[t + k * kHeavyThreads] = kEmpty;
+        s_hc[t + k * kHeavyThreads] = 0;
+    }
+    // the samples: row j of table x from an evenly spaced pass-A tile's run of the bucket
     const uint32_t n0 = p.ntab > 1 ? (uint32_t)(((uint64_t)kHeavySamples * L0 + L / 2) / L) : (uint32_t)kHeavySamples;
+    int64_t key[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const uint32_t i = (uint32_t)t + (uint32_t)k * kHeavyThreads;
         const int x = i < n0 ? 0 : 1;
         const uint32_t j = x ? i - n0 : i, nx = x ? kHeavySamples - n0 : n0;
-        int64_t key = INT64_MAX;  // no sample
+        key[k] = INT64_MAX;  // no sample
         if (j < nx && p.ntiles[x] > 0) {
             const int64_t tile = (int64_t)(((unsigned __int128)j * (uint64_t)p.ntiles[x]) / nx);
             const uint32_t *o = p.offs[x] + tile * kOffsARow;
             const uint32_t s0 = o[a], s1 = o[a + 1];  // o[kBucketsA] = the tile's rows
             if (s1 > s0) {
                 const uint32_t r = s0 + (uint32_t)(((uint64_t)(j * 0x9E3779B9u) * (s1 - s0)) >> 32);
-                key = p.tempA[x][((int64_t)tile * p.tile[x] + r) * p.cols[x] + p.key[x]];
+                key[k] = p.tempA[x][((int64_t)tile * p.tile[x] + r) * p.cols[x] + p.key[x]];
             }
         }
-        s_k[i] = key;
     }
     __syncthreads();
-    for (uint32_t k = 2; k <= (uint32_t)kHeavySamples; k <<= 1)  // bitonic sort, ascending
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int q = 0; q < PAIRS / kHeavyThreads; q++) {
-                const uint32_t pr = (uint32_t)t + (uint32_t)q * kHeavyThreads;
-                const uint32_t i = ((pr & ~(j - 1u)) << 1) | (pr & (j - 1u)), l = i + j;
-                const int64_t u = s_k[i], v = s_k[l];
-                if ((u > v) == ((i & k) == 0)) {
-                    s_k[i] = v;
-                    s_k[l] = u;
-                }
-            }
-            __syncthreads();
-        }
-    // runs of equal sampled keys over this thread's positions [PER t, PER t + PER)
-    uint32_t len[PER];
+    // count them in an LDS hash table (linear probing; <= half full)
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        const uint32_t q = (uint32_t)t * PER + (uint32_t)k;
-        const int64_t v = s_k[q];
-        len[k] = 0;
-        if (v != INT64_MAX && (q == 0 || s_k[q - 1] != v)) {  // a run starts at q: its end by binary search
-            uint32_t lo = q, n = (uint32_t)kHeavySamples - q;
-            while (n) {
-                const uint32_t h = n >> 1;
-                if (s_k[lo + h] <= v) {
-                    lo += h + 1;
-                    n -= h + 1;
-                } else {
-                    n = h;
-                }
+        if (key[k] == INT64_MAX) continue;
+        const unsigned long long u = (unsigned long long)key[k];
+        uint32_t h = (uint32_t)((u * 0x9E3779B97F4A7C15ull) >> 52) & (kHeavySlots - 1);
+        for (int probe = 0; probe < kHeavySlots; probe++) {
+            const unsigned long long prev = atomicCAS(&s_hk[h], kEmpty, u);
+            if (prev == kEmpty || prev == u) {
+                atomicAdd(&s_hc[h], 1u);
+                break;
             }
-            len[k] = lo - q;
+            h = (h + 1) & (kHeavySlots - 1);
         }
     }
+    __syncthreads();
     // hits for ~kHeavyRows rows of the bucket; raised until <= kHeavyMax keys qualify
     uint32_t thr = max(3u, (uint32_t)(((uint64_t)kHeavySamples * kHeavyRows + L - 1) / L));
     for (int round = 0; round < 16; round++) {
@@ -925,7 +916,7 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
         __syncthreads();
         uint32_t c = 0;
 #pragma unroll
-        for (int k = 0; k < PER; k++) c += len[k] >= thr ? 1u : 0u;
+        for (int k = 0; k < SPT; k++) c += s_hc[t + k * kHeavyThreads] >= thr ? 1u : 0u;
         if (c) atomicAdd(&s_cnt, c);
         __syncthreads();
         const uint32_t tot = s_cnt;
@@ -933,20 +924,26 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
         if (tot <= (uint32_t)kHeavyMax) break;
         thr = thr + thr / 2 + 1;
     }
-    // the qualifying keys, ascending (positions are contiguous per thread)
-    uint32_t c = 0;
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PER; k++) c += len[k] >= thr ? 1u : 0u;
-    uint32_t tot;
-    uint32_t e = block_excl_scan<NW>(c, s_wsum, &tot);
-    int64_t *hv = p.heavy + (int64_t)a * kHeavyMax;
-#pragma unroll
-    for (int k = 0; k < PER; k++)
-        if (len[k] >= thr) {
-            if (e < (uint32_t)kHeavyMax) hv[e] = s_k[(uint32_t)t * PER + (uint32_t)k];
-            e++;
+    for (int k = 0; k < SPT; k++) {
+        const int i = t + k * kHeavyThreads;
+        if (s_hc[i] >= thr) {
+            const uint32_t at = atomicAdd(&s_cnt, 1u);
+            if (at < (uint32_t)kHeavyMax) s_cand[at] = (int64_t)s_hk[i];
         }
-    if (t == 0) p.nheavy[a] = min(tot, (uint32_t)kHeavyMax);
+    }
+    __syncthreads();
+    // ascending: each candidate's rank among the (distinct) candidates
+    const uint32_t m = min(s_cnt, (uint32_t)kHeavyMax);
+    if ((uint32_t)t < m) {
+        const int64_t v = s_cand[t];
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < m; i++) r += s_cand[i] < v ? 1u : 0u;
+        p.heavy[(int64_t)a * kHeavyMax + r] = v;
+    }
+    if (t == 0) p.nheavy[a] = m;
 }
 
 // one workgroup of kOffsA threads: thread = bucket.  Bucket sizes / bases of
@@ -1632,9 +1629,25 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // or after the next tile's gathers as before, is waited with vmcnt(0),
         // which also retires the gathers and the previous tile's stores)
         const uint2 tn2 = sc_tinfo(p.tinfo, min(gn + (int64_t)gridDim.x, ntl - 1));
-        // the tile's bucket's heavy keys (C5; block-uniform: no load, no wait elsewhere)
+        // the tile's bucket's heavy keys (C5; block-uniform: none elsewhere).
+        // Eight per wave through scalar loads: an SMEM wait is on lgkmcnt, so
+        // it does not retire this tile's gathers and the previous tile's
+        // stores, as the vmcnt wait of a vector load here would (every tile
+        // of a heavy bucket then drained its stores: C5 part_b +1 ms, r05e)
         const uint32_t hm = msd_heavy_count(b.one_key);
-        if (hm && (uint32_t)tid < hm) s_hv[tid] = p.heavy[(int64_t)ti.x * kHeavyMax + tid];
+        if (hm) {
+            const uint32_t w8 = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 8u;
+            if (w8 < hm) {
+                SMJ_CONST(int64_t) *hq =
+                    (SMJ_CONST(int64_t) *)uni64((uint64_t)(p.heavy + (int64_t)ti.x * kHeavyMax + w8));
+                const int64_t h0 = hq[0], h1 = hq[1], h2 = hq[2], h3 = hq[3], h4 = hq[4], h5 = hq[5], h6 = hq[6],
+                              h7 = hq[7];
+                const int l8 = lane & 7;
+                const int64_t v = l8 == 0 ? h0 : l8 == 1 ? h1 : l8 == 2 ? h2 : l8 == 3 ? h3 : l8 == 4 ? h4
+                                                                                           : l8 == 5 ? h5 : l8 == 6 ? h6 : h7;
+                if (lane < 8 && w8 + (uint32_t)lane < hm) s_hv[w8 + lane] = v;
+            }
+        }
         __syncthreads();
 
         uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
@@ -2124,8 +2137,8 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         bool hv_only = false;  // the group is one heavy key's sub-bucket
         uint32_t hj = 0;
         if (hm && b1 == b0 + 1) hj = heavy_below(b0, hv_only);
-        if (hv_only)
-            gr.flags = kGroupSingle;  // whatever its size: streamed in stable order, no sort
+        if (hv_only)  // one key: the staged kernel's no-sort path when it fits a combined group, else streamed
+            gr.flags = comb && gr.nR + gr.nS <= (uint32_t)kStRows ? (uint16_t)0 : kGroupSingle;
         else if (comb ? gr.nR + gr.nS > (uint32_t)kStRows : (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap))
             gr.flags = single_sub ? kGroupSingle : kGroupBig;
 #pragma unroll
@@ -3264,6 +3277,11 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // the barriers below order this before its atomicOr)
     for (int i = tid; i < kStRows / 32; i += kStThreads) sm.L.starts[i] = 0;
     const int kc0 = p.tab[0].key, kc1 = p.tab[1].key;
+    // one key value (a heavy key's group, msd_heavy_kernel; combined layout
+    // only): the gather order is already the stable sorted order -- the sort
+    // words are the identity, nothing is counted, and R position i pairs with
+    // S position i (below)
+    const bool one = COMB && g.span == 1u;  // block-uniform
 #pragma unroll
     for (int k = 0; k < kStIt; k++) {
         const int v = tid + k * kStThreads;
@@ -3272,9 +3290,13 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             const bool x = L.is_s(k, (uint32_t)v);
             const int kc = x ? kc1 : kc0;
             sm.pay[v] = kc ? rows[k].x : rows[k].y;
-            const uint32_t res = (uint32_t)((uint64_t)st_key(rows[k], kc) - (uint64_t)g.base);
-            const uint32_t sh = 16u * (res & 1u);
-            w[k] = (res << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][res >> 1], 1u << sh) >> sh) & 0xffffu);
+            if (one) {
+                sm.key[v] = (uint32_t)v;
+            } else {
+                const uint32_t res = (uint32_t)((uint64_t)st_key(rows[k], kc) - (uint64_t)g.base);
+                const uint32_t sh = 16u * (res & 1u);
+                w[k] = (res << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][res >> 1], 1u << sh) >> sh) & 0xffffu);
+            }
         }
     }
     __syncthreads();
@@ -3427,7 +3449,18 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     constexpr int JI = COMB ? kStIt : kStIt / 2;
 #pragma unroll
     for (int q = 0; q < kStIt; q++) part[q] = 0;
-    if (p.join && nR > 0 && nS > 0) {
+    if (one) {
+        if (p.join) {
+#pragma unroll
+            for (int q = 0; q < JI; q++) {
+                const uint32_t i = (uint32_t)tid * JI + q;
+                if (i < nR && i < nS) {
+                    part[q] = i;
+                    mmask |= 1u << q;
+                }
+            }
+        }
+    } else if (p.join && nR > 0 && nS > 0) {
 #pragma unroll
         for (int q = 0; q < JI; q++) {
             const uint32_t i = (uint32_t)tid * JI + q;

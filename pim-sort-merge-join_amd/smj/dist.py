@@ -93,8 +93,11 @@ def default_stages(world):
 # RCCL exchange on a one-GPU box
 LOOPBACK = os.environ.get("SMJ_DIST_LOOPBACK", "0") == "1"
 # diagnostics: SMJ_DIST_TRACE=1 synchronises after every phase and prints its
-# wall time (rank 0, stderr) -- it serialises the overlap, so never in a timed run
-TRACE = os.environ.get("SMJ_DIST_TRACE", "0") == "1"
+# wall time (rank 0, stderr) -- it serialises the overlap, so never in a timed
+# run; SMJ_DIST_TRACE=2 prints the host's progress without synchronising (where
+# the host thread is when a run stalls)
+TRACE_MODE = os.environ.get("SMJ_DIST_TRACE", "0")
+TRACE = TRACE_MODE in ("1", "2")
 
 
 class _Tracer:
@@ -106,7 +109,8 @@ class _Tracer:
     def __call__(self, what):
         if not self.on:
             return
-        torch.cuda.synchronize()
+        if TRACE_MODE == "1":
+            torch.cuda.synchronize()
         t = self.time.perf_counter()
         import sys
         print(f"smj.dist trace: {what}: {(t - self.t) * 1e3:.2f} ms", file=sys.stderr, flush=True)
@@ -698,6 +702,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
             # the current stream's work, and they must not wait for the sort
             side.wait_stream(torch.cuda.current_stream())
             job = begin(Rk, Sk, k1, k2, None, None, stream=side)
+            tr(f"stage {k} pipeline begun")
         if k + 1 < K:
             try:
                 pending = [post_stage(k + 1, K, sends, regs, sl, rank, world, R.device, group, loopback)]
@@ -705,6 +710,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
                 if job is not None:  # the thread's pipeline scratch is the job's until it ends
                     job.end()
                 raise
+            tr(f"stage {k + 1} posted")
         if Rk.shape[0] == 0 or Sk.shape[0] == 0:
             continue
         if job is not None:
