@@ -183,6 +183,8 @@ for s in $STEPS; do
     dbg4s) SMJ_DIST_TRACE=2 SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run dbg4s 170 python -u bench.py --loopback --workload c4 --steps 2 --warmup 1 $NOCPU ;;
     dbg4h0) SMJ_HEAVY=0 SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run dbg4h0 170 python -u bench.py --loopback --workload c4 --steps 2 --warmup 1 $NOCPU ;;
     seqb)  SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seqb 170 python -u tools/seq_sizes.py ;;
+    sb:*)  # sb:SEQ -- the size-sequence probe on the bounds-checking build (reports instead of faulting)
+           q=${s#sb:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so SMJ_DEBUG_PART1=1 run sb_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
     seq)   SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seq 170 python -u tools/seq_sizes.py ;;
     dbg4n) SMJ_DIST_S_SIDE=0 SMJ_DIST_TRACE=1 SMJ_DEBUG_PART1=1 run dbg4n 170 python -u bench.py --loopback --workload c4 --steps 1 --warmup 0 $NOCPU ;;
     abh5)  for r in 1 2; do  # same-box A/B of heavy-key sub-buckets on C5
