@@ -262,13 +262,19 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
                         ? jj
                         : min(t.n - 1, ((2 * (int64_t)(jj / kSampleRun) + 1) * t.n) / (2 * kClusters) +
                                            jj % kSampleRun);
+        bool dup = false;
         if (t.desc) {  // a chunked part: row r of tile r / tile (clamped to the tile's rows) -- any row of it samples
             const uint64_t d = t.desc[min(t.ntiles - 1, r / t.tile)];
-            r = (int64_t)(d >> 16) + min(r % t.tile, (int64_t)(d & 0xffffu) - 1);
+            const int64_t rows = (int64_t)(d & 0xffffu);
+            // a clamped sample after its cluster's first repeats the row before
+            // it: dropped, so that the sample's repeated keys (plan->skew, the
+            // heavy-key gate) are repeated keys of the table, not of the clamp
+            dup = r % t.tile >= rows && jj % kSampleRun != 0;
+            r = (int64_t)(d >> 16) + min(r % t.tile, rows - 1);
         }
         const int64_t *row = t.src + r * t.cols;
         const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
-        if (!t.use_sel || sv > t.sel_val) {
+        if (!dup && (!t.use_sel || sv > t.sel_val)) {
             k = kv;
             valid = 1;
         }

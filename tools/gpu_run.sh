@@ -32,7 +32,7 @@ run() {  # name timeout cmd...   (rc 1 tolerated: a bench step's stderr is read 
   echo "[$(date +%T)] $name rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" | tee -a "$OUT/steps.log"; exit $rc; fi
   # a GPU fault inside a Python step surfaces as an exception (rc 1): stop there too
-  if [ $rc -ne 0 ] && grep -qE "HSA_STATUS_ERROR|Memory access fault|hardware exception|unspecified launch failure|hipErrorLaunchFailure|page not present" "$OUT/$name.err"; then
+  if [ $rc -ne 0 ] && grep -qE "HSA_STATUS_ERROR|Memory access fault|hardware exception|unspecified launch failure|hipErrorLaunchFailure|page not present|illegal memory access" "$OUT/$name.err"; then
     echo "stopping after $name (GPU fault in stderr)" | tee -a "$OUT/steps.log"; exit 3
   fi
   return $rc
@@ -185,6 +185,8 @@ for s in $STEPS; do
     seqb)  SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seqb 170 python -u tools/seq_sizes.py ;;
     sb:*)  # sb:SEQ -- the size-sequence probe on the bounds-checking build (reports instead of faulting)
            q=${s#sb:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so SMJ_DEBUG_PART1=1 run sb_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
+    sr4:*) # sr4:SEQ -- the same probe on round 4's library (db75936) built with the bounds checks
+           q=${s#sr4:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/r4b/libsmj_hip.so SMJ_DEBUG_PART1=1 run sr4_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
     seq)   SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seq 170 python -u tools/seq_sizes.py ;;
     dbg4n) SMJ_DIST_S_SIDE=0 SMJ_DIST_TRACE=1 SMJ_DEBUG_PART1=1 run dbg4n 170 python -u bench.py --loopback --workload c4 --steps 1 --warmup 0 $NOCPU ;;
     abh5)  for r in 1 2; do  # same-box A/B of heavy-key sub-buckets on C5
