@@ -2143,8 +2143,10 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         bool hv_only = false;  // the group is one heavy key's sub-bucket
         uint32_t hj = 0;
         if (hm && b1 == b0 + 1) hj = heavy_below(b0, hv_only);
-        if (hv_only)  // one key: the staged kernel's no-sort path when it fits a combined group, else streamed
+        if (hv_only) {  // one key: the staged kernel's no-sort path when it fits a combined group, else streamed
             gr.flags = comb && gr.nR + gr.nS <= (uint32_t)kStRows ? (uint16_t)0 : kGroupSingle;
+            gr.pad[0] = 1;  // one sub-bucket of a multi-key bucket: msd_single copies it run by run
+        }
         else if (comb ? gr.nR + gr.nS > (uint32_t)kStRows : (gr.nR > (uint32_t)kGroupCap || gr.nS > (uint32_t)kGroupCap))
             gr.flags = single_sub ? kGroupSingle : kGroupBig;
 #pragma unroll
@@ -4416,6 +4418,67 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
     const uint2 w = work[blockIdx.x];
     const MsdGroup g = p.groups[w.x];
     const int tid = threadIdx.x;
+    if (w.y == kSingleWhole) {
+        // a heavy key's sub-bucket b0 of a multi-key bucket (msd_heavy_kernel),
+        // the whole group in this workgroup: its rows are one run per pass-B
+        // tile of the bucket, copied run by run (a wave per run, coalesced) to
+        // the run's place -- the prefix of the earlier runs -- then the zip
+        // join read back from the sorted rows just written (workgroup fence)
+        uint2 *s_run = reinterpret_cast<uint2 *>(s_tmp);  // {tempB row, output row} per tile of a batch
+        uint32_t *s_len = s_addr[0];
+        const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            if (x >= p.ntab) continue;
+            const MsdTab &tb = p.tab[x];
+            const int cols = C1 > 0 ? (x ? C2 : C1) : tb.cols;
+            const MsdBucket bk = tb.bk[g.a];
+            const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
+            int64_t *dst = tb.out + (int64_t)(x ? g.outS : g.outR) * cols;
+            uint32_t carry = 0;
+            for (uint32_t kb = 0; kb < K; kb += kMsdThreads) {
+                const uint32_t nb = min(K - kb, (uint32_t)kMsdThreads);
+                uint32_t len = 0, src = 0;
+                if ((uint32_t)tid < nb) {
+                    const int64_t id = (int64_t)bk.tile_base + kb + tid;
+                    const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
+                    src = (uint32_t)id * (uint32_t)tb.tile + lo;
+                    len = hi - lo;
+                }
+                uint32_t total;
+                const uint32_t ex = carry + block_excl_scan<kMsdWaves>(len, s_wsum, &total);
+                if ((uint32_t)tid < nb) {
+                    s_run[tid] = make_uint2(src, ex);
+                    s_len[tid] = len;
+                }
+                __syncthreads();
+                for (uint32_t j = (uint32_t)wave; j < nb; j += kMsdWaves) {
+                    const uint2 e = s_run[j];
+                    const uint32_t n = s_len[j];
+                    for (uint32_t r = (uint32_t)lane; r < n; r += 64) {
+                        if constexpr (C1 > 0) {
+                            if (x) copy_row<C2>(tb.tempB + (int64_t)(e.x + r) * C2, dst + (int64_t)(e.y + r) * C2, C2);
+                            else copy_row<C1>(tb.tempB + (int64_t)(e.x + r) * C1, dst + (int64_t)(e.y + r) * C1, C1);
+                        } else {
+                            copy_row<0>(tb.tempB + (int64_t)(e.x + r) * cols, dst + (int64_t)(e.y + r) * cols, cols);
+                        }
+                    }
+                }
+                carry += total;
+                __syncthreads();
+            }
+        }
+        if (!p.join) return;
+        __threadfence_block();  // the sorted rows written above, visible to the whole workgroup
+        __syncthreads();
+        const uint32_t m = min(g.nR, p.ntab > 1 ? g.nS : 0u);
+        const int c1 = C1 > 0 ? C1 : p.tab[0].cols, c2 = C2 > 0 ? C2 : p.tab[1].cols, tc = c1 + c2 - 1;
+        const int64_t *oR = p.tab[0].out + (int64_t)g.outR * c1, *oS = p.tab[1].out + (int64_t)g.outS * c2;
+        int64_t *dj = p.slots + (int64_t)g.outR * tc;
+        for (uint32_t v = tid; v < m; v += kMsdThreads)
+            emit_join_row<C1, C2>(oR + (int64_t)v * c1, oS + (int64_t)v * c2, dj + (int64_t)v * tc, c1, c2, p.key2);
+        return;
+    }
     const uint32_t V0 = w.y * (uint32_t)kGroupCap;
     const uint32_t n[2] = {g.nR, p.ntab > 1 ? g.nS : 0u};
     uint2 *s_list = reinterpret_cast<uint2 *>(s_tmp);
