@@ -187,6 +187,8 @@ for s in $STEPS; do
            q=${s#sb:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/bounds/libsmj_hip.so SMJ_DEBUG_PART1=1 run sb_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
     sr4:*) # sr4:SEQ -- the same probe on round 4's library (db75936) built with the bounds checks
            q=${s#sr4:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/r4b/libsmj_hip.so SMJ_DEBUG_PART1=1 run sr4_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
+    sv:*)  # sv:VARIANT:SEQ -- the probe on lib/variants/VARIANT
+           r=${s#sv:}; v=${r%%:*}; q=${r#*:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/$v/libsmj_hip.so SMJ_DEBUG_PART1=1 run sv_${v}_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
     seq)   SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seq 170 python -u tools/seq_sizes.py ;;
     dbg4n) SMJ_DIST_S_SIDE=0 SMJ_DIST_TRACE=1 SMJ_DEBUG_PART1=1 run dbg4n 170 python -u bench.py --loopback --workload c4 --steps 1 --warmup 0 $NOCPU ;;
     abh5)  for r in 1 2; do  # same-box A/B of heavy-key sub-buckets on C5
