@@ -2488,7 +2488,11 @@ static_assert(kGroupCap == (1 << kFinIdxBits), "sort word = residual << 10 | gro
 constexpr int kCountRange = 4096;  // counting-sort residual range (packed u16 bins)
 constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re-orders
 #ifndef SMJ_ST_FOLDSCAN
-#define SMJ_ST_FOLDSCAN 1  // the staged kernel's join-row scan shares the st_issue_lists barrier
+#define SMJ_ST_FOLDSCAN 0  // the staged kernel's join-row scan sharing the st_issue_lists barrier: off --
+                           // neutral in the same-box A/B (r05d), and the size-sequence probe
+                           // (tools/seq_sizes.py, r05i/r05j) caught it with a wrong join count and
+                           // inconsistent run metadata on repeated partitioned calls; off, the probe
+                           // is clean (a race not yet understood)
 #endif
 #ifndef SMJ_ST_RUNFIX
 #define SMJ_ST_RUNFIX 0  // the staged kernel: groups whose longest equal-key run is <= this sort runs in one pass
