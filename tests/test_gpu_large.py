@@ -285,3 +285,29 @@ def test_loopback_full_size_equals_single_call(gpu, workload, stages):
     r = subprocess.run([sys.executable, os.path.join(repo, "tools", "loop_check.py"), "--workload", workload,
                         "--steps", "2"], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_repeated_partitioned_calls_agree(gpu):
+    """Partitioned-mode calls of different sizes in one process, in both the
+    overlapped (two parts in flight) and the profiled (parts in turn) order --
+    the sequence bench.py's C4 loopback verification makes -- each equal to a
+    fresh repetition of itself by the order-sensitive digest of all three
+    outputs (r05f-r05j: a racy staged-kernel change showed up here as a wrong
+    join count and inconsistent run metadata, tools/seq_sizes.py)."""
+    from smj import ops
+    ref = {}
+    for n, prof in ((292_000_000, False), (559_000_000, False), (292_000_000, True), (559_000_000, True),
+                    (559_000_000, True)):
+        R = ops.gen_uniform(n, seed=1, key_range=3 * n)
+        S = ops.gen_uniform(n, seed=2, key_range=3 * n)
+        ops.prof_enable(prof)
+        try:
+            gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, SEL), (0, SEL))
+            torch.cuda.synchronize()
+        finally:
+            ops.prof_enable(False)
+            ops.prof_report()
+        d = (gR.shape[0], gS.shape[0], gJ.shape[0], ops.digest(gR), ops.digest(gS), ops.digest(gJ))
+        assert ref.setdefault(n, d) == d, (n, prof, ref[n], d)
+        del R, S, gR, gS, gJ
+        torch.cuda.empty_cache()
