@@ -701,11 +701,11 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         size_t nw = 0;
         for (const Listed &e : singles) {
             const MsdGroup &g = *e.g;
-            if (g.pad[0] == 1) {  // a heavy key's sub-bucket: one workgroup, run by run
-                work[nw++] = make_uint2(e.slot, kSingleWhole);
+            const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
+            if (g.pad[0] == 1) {  // a heavy key's sub-bucket: run by run, kSingleRunRows a work item
+                for (uint32_t c = 0; c * kSingleRunRows < rows; c++) work[nw++] = make_uint2(e.slot, kSingleRuns | c);
                 continue;
             }
-            const uint32_t rows = std::max(g.nR, ntab > 1 ? g.nS : 0u);
             for (uint32_t c = 0; c * (uint32_t)kGroupCap < rows; c++) work[nw++] = make_uint2(e.slot, c);
         }
         hw_at += nw * sizeof(uint2);

@@ -232,10 +232,11 @@ constexpr int kSampleMax = 4096;           // sampled keys per table
 constexpr int kMsdSegs = SMJ_MSD_SEGS;     // segments of the run scans (x 4 waves: ~24 tiles per lane at 1e8 rows)
 constexpr int kGroupSlices = 8;            // tile slices per bucket in msd_group_sum_kernel
 constexpr uint16_t kGroupEmpty = 1, kGroupSingle = 2, kGroupBig = 4;
-// msd_single_kernel work item {group, kSingleWhole}: the whole group in one
-// workgroup, run by run (a heavy key's sub-bucket: MsdGroup::pad[0] = 1);
-// else {group, chunk of kGroupCap rows}
-constexpr uint32_t kSingleWhole = 0xffffffffu;
+// msd_single_kernel work item {group, kSingleRuns | c}: rows [c R, (c + 1) R)
+// of a heavy key's sub-bucket (MsdGroup::pad[0] = 1), R = kSingleRunRows,
+// copied run by run; else {group, chunk c of kGroupCap rows}
+constexpr uint32_t kSingleRuns = 0x80000000u;
+constexpr uint32_t kSingleRunRows = 8 * 1024;
 
 struct MsdTable {        // an input table as the sampler and part_a see it
     const int64_t *src;

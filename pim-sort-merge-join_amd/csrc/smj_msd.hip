@@ -4422,25 +4422,30 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
     const uint2 w = work[blockIdx.x];
     const MsdGroup g = p.groups[w.x];
     const int tid = threadIdx.x;
-    if (w.y == kSingleWhole) {
-        // a heavy key's sub-bucket b0 of a multi-key bucket (msd_heavy_kernel),
-        // the whole group in this workgroup: its rows are one run per pass-B
-        // tile of the bucket, copied run by run (a wave per run, coalesced) to
-        // the run's place -- the prefix of the earlier runs -- then the zip
-        // join read back from the sorted rows just written (workgroup fence)
+    if (w.y & kSingleRuns) {
+        // a heavy key's sub-bucket b0 of a multi-key bucket (msd_heavy_kernel):
+        // rows [V0, V1) of each table, kSingleRunRows a work item.  The group's
+        // rows are one run per pass-B tile of the bucket; the runs' places are
+        // the prefix of the earlier runs (a scan of their offsB lengths), and
+        // the runs meeting [V0, V1) are copied run by run (a wave per run,
+        // coalesced) -- no per-row search.  The zip join is read back from
+        // the sorted rows just written (workgroup fence).
         uint2 *s_run = reinterpret_cast<uint2 *>(s_tmp);  // {tempB row, output row} per tile of a batch
         uint32_t *s_len = s_addr[0];
         const int lane = tid & 63, wave = tid >> 6;
+        const uint32_t V0 = (w.y & ~kSingleRuns) * kSingleRunRows;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
-            if (x >= p.ntab) continue;
+            const uint32_t nx = x ? (p.ntab > 1 ? g.nS : 0u) : g.nR;
+            if (V0 >= nx) continue;
+            const uint32_t V1 = min(V0 + kSingleRunRows, nx);
             const MsdTab &tb = p.tab[x];
             const int cols = C1 > 0 ? (x ? C2 : C1) : tb.cols;
             const MsdBucket bk = tb.bk[g.a];
             const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
             int64_t *dst = tb.out + (int64_t)(x ? g.outS : g.outR) * cols;
             uint32_t carry = 0;
-            for (uint32_t kb = 0; kb < K; kb += kMsdThreads) {
+            for (uint32_t kb = 0; kb < K && carry < V1; kb += kMsdThreads) {
                 const uint32_t nb = min(K - kb, (uint32_t)kMsdThreads);
                 uint32_t len = 0, src = 0;
                 if ((uint32_t)tid < nb) {
@@ -4458,8 +4463,8 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
                 __syncthreads();
                 for (uint32_t j = (uint32_t)wave; j < nb; j += kMsdWaves) {
                     const uint2 e = s_run[j];
-                    const uint32_t n = s_len[j];
-                    for (uint32_t r = (uint32_t)lane; r < n; r += 64) {
+                    const uint32_t r0 = e.y < V0 ? V0 - e.y : 0u, r1 = min(s_len[j], V1 > e.y ? V1 - e.y : 0u);
+                    for (uint32_t r = r0 + (uint32_t)lane; r < r1; r += 64) {
                         if constexpr (C1 > 0) {
                             if (x) copy_row<C2>(tb.tempB + (int64_t)(e.x + r) * C2, dst + (int64_t)(e.y + r) * C2, C2);
                             else copy_row<C1>(tb.tempB + (int64_t)(e.x + r) * C1, dst + (int64_t)(e.y + r) * C1, C1);
@@ -4473,13 +4478,15 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
             }
         }
         if (!p.join) return;
+        const uint32_t m = min(g.nR, p.ntab > 1 ? g.nS : 0u);
+        if (V0 >= m) return;
         __threadfence_block();  // the sorted rows written above, visible to the whole workgroup
         __syncthreads();
-        const uint32_t m = min(g.nR, p.ntab > 1 ? g.nS : 0u);
+        const uint32_t V1 = min(V0 + kSingleRunRows, m);
         const int c1 = C1 > 0 ? C1 : p.tab[0].cols, c2 = C2 > 0 ? C2 : p.tab[1].cols, tc = c1 + c2 - 1;
         const int64_t *oR = p.tab[0].out + (int64_t)g.outR * c1, *oS = p.tab[1].out + (int64_t)g.outS * c2;
         int64_t *dj = p.slots + (int64_t)g.outR * tc;
-        for (uint32_t v = tid; v < m; v += kMsdThreads)
+        for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads)
             emit_join_row<C1, C2>(oR + (int64_t)v * c1, oS + (int64_t)v * c2, dj + (int64_t)v * tc, c1, c2, p.key2);
         return;
     }
