@@ -856,7 +856,7 @@ constexpr int kHeavyThreads = 256;  // small: on unskewed tables every workgroup
 constexpr uint32_t kHeavySkew = 8;  // sampled keys repeated within the pass-A sample that open the gate
 constexpr int kHeavySlots = 2 * kHeavySamples;  // LDS hash table of the sampled keys (load <= 1/2)
 __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavyParams p) {
-    constexpr int NW = kHeavyThreads / 64, PER = kHeavySamples / kHeavyThreads, SPT = kHeavySlots / kHeavyThreads;
+    constexpr int PER = kHeavySamples / kHeavyThreads, SPT = kHeavySlots / kHeavyThreads;
     constexpr unsigned long long kEmpty = (unsigned long long)INT64_MAX;  // (an INT64_MAX key is never counted)
     __shared__ unsigned long long s_hk[kHeavySlots];
     __shared__ uint32_t s_hc[kHeavySlots];
@@ -1200,14 +1200,19 @@ __device__ __forceinline__ uint32_t pb_lin(const MsdBucket &b, uint64_t r) {
     return b.s32 ? __umulhi((uint32_t)r, b.s32)  // < D: r < 2^32 in such a bucket
                  : b.scale ? min((uint32_t)__umul64hi(r, b.scale), (uint32_t)(kRadB - 1)) : (uint32_t)r;
 }
-// heavy keys below `key` in the bucket's sorted list hv[0, m) (m <= kHeavyMax;
-// a fixed 7-step search), and whether key is one of them
+// heavy keys below `key` in the bucket's sorted list hv[0, m) (m <= kHeavyMax),
+// and whether key is one of them.  hv holds kHeavyMax entries, those past m
+// INT64_MAX, so the search is a fixed branch-free one: every row's steps are
+// plain LDS loads, and a thread's items search side by side (the guarded form,
+// `pos + st <= m && ...`, compiled to a branch per step and item, and the
+// items' dependent LDS loads ran one after the other: C5 part_b +12 %, r05m)
 __device__ __forceinline__ uint32_t heavy_rank(const int64_t *hv, uint32_t m, int64_t key, bool &eq) {
     uint32_t pos = 0;
 #pragma unroll
-    for (uint32_t st = kHeavyMax; st >= 1; st >>= 1)
-        if (pos + st <= m && hv[pos + st - 1] < key) pos += st;
-    eq = pos < m && hv[pos] == key;
+    for (uint32_t st = kHeavyMax / 2; st >= 1; st >>= 1) pos += hv[pos + st - 1] < key ? st : 0u;
+    const int64_t h = hv[pos];
+    pos += h < key ? 1u : 0u;  // pos == kHeavyMax - 1: all kHeavyMax below key
+    eq = h == key && pos < m;
     return pos;
 }
 // the digit with m heavy keys: lin + 2 c + e (order-preserving; heavy key j --
@@ -1313,8 +1318,8 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         const uint32_t q0 = ti.y;
         const int J = (int)runs_of(ti, b, g);
         for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
-        if (msd_heavy_count(b.one_key) && (uint32_t)tid < msd_heavy_count(b.one_key))  // read after two barriers
-            s_hv[tid] = p.heavy[(int64_t)ti.x * kHeavyMax + tid];
+        if (msd_heavy_count(b.one_key) && tid < kHeavyMax)  // read after two barriers; padded (heavy_rank)
+            s_hv[tid] = (uint32_t)tid < msd_heavy_count(b.one_key) ? p.heavy[(int64_t)ti.x * kHeavyMax + tid] : INT64_MAX;
         if (p.dbg & 32) goto lookups_done;
         if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
         for (int j = tid + NT; j < J; j += NT)  // > NT runs: rare
@@ -1641,7 +1646,8 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
         // stores, as the vmcnt wait of a vector load here would (every tile
         // of a heavy bucket then drained its stores: C5 part_b +1 ms, r05e)
         const uint32_t hm = msd_heavy_count(b.one_key);
-        if (hm) {
+        if (hm) {  // padded to kHeavyMax with INT64_MAX (heavy_rank)
+            static_assert(NW * 8 > kHeavyMax, "eight heavy keys per wave, the last wave free");
             const uint32_t w8 = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 8u;
             if (w8 < hm) {
                 SMJ_CONST(int64_t) *hq =
@@ -1652,6 +1658,15 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                 const int64_t v = l8 == 0 ? h0 : l8 == 1 ? h1 : l8 == 2 ? h2 : l8 == 3 ? h3 : l8 == 4 ? h4
                                                                                            : l8 == 5 ? h5 : l8 == 6 ? h6 : h7;
                 if (lane < 8 && w8 + (uint32_t)lane < hm) s_hv[w8 + lane] = v;
+            }
+            // the pads, by the last wave (it loads none: NW * 8 > kHeavyMax)
+            if (wave == NW - 1 && hm + (uint32_t)lane < (uint32_t)kHeavyMax) {
+                // INT64_MAX made here: left to the compiler, the constant was
+                // hoisted out of the loop, spilled, and reloaded here behind a
+                // vmcnt(0) that drained the tile's gathers and stores
+                uint32_t lo = ~0u, hi = 0x7fffffffu;
+                asm volatile("" : "+v"(lo), "+v"(hi));
+                reinterpret_cast<uint2 *>(s_hv)[hm + lane] = make_uint2(lo, hi);
             }
         }
         __syncthreads();
@@ -1666,10 +1681,16 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
             vmask |= v ? (1u << it) : 0u;
         }
         if (__builtin_expect(hm != 0u, 0)) {  // heavy keys in the bucket (C5): lin + 2 c + e
+            // (two items at a time, no branches: four side by side spilled at 64 VGPRs)
 #pragma unroll
-            for (int it = 0; it < ITEMS; it++)
-                if ((vmask >> it) & 1u)
-                    dig[it] = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
+            for (int i0 = 0; i0 < ITEMS; i0 += 2) {
+#pragma unroll
+                for (int it = i0; it < i0 + 2 && it < ITEMS; it++) {
+                    const uint32_t hd = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
+                    dig[it] = ((vmask >> it) & 1u) ? hd : dig[it];
+                }
+                asm volatile("" ::: "memory");
+            }
         }
         // a heavy key's own bucket (one key value): every row falls in
         // sub-bucket 0 and the tile's gather order is already its stable

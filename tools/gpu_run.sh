@@ -142,6 +142,11 @@ for s in $STEPS; do
     prof4) run prof4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o c4 -- \
                python3 "$ROOT/bench.py" --workload c4 --steps 2 --warmup 1 $NOCPU
            rm -f "$OUT/prof4/c4_kernel_trace.csv" ;;
+    prof5n|prof5n0)  # C5 kernel stats with the parts serialised (no overlap), heavy keys on / off
+           h=1; [ $s = prof5n0 ] && h=0
+           SMJ_HEAVY=$h SMJ_PART_OVERLAP=0 run $s 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$s" -o c5 -- \
+               python3 "$ROOT/bench.py" --workload c5 --steps 2 --warmup 1 $NOCPU
+           rm -f "$OUT/$s/c5_kernel_trace.csv" ;;
     proflp) run proflp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflp" -o loop -- \
                python3 "$ROOT/bench.py" --loopback --steps 5 --warmup 2 $NOCPU
            rm -f "$OUT/proflp/loop_kernel_trace.csv" ;;
