@@ -622,3 +622,41 @@ def test_heavy_keys_get_own_sub_buckets(gpu, oracle_built, monkeypatch, kc, sel,
     np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
     np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
+@pytest.mark.parametrize("kc", [0, 1])
+def test_heavy_keys_edge_cases(gpu, oracle_built, kc):
+    """Heavy-key sub-buckets at their limits, bit-exact against the oracle:
+    a bucket with more heavy candidates than kHeavyMax (the threshold rises,
+    the padded search sees a full list of 64), INT64_MIN and negative heavy
+    keys, a key with tens of thousands of rows in both tables (msd_single's
+    run mode in several 8k-row work items, with nR != nS), and a heavy key
+    right above a light one in the same linear sub-bucket."""
+    from smj import ops
+    rng = np.random.default_rng(101 + kc)
+    lo = -(1 << 40)
+    base = int(rng.integers(lo, -lo))
+    cluster = base + np.sort(rng.choice(6000, 150, replace=False))  # > kHeavyMax heavy keys in one bucket
+
+    def make(n, pay0, big):
+        keys = [rng.integers(lo, -lo, n), rng.integers(base, base + 6000, n // 50)]
+        for i, v in enumerate(cluster):
+            keys.append(np.full(300 + (i * 97) % 1700, v))
+        keys.append(np.full(3000, np.iinfo(np.int64).min))
+        keys.append(np.full(2500, -5))
+        keys.append(np.full(4, -6))  # a light key next to a heavy one
+        keys.append(np.full(big, base - 77))
+        k = rng.permutation(np.concatenate(keys))
+        t = np.empty((len(k), 2), dtype=np.int64)
+        t[:, kc] = k
+        t[:, 1 - kc] = pay0 + np.arange(len(k))
+        return t
+
+    R, S = make(2_000_000, 0, 50_000), make(1_500_000, 10 ** 9, 21_000)
+    for sel in (None, (kc, int(base + 3000))):
+        Rs, Ss, J = ref_pipeline(R, S, kc, kc, sel, sel)
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, sel)
+        np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+        np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+        np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    assert ops.msd_stats()[0] > 0  # single-key groups streamed

@@ -184,6 +184,7 @@ for s in $STEPS; do
            n=$(basename "$f" .py)_$(echo "$k" | tr -c 'a-zA-Z0-9' '_' | cut -c1-30)
            if [ -n "$k" ]; then test_run "$n" 1200 $PYT "$f" -m gpu -k "${k//+/ }"
            else test_run "$n" 1200 $PYT "$f" -m gpu; fi ;;
+    dbg3)  SMJ_DIST_TRACE=1 run dbg3 170 python -u bench.py --loopback --steps 3 --warmup 1 $NOCPU ;;
     dbg4)  SMJ_DIST_TRACE=1 SMJ_DEBUG_PART1=1 run dbg4 170 python -u bench.py --loopback --workload c4 --steps 1 --warmup 0 $NOCPU ;;
     dbg4s) SMJ_DIST_TRACE=2 SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run dbg4s 170 python -u bench.py --loopback --workload c4 --steps 2 --warmup 1 $NOCPU ;;
     dbg4h0) SMJ_HEAVY=0 SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run dbg4h0 170 python -u bench.py --loopback --workload c4 --steps 2 --warmup 1 $NOCPU ;;
