@@ -252,6 +252,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ms0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
@@ -260,6 +261,12 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ms1 = torch.cuda.memory_stats(dev)
+    # device allocations inside the timed steps (a cache miss of the torch
+    # allocator maps fresh memory -- tens of ms per large buffer): logged, so
+    # a slow run shows whether that is where its time went
+    progress("allocator in the timed steps: " + ", ".join(
+        f"{k} +{ms1.get(k, 0) - ms0.get(k, 0)}" for k in ("num_alloc_retries", "num_device_alloc", "num_device_free")))
     # the per-kernel breakdown (HIP events around every pipeline stage) from
     # separate steps after the timed ones: recording the events adds a little
     # host gap per stage, so they stay out of the timed steps

@@ -311,6 +311,23 @@ double smj_zipf_zeta(int64_t n, double theta);
 int smj_dev_digest(const int64_t *rows, int64_t n_rows, int col_num, int64_t pos0, uint64_t *d_digest,
                    void *stream);
 
+/* Splitters of the range-partitioned multi-GPU path (the
+ * reference deals rows to DPUs by count, app.c:155-218, and has no key
+ * ranges).  Two device steps around the caller's all_gather:
+ *   smj_dev_dist_sample: d_buf (DEVICE, 5 + 2 samples words) = the header
+ *     [c0 + c1, c0, c1, nR, nS], then the keys of rows j (n - 1) / (c - 1),
+ *     j < c = min(samples, n), of R then S, then INT64_MAX pads.
+ *   smj_dev_dist_splitters: d_all = world such buffers back to back (stride
+ *     words each); d_out (DEVICE, parts words) = the keys at sorted positions
+ *     max(0, (q + 1) L / parts - 1), or max(0, q20[q] L / 2^20 - 1) when q20
+ *     (HOST, parts - 1 fractions << 20) is given, q < parts - 1, then L (the
+ *     valid samples of all ranks; L = 0: every splitter 0).  parts <= 64.
+ * Async. */
+int smj_dev_dist_sample(const int64_t *R, int64_t nR, int colsR, int keyR, const int64_t *S, int64_t nS, int colsS,
+                        int keyS, int samples, int64_t *d_buf, void *stream);
+int smj_dev_dist_splitters(const int64_t *d_all, int world, int64_t stride, int parts, const int32_t *q20,
+                           int64_t *d_out, void *stream);
+
 /* ---- T = UINT64 / DOUBLE (common.h:3-9) ------------- */
 /* The fused pipeline with keys and select values compared as key_type
  * (uint64 or IEEE double, as cpu_app.c compiled with that T): tables are

@@ -2578,6 +2578,45 @@ extern "C" int smj_dev_digest(const T *rows, int64_t n_rows, int col_num, int64_
     return SMJ_OK;
 }
 
+extern "C" int smj_dev_dist_sample(const T *R, int64_t nR, int colsR, int keyR, const T *S, int64_t nS, int colsS,
+                                   int keyS, int samples, int64_t *d_buf, void *stream) {
+    if (nR < 0 || nS < 0 || (nR && !R) || (nS && !S) || !d_buf || samples < 1 || samples > (1 << 20) ||
+        colsR < 1 || colsS < 1 || keyR < 0 || keyR >= colsR || keyS < 0 || keyS >= colsS)
+        return SMJ_ERR_INVALID;
+    DistSampleArgs a{};
+    a.t[0] = R;
+    a.t[1] = S;
+    a.n[0] = nR;
+    a.n[1] = nS;
+    a.cols[0] = colsR;
+    a.cols[1] = colsS;
+    a.key[0] = keyR;
+    a.key[1] = keyS;
+    a.samples = samples;
+    a.buf = d_buf;
+    HIP_TRY(launch_dist_sample(a, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_dist_splitters(const int64_t *d_all, int world, int64_t stride, int parts, const int32_t *q20,
+                                      int64_t *d_out, void *stream) {
+    if (!d_all || !d_out || world < 1 || stride <= kDistHdr || parts < 1 || parts > kDistMaxParts)
+        return SMJ_ERR_INVALID;
+    DistSelectArgs a{};
+    a.all = d_all;
+    a.stride = stride;
+    a.world = world;
+    a.parts = parts;
+    a.use_q = q20 ? 1 : 0;
+    for (int i = 0; q20 && i < parts - 1; i++) {
+        if (q20[i] < 0 || q20[i] > (1 << 20)) return SMJ_ERR_INVALID;
+        a.q20[i] = q20[i];
+    }
+    a.out = d_out;
+    HIP_TRY(launch_dist_select(a, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
 // ---------------------------------------------------------------------------
 // release of every library-owned buffer (smj_finalize, smj_host.hip)
 // ---------------------------------------------------------------------------

@@ -143,6 +143,25 @@ hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t
                               uint64_t key_range, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
                            double theta, double zeta_n, hipStream_t s);
+// distributed splitters (smj_dev_dist_sample / smj_dev_dist_splitters)
+constexpr int kDistHdr = 5;         // [valid samples, samples of R, of S, rows of R, of S]
+constexpr int kDistMaxParts = 64;   // splitters + 1 (the partition kernels' <= 64 buckets)
+struct DistSampleArgs {
+    const int64_t *t[2];
+    int64_t n[2];
+    int cols[2], key[2];
+    int samples;
+    int64_t *buf;                   // kDistHdr + 2 samples words
+};
+struct DistSelectArgs {
+    const int64_t *all;             // world rows of `stride` words (gathered sample buffers)
+    int64_t stride;
+    int world, parts, use_q;
+    int32_t q20[kDistMaxParts];     // stage fractions << 20 (use_q)
+    int64_t *out;                   // parts words: parts - 1 splitters, then L
+};
+hipError_t launch_dist_sample(const DistSampleArgs &a, hipStream_t s);
+hipError_t launch_dist_select(const DistSelectArgs &a, hipStream_t s);
 // *out = sum over rows i of hash(pos0 + i, row i) mod 2^64 (smj_dev_digest)
 hipError_t launch_digest(const int64_t *rows, int64_t n, int cols, int64_t pos0, uint64_t *out, hipStream_t s);
 

@@ -1083,6 +1083,104 @@ hipError_t launch_digest(const int64_t *rows, int64_t n, int cols, int64_t pos0,
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// distributed splitters (smj/dist.py choose_splitters)
+// ---------------------------------------------------------------------------
+// Sample: thread j < 2 samples -> buf[kDistHdr + j]: the key of row
+// jj (n - 1) / (c - 1) of table x (c = min(samples, n) rows, exact int64: the
+// evenly spaced rows of dist.sample_index), R's c0 samples then S's c1, then
+// INT64_MAX pads; thread 0 writes the header [c0 + c1, c0, c1, nR, nS].
+__global__ __launch_bounds__(256) void dist_sample_kernel(const DistSampleArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= 2LL * a.samples) return;
+    const int64_t c0 = min((int64_t)a.samples, a.n[0]), c1 = min((int64_t)a.samples, a.n[1]);
+    if (j == 0) {
+        a.buf[0] = c0 + c1;
+        a.buf[1] = c0;
+        a.buf[2] = c1;
+        a.buf[3] = a.n[0];
+        a.buf[4] = a.n[1];
+    }
+    int64_t v = INT64_MAX;
+    if (j < c0 + c1) {
+        const int x = j < c0 ? 0 : 1;
+        const int64_t jj = x ? j - c0 : j, c = x ? c1 : c0, n = a.n[x];
+        const int64_t r = jj * (n - 1) / max(c - 1, (int64_t)1);
+        v = a.t[x][r * a.cols[x] + a.key[x]];
+    }
+    a.buf[kDistHdr + j] = v;
+}
+
+// Select: the gathered samples of every rank (world rows of `stride` words:
+// header + cap keys), L = the sum of the ranks' valid counts; splitter q =
+// the key at sorted position max(0, (q + 1) L / parts - 1), or max(0, q20[q]
+// L / 2^20 - 1) with stage fractions -- the value at a sorted position does
+// not depend on how ties break, so each key's rank under (key, index) (a
+// permutation), counted against all N = world cap keys, picks them: block b
+// ranks keys [32 b, 32 b + 32); lane & 31 picks the key, 2 wave + (lane >> 5)
+// one of 32 slices of every rank's row to count against.  out[parts - 1] = L
+// (L = 0: every splitter 0).  grid ceil(N / 32) x 1024.
+constexpr int kDsKeys = 32, kDsSlices = 32;
+__global__ __launch_bounds__(1024) void dist_select_kernel(const DistSelectArgs a) {
+    __shared__ uint32_t s_rank[kDsSlices][kDsKeys];
+    __shared__ int64_t s_pos[kDistMaxParts];
+    __shared__ int64_t s_L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t cap = a.stride - kDistHdr, N = (int64_t)a.world * cap;
+    if (tid == 0) {
+        int64_t L = 0;
+        for (int r = 0; r < a.world; r++) L += a.all[(int64_t)r * a.stride];
+        s_L = L;
+    }
+    __syncthreads();
+    const int64_t L = s_L;
+    if (tid < a.parts - 1) {
+        const int64_t q = a.use_q ? (int64_t)a.q20[tid] * L / (1 << 20) : (int64_t)(tid + 1) * L / a.parts;
+        s_pos[tid] = max(q - 1, (int64_t)0);
+    }
+    const int li = lane & 31, slice = 2 * w + (lane >> 5);
+    const int64_t i = (int64_t)blockIdx.x * kDsKeys + li;
+    const int64_t ir = i / max(cap, (int64_t)1), ij = i - ir * cap;
+    const int64_t my = i < N ? a.all[ir * a.stride + kDistHdr + ij] : INT64_MAX;
+    const int64_t j0 = slice * cap / kDsSlices, j1 = (slice + 1) * cap / kDsSlices;
+    uint32_t rk = 0;
+    for (int r = 0; r < a.world; r++) {
+        const int64_t *row = a.all + (int64_t)r * a.stride + kDistHdr;
+        const int64_t base = (int64_t)r * cap;
+#pragma unroll 8
+        for (int64_t j = j0; j < j1; j++) {
+            const int64_t o = row[j];
+            rk += (o < my || (o == my && base + j < i)) ? 1u : 0u;
+        }
+    }
+    s_rank[slice][li] = rk;
+    __syncthreads();
+    if (tid < kDsKeys && i < N && L > 0) {
+        uint32_t rank = 0;
+#pragma unroll
+        for (int q = 0; q < kDsSlices; q++) rank += s_rank[q][tid];
+        for (int q = 0; q < a.parts - 1; q++)
+            if (s_pos[q] == (int64_t)rank) a.out[q] = my;
+    }
+    if (blockIdx.x == 0) {
+        if (tid == 0) a.out[a.parts - 1] = L;
+        if (L == 0 && tid < a.parts - 1) a.out[tid] = 0;
+    }
+}
+
+hipError_t launch_dist_sample(const DistSampleArgs &a, hipStream_t s) {
+    const int n = 2 * a.samples;
+    hipLaunchKernelGGL(dist_sample_kernel, dim3((unsigned)blocks_for(n, 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dist_select(const DistSelectArgs &a, hipStream_t s) {
+    const int64_t N = (int64_t)a.world * (a.stride - kDistHdr);
+    hipLaunchKernelGGL(dist_select_kernel, dim3((unsigned)std::max<int64_t>(1, blocks_for(N, kDsKeys))), dim3(1024), 0, s,
+                       a);
+    return hipGetLastError();
+}
+
 // Ablation switches for profiling builds of the bench tools only (unset in
 // production): SMJ_DEBUG_PASS bit0 = no look-back, bit1 = no HBM stores,
 // bit2 = no LDS staging / scatter; SMJ_DEBUG_JOIN bit0 = no look-back.

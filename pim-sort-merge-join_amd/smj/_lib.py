@@ -67,6 +67,8 @@ SIGNATURES = {
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
     "smj_zipf_zeta": (_D, [_L, _D]),
     "smj_dev_digest": (_I, [_P, _L, _I, _L, _P, _P]),
+    "smj_dev_dist_sample": (_I, [_P, _L, _I, _I, _P, _L, _I, _I, _I, _P, _P]),
+    "smj_dev_dist_splitters": (_I, [_P, _I, _L, _I, _PI, _P, _P]),
     "smj_debug_msd_stats": (None, [_PL]),
     "smj_debug_msd_groups": (None, [_PL]),
     "smj_debug_msd_tiers": (None, [_PL]),

@@ -143,6 +143,8 @@ class HipOps:
     partition_apply = staticmethod(hip_ops.partition_apply)
     partition_regions = staticmethod(hip_ops.partition_regions)  # one read of the table (msd_part1_kernel)
     sort_merge_join_begin = staticmethod(hip_ops.sort_merge_join_begin)  # the pipeline enqueued; job.end(out) finishes it
+    dist_sample = staticmethod(hip_ops.dist_sample)        # the splitter sample (smj_dev_dist_sample)
+    dist_splitters = staticmethod(hip_ops.dist_splitters)  # the splitters from the gathered samples
     region_capacities = staticmethod(hip_ops.region_capacities)
     writes_into = True  # sort_merge_join(..., out=view) writes the joined rows there
 
@@ -191,8 +193,51 @@ def seg_fracs(world, K, frac=None):
     return [(d + cum[k]) / world for d in range(world) for k in range(K)][1:]
 
 
+_PINNED = {}  # (device, words) -> a pinned host buffer for _splitters_hip's one copy
+
+
+def _splitters_hip(ops, tables_and_keys, world, group, samples, parts, own, fracs, est):
+    """choose_splitters on the device, in four operations: the library's
+    sample kernel, one all_gather_into_tensor, the library's order-statistic
+    kernel, one device -> host copy (round 4's torch path took ~25 small
+    launches and host gaps, ~0.6 ms of the loopback step; profiles/r05/r05p).
+    Same samples, same positions, same splitters as the torch path."""
+    (R, kR), (S, kS) = tables_and_keys
+    H, stride = 5, 5 + 2 * samples
+    dev = R.device
+    buf = ops.dist_sample(R, S, kR, kS, samples)
+    allx = torch.empty(world * stride + parts, dtype=torch.int64, device=dev)
+    gathered = allx[:world * stride]
+    dist.all_gather_into_tensor(gathered, buf, group=group)
+    q20 = [int(round(f_ * (1 << 20))) for f_ in fracs] if fracs is not None else None
+    ops.dist_splitters(gathered, world, stride, parts, q20, out=allx[world * stride:])
+    key = (str(dev), allx.numel())
+    host = _PINNED.get(key)
+    if host is None:
+        if len(_PINNED) > 8:
+            _PINNED.clear()
+        host = _PINNED[key] = torch.empty(allx.numel(), dtype=torch.int64, pin_memory=True)
+    host.copy_(allx, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    got = host.numpy().copy()
+    me = dist.get_rank(group)
+    if own is not None:
+        o = me * stride + H
+        for x in range(2):
+            c = int(got[me * stride + 1 + x])
+            own.append(got[o: o + c])
+            o += c
+    if est is not None:
+        est["all"] = got[:world * stride].reshape(world, stride)
+        est["H"], est["nt"] = H, 2
+    spl = got[world * stride: world * stride + parts - 1]
+    if int(got[world * stride + parts - 1]) == 0:
+        return [0] * (parts - 1)
+    return [int(x) for x in spl]
+
+
 def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=None, own=None, fracs=None,
-                     est=None):
+                     est=None, ops=None):
     """parts - 1 (default W - 1) sorted key splitters, identical on every rank,
     as a host list: one all_gather of every rank's sample (a fixed-size buffer,
     padded with INT64_MAX, plus its valid count), the sort and the order
@@ -204,6 +249,9 @@ def choose_splitters(tables_and_keys, world, group=None, samples=4096, parts=Non
     parts = parts or world
     home = tables_and_keys[0][0].device
     dev = _wire_device(tables_and_keys[0][0], group)
+    if (ops is not None and hasattr(ops, "dist_splitters") and len(tables_and_keys) == 2 and dev.type == "cuda"
+            and all(t.is_cuda for t, _ in tables_and_keys) and parts <= MAX_BOUNDS + 1):
+        return _splitters_hip(ops, tables_and_keys, world, group, samples, parts, own, fracs, est)
     nt = len(tables_and_keys)
     cap = nt * samples
     H = 1 + 2 * nt  # header: [total samples, samples per table..., rows per table...]
@@ -606,7 +654,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
     fr = stage_fracs(world, K)
     fracs = seg_fracs(world, K, fr) if fr else None
     spl = choose_splitters([(R, k1), (S, k2)], world, group, samples, parts=nseg, own=own, fracs=fracs,
-                           est=est)  # host sync 1
+                           est=est, ops=ops)  # host sync 1
     tr("splitters")
     bounds, single = bucket_bounds(spl)
     nb = len(bounds) + 1

@@ -503,6 +503,52 @@ def gen_zipf(rows, row0=0, seed=3, domain=100_000_000, theta=0.9, device="cuda",
 MASK64 = (1 << 64) - 1
 
 
+DIST_HDR = 5  # smj.h smj_dev_dist_sample: [valid samples, samples of R, of S, rows of R, of S]
+
+
+def dist_sample(R, S, key_R, key_S, samples, out=None, stream=None):
+    """smj_dev_dist_sample: this rank's splitter sample of R and S (evenly
+    spaced rows, R's then S's keys after a 5-word header, INT64_MAX pads) in
+    a device int64 vector of 5 + 2 samples words.  Asynchronous."""
+    lib = _lib.load()
+    _table(R, "R")
+    _table(S, "S")
+    n = DIST_HDR + 2 * samples
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=R.device)
+    elif not (out.is_cuda and out.dtype == torch.int64 and out.is_contiguous() and out.numel() >= n):
+        raise ValueError(f"out must be a contiguous int64 CUDA tensor of >= {n} entries")
+    _lib.check(lib.smj_dev_dist_sample(_ptr(R), R.shape[0], R.shape[1], key_R, _ptr(S), S.shape[0], S.shape[1],
+                                       key_S, int(samples), ctypes.c_void_p(out.data_ptr()), _stream(stream)),
+               "smj_dev_dist_sample")
+    return out
+
+
+def dist_splitters(gathered, world, stride, parts, q20=None, out=None, stream=None):
+    """smj_dev_dist_splitters: from the world gathered sample buffers
+    (`gathered`, world * stride int64 words on the device), the parts - 1
+    splitters then L (the ranks' valid samples) into `out` (parts int64 words,
+    device).  q20: the cumulative stage fractions << 20 (host ints) or None
+    for equal parts.  Asynchronous."""
+    lib = _lib.load()
+    if not (gathered.is_cuda and gathered.dtype == torch.int64 and gathered.is_contiguous()
+            and gathered.numel() >= world * stride):
+        raise ValueError("gathered must be a contiguous int64 CUDA tensor of world * stride entries")
+    if out is None:
+        out = torch.empty(parts, dtype=torch.int64, device=gathered.device)
+    elif not (out.is_cuda and out.dtype == torch.int64 and out.is_contiguous() and out.numel() >= parts):
+        raise ValueError(f"out must be a contiguous int64 CUDA tensor of >= {parts} entries")
+    q = None
+    if q20 is not None:
+        if len(q20) != parts - 1:
+            raise ValueError("q20 needs parts - 1 entries")
+        q = (ctypes.c_int * max(1, len(q20)))(*[int(v) for v in q20])
+    _lib.check(lib.smj_dev_dist_splitters(ctypes.c_void_p(gathered.data_ptr()), int(world), int(stride), int(parts), q,
+                                          ctypes.c_void_p(out.data_ptr()), _stream(stream)),
+               "smj_dev_dist_splitters")
+    return out
+
+
 def digest_async(table, pos0=0, out=None, stream=None):
     """smj_dev_digest of `table` (rows at global positions pos0, pos0 + 1, ...)
     into out (a 1-element int64 CUDA tensor holding the uint64 bits;

@@ -331,3 +331,50 @@ def _run_and_check(tmp_path, world, kind, cfg, n):
     assert len(ref) > 0
     np.testing.assert_array_equal(got, ref)
     return float(np.load(tmp_path / "load.npy")[0])
+
+
+def _splitter_worker(rank, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "pim-sort-merge-join_amd"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    from smj import dist as sdist
+    from smj import ops
+    bad = []
+    rng = np.random.default_rng(5)
+    cases = [(1_000_000, 700_000, 2, 2, 0, 0, 4096, 2, None), (1_000_000, 700_000, 2, 2, 0, 0, 4096, 3,
+                                                               [0.05, 0.15]),
+             (5000, 3, 3, 2, 1, 0, 64, 7, None), (0, 90_000, 2, 4, 0, 3, 1024, 4, [0.1, 0.5, 0.9]),
+             (0, 0, 2, 2, 0, 0, 512, 3, None), (200_000, 200_000, 2, 2, 0, 0, 4096, 32, None)]
+    for nr, ns, cr, cs, kr, ks, samples, parts, fracs in cases:
+        R = torch.from_numpy(rng.integers(-50, 50, size=(nr, cr)).astype(np.int64)).cuda()
+        S = torch.from_numpy(rng.integers(-(1 << 62), 1 << 62, size=(ns, cs)).astype(np.int64)).cuda()
+        if ns:
+            S[: ns // 3, ks] = 7  # a heavy key: repeated splitters
+        res = []
+        for o in (sdist.HipOps, None):
+            own, est = [], {}
+            spl = sdist.choose_splitters([(R, kr), (S, ks)], 1, None, samples, parts=parts, own=own, fracs=fracs,
+                                         est=est, ops=o)
+            res.append((spl, [np.asarray(x).tolist() for x in own], np.asarray(est["all"]).tolist()))
+        if res[0] != res[1]:
+            bad.append((nr, ns, parts, fracs))
+    np.save(os.path.join(outdir, "bad.npy"), np.array([len(bad)]))
+    with open(os.path.join(outdir, "bad.txt"), "w") as f:
+        f.write(repr(bad))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_hip_splitters_equal_torch_path(tmp_path, pkg_built):
+    """smj_dev_dist_sample + smj_dev_dist_splitters (the RCCL path's splitter
+    choice: one sample kernel, one all_gather_into_tensor, one order-statistic
+    kernel, one host copy) give the torch path's splitters, own samples and
+    gathered estimate exactly: even and stage-fraction positions, a repeated
+    (heavy) key, empty tables, 3 / 4-column rows, up to 32 parts."""
+    mp.spawn(_splitter_worker, args=(free_port(), str(tmp_path)), nprocs=1, join=True)
+    assert int(np.load(tmp_path / "bad.npy")[0]) == 0, (tmp_path / "bad.txt").read_text()
