@@ -319,7 +319,7 @@ def estimate_counts(est, t, bounds):
         o = H + sum(c[:t])
         b = np.searchsorted(bnd, a[r, o: o + c[t]], side="left")
         tot += np.bincount(b, minlength=nb) * (n / c[t])
-    return [int(round(v)) for v in tot]
+    return np.rint(tot).astype(np.int64).tolist()  # (round half to even, as round())
 
 
 def bucket_bounds(spl):

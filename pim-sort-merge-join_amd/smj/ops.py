@@ -432,21 +432,15 @@ def region_capacities(sample_keys, n, bounds, tile=4096, sigmas=8.0):
     nb = len(bounds) + 1
     sample_keys = np.asarray(sample_keys, dtype=np.int64)
     m = len(sample_keys)
-    sc = np.bincount(np.searchsorted(np.asarray(bounds, dtype=np.int64), np.asarray(sample_keys, dtype=np.int64),
-                                     side="left"), minlength=nb).tolist() if m else [0] * nb
-    starts, caps, at = [], [], 0
-    for b in range(nb):
-        if m == 0:
-            cap = n
-        else:
-            f = sc[b] / m
-            est = n * f
-            sd = n / m * (m * f * (1.0 - f) + 1.0) ** 0.5
-            cap = min(n, int(est + sigmas * sd) + tile)
-        starts.append(at)
-        caps.append(cap)
-        at += cap
-    return starts + caps, at
+    if m == 0:
+        caps = np.full(nb, n, dtype=np.int64)
+    else:  # (vectorised: this runs between the splitters' host copy and the first partition launch)
+        f = np.bincount(np.searchsorted(np.asarray(bounds, dtype=np.int64), sample_keys, side="left"),
+                        minlength=nb) / m
+        sd = n / m * np.sqrt(m * f * (1.0 - f) + 1.0)
+        caps = np.minimum(n, (n * f + sigmas * sd).astype(np.int64) + tile)
+    ends = np.cumsum(caps)
+    return (ends - caps).tolist() + caps.tolist(), int(ends[-1])
 
 
 def partition_regions(table, bounds, region, counts, key_col=0, select_col=0, select_val=None, out=None,

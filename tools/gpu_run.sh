@@ -90,7 +90,7 @@ for s in $STEPS; do
              SMJ_BG_MAX_ROWS=32768 run c5bg32k_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5bg32k_$r.out" c5_bgmax32k
            done ;;
     loopk) for r in 1 2; do
-             for k in 2 3 4; do
+             for k in ${LOOPK:-2 3 4}; do
                SMJ_DIST_STAGES=$k run loopk${k}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/loopk${k}_$r.out" loop_k$k
              done
            done ;;
