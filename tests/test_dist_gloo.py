@@ -378,3 +378,44 @@ def test_hip_splitters_equal_torch_path(tmp_path, pkg_built):
     (heavy) key, empty tables, 3 / 4-column rows, up to 32 parts."""
     mp.spawn(_splitter_worker, args=(free_port(), str(tmp_path)), nprocs=1, join=True)
     assert int(np.load(tmp_path / "bad.npy")[0]) == 0, (tmp_path / "bad.txt").read_text()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_dist_splitters_kernel_many_ranks(pkg_built, world):
+    """smj_dev_dist_splitters on a gathered buffer of `world` ranks (as the
+    all_gather lays it out: per rank a 5-word header, R's then S's sampled
+    keys, INT64_MAX pads) against numpy: the keys at sorted positions
+    max(0, (q + 1) L / parts - 1) -- and at the stage-fraction positions --
+    with ranks of different valid counts, duplicates and INT64 extremes."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pim-sort-merge-join_amd"))
+    from smj import ops
+    rng = np.random.default_rng(world)
+    samples = 1024
+    H, stride = 5, 5 + 2 * samples
+    for trial in range(4):
+        allb = np.full((world, stride), np.iinfo(np.int64).max, dtype=np.int64)
+        for r in range(world):
+            c0, c1 = int(rng.integers(0, samples + 1)), int(rng.integers(0, samples + 1))
+            if trial == 3:
+                c0 = c1 = 0  # no samples anywhere: every splitter 0
+            allb[r, :H] = [c0 + c1, c0, c1, 10 * c0, 10 * c1]
+            keys = rng.integers(-1000, 1000, c0 + c1) * (1 << 50) if trial else rng.integers(-5, 5, c0 + c1)
+            if c0 + c1 > 2:
+                keys[0], keys[1] = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+            allb[r, H: H + c0 + c1] = keys
+        L = int(allb[:, 0].sum())
+        srt = np.sort(allb[:, H:].reshape(-1))
+        for parts, fr in ((world * 2, None), (min(32, world * 4), "q")):
+            q20 = None
+            if fr:
+                cum = np.sort(rng.random(parts - 1))
+                q20 = [int(round(f * (1 << 20))) for f in cum]
+                pos = [max(0, q * L // (1 << 20) - 1) for q in q20]
+            else:
+                pos = [max(0, i * L // parts - 1) for i in range(1, parts)]
+            ref = [0] * (parts - 1) if L == 0 else [int(srt[p]) for p in pos]
+            out = ops.dist_splitters(torch.from_numpy(allb.reshape(-1)).cuda(), world, stride, parts, q20)
+            got = out.cpu().numpy()
+            assert got[:parts - 1].tolist() == ref and int(got[parts - 1]) == L, (trial, parts, fr)
