@@ -205,7 +205,10 @@ __host__ __device__ constexpr int pb_threads(int cols) { return cols == 2 ? 1024
 // runs a final group gathers (127 splitters and an odd single-key bucket per
 // splitter -- the round-1 layout -- gave ~191 tiles of half the run length,
 // and buckets over the final stage's 256-tile list from ~1.3e8 rows on).
-constexpr int kBitsA = 8;                    // pass-A digit bits
+#ifndef SMJ_BITS_A
+#define SMJ_BITS_A 8
+#endif
+constexpr int kBitsA = SMJ_BITS_A;           // pass-A digit bits
 constexpr int kBucketsA = 1 << kBitsA;       // 256 pass-A buckets
 constexpr int kSplA = kBucketsA - 1;         // 255 pass-A splitters
 constexpr int kOffsA = kBucketsA;            // per-bucket arrays (segment partials, bucket records)

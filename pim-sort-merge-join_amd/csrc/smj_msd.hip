@@ -427,8 +427,8 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
-    static_assert(RADIX < NT && RADIX < kOffsARow, "one offsA entry per thread");
-    if (tid <= RADIX) p.offs[t * kOffsARow + tid] = s_bin[tid];  // s_bin[RADIX] = the tile's selected rows
+    static_assert(RADIX < kOffsARow, "the offsA row holds the starts and the count");
+    for (int i = tid; i <= RADIX; i += NT) p.offs[t * kOffsARow + i] = s_bin[i];  // s_bin[RADIX] = the tile's selected rows
     if (tid == 0) {
         p.tmm[2 * t] = mn;
         p.tmm[2 * t + 1] = mx;
@@ -1095,8 +1095,9 @@ __device__ __forceinline__ void runs_apply_body(const uint32_t *__restrict__ off
     // dealt round-robin over the 8 XCDs), one after another -- so the line
     // is fetched into one L2 once instead of into eight
     const uint32_t p = blockIdx.x + blockIdx.y * gridDim.x;
+    constexpr uint32_t G8 = kBucketsA / 32;  // groups of eight quads (one offsA line) per segment
     const uint32_t x = p & 7u, r = (p >> 3) & 7u, sj = (p >> 6) * 8u + x;
-    const uint32_t seg = sj >> 3, quad = (sj & 7u) * 8u + r;
+    const uint32_t seg = sj / G8, quad = (sj % G8) * 8u + r;
     const int a = (int)quad * 4 + (threadIdx.x >> 6);
     const int64_t Ls = (ntiles + kMsdSegs - 1) / kMsdSegs;
     const int64_t c0 = min((int64_t)seg * Ls, ntiles), c1 = min(c0 + Ls, ntiles);
@@ -4940,7 +4941,7 @@ hipError_t launch_msd_heavy(const MsdHeavyParams &p, hipStream_t s) {
 
 hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s) {
     static_assert(kBucketsA % 4 == 0, "four buckets (waves) per workgroup");
-    static_assert(kBucketsA / 4 == 64 && kMsdSegs % 8 == 0, "runs_apply_body's XCD-aware block order");
+    static_assert(kBucketsA % 32 == 0 && kMsdSegs % 8 == 0, "runs_apply_body's XCD-aware block order");
     const dim3 grid(kBucketsA / 4, kMsdSegs, a.ntab);
     hipLaunchKernelGGL(msd_runs_apply_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();
