@@ -317,7 +317,10 @@ struct MsdBucket {       // per pass-A bucket and table
 // <= kHeavyMax per bucket, each given a sub-bucket of its own by the pass-B
 // digit -- a single-key group, streamed in stable order by msd_single_kernel
 constexpr int kHeavyMax = 64;
-constexpr int kHeavySamples = 2048;   // sampled rows per bucket (both tables)
+#ifndef SMJ_HEAVY_SAMPLES
+#define SMJ_HEAVY_SAMPLES 1024  // (2048: msd_heavy 0.44 -> 0.28 ms per C5 step at 1024, C5 -0.2 ms; r05zc)
+#endif
+constexpr int kHeavySamples = SMJ_HEAVY_SAMPLES;  // sampled rows per bucket (both tables)
 constexpr uint32_t kHeavyRows = 768;  // a key is heavy from ~this many rows (sample hits scaled)
 __host__ __device__ inline uint32_t msd_heavy_count(uint32_t one_key_word) { return (one_key_word >> 8) & 0xffu; }
 struct MsdHeavyParams {
