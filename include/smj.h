@@ -328,6 +328,31 @@ int smj_dev_dist_sample(const int64_t *R, int64_t nR, int colsR, int keyR, const
 int smj_dev_dist_splitters(const int64_t *d_all, int world, int64_t stride, int parts, const int32_t *q20,
                            int64_t *d_out, void *stream);
 
+/* Packed exchange rows (frame-of-reference packing of the
+ * range-partitioned rows before they cross xGMI): a 2-column row
+ * (key in column key_col, the other column o) travels as ONE int64 word
+ *   w = (uint32)(key - key_base) | (uint64)(uint32)(o - other_base) << 32,
+ * differences taken mod 2^64; it round-trips iff both differences fit int32.
+ *   smj_dev_partition_regions_pk: smj_dev_partition_regions of a 2-column
+ *     table writing packed words (out: one int64 per row of every region);
+ *     d_counts[n_split + 1] gets bit 2 (4) when some row did not fit -- the
+ *     caller then re-partitions unpacked (the output is not usable).
+ *   smj_dev_unpack_rows: n packed words -> n x 2 rows.
+ *   smj_dev_sort_merge_join_begin_pk: smj_dev_sort_merge_join_begin on two
+ *     2-column tables without a select, either of them packed (pkX = 1; rows
+ *     of <= 1.6e8 per table, else SMJ_ERR_UNSUPPORTED: unpack first); ended by
+ *     smj_dev_sort_merge_join_end.
+ * Async. */
+int smj_dev_partition_regions_pk(const int64_t *in, int64_t n, int use_select, int select_col, int64_t select_val,
+                                 int key_col, const int64_t *h_splitters, int n_split, const int64_t *h_region,
+                                 int64_t *out, int64_t *d_counts, int64_t key_base, int64_t other_base, void *stream);
+int smj_dev_unpack_rows(const int64_t *d_packed, int64_t n, int key_col, int64_t key_base, int64_t other_base,
+                        int64_t *d_out, void *stream);
+int smj_dev_sort_merge_join_begin_pk(const int64_t *R, int64_t nR, int key1, int pk1, int64_t key_base1,
+                                     int64_t other_base1, const int64_t *S, int64_t nS, int key2, int pk2,
+                                     int64_t key_base2, int64_t other_base2, int64_t *R_sorted, int64_t *S_sorted,
+                                     void *stream, void **job);
+
 /* ---- T = UINT64 / DOUBLE (common.h:3-9) ------------- */
 /* The fused pipeline with keys and select values compared as key_type
  * (uint64 or IEEE double, as cpu_app.c compiled with that T): tables are

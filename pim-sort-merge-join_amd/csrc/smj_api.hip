@@ -635,6 +635,8 @@ struct MsdIn {            // one input table of the pipeline
     T *out;               // sorted selected rows
     const uint64_t *desc = nullptr;  // a chunked part (msd_part1c): its pass-A tiles' rows in src (MsdPartAParams::desc)
     int64_t ntiles = 0;
+    int pk = 0;                      // packed input (MsdTable::pk): one word per row, cols == 2, no select
+    int64_t pkk = 0, pkp = 0;
 };
 
 // Records the index of the last profiling record (to patch its byte count
@@ -946,6 +948,8 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
     for (int x = 0; x < ntab; x++)  // internal callers too: a bad column index would fault on the device
         SMJ_TRY(check_table(in[x].n, in[x].cols, in[x].use_sel ? in[x].sel_col : 0, in[x].key));
     if (join && (ntab != 2 || key2 != in[1].key)) return SMJ_ERR_INVALID;
+    for (int x = 0; x < ntab; x++)  // packed input: two columns, no select, contiguous (read by the sampler and part_a)
+        if (in[x].pk && (in[x].cols != 2 || in[x].use_sel || in[x].desc || stg)) return SMJ_ERR_INVALID;
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
     int T_[2] = {1, 1}, TB_[2] = {1, 1};  // pass-A / pass-B tile rows
@@ -980,8 +984,13 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
     {
         MsdSampleParams sp{};
         for (int x = 0; x < ntab; x++)
+        {
             sp.tab[x] = MsdTable{in[x].src, in[x].n, in[x].cols, in[x].key, in[x].use_sel, in[x].sel_col, in[x].sel_val,
                                  in[x].desc, in[x].ntiles, T_[x]};
+            sp.tab[x].pk = in[x].pk;
+            sp.tab[x].pkk = in[x].pkk;
+            sp.tab[x].pkp = in[x].pkp;
+        }
         sp.ntab = ntab;
         sp.spl = ms->spl;
         sp.samp = ms->samp;
@@ -1005,10 +1014,14 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         }
     } ev_release{chunk_ev};
     MsdPartAParams pp[2];
-    for (int x = 0; x < ntab; x++)
+    for (int x = 0; x < ntab; x++) {
         pp[x] = MsdPartAParams{in[x].src, in[x].n, in[x].use_sel, in[x].sel_col, in[x].key, 0, in[x].sel_val, ms->spl,
                                (int64_t *)ms->t[x].tempA, (uint32_t *)ms->t[x].offsA, (int64_t *)ms->t[x].tmm,
                                in[x].desc, in[x].ntiles};
+        pp[x].pk = in[x].pk;
+        pp[x].pkk = in[x].pkk;
+        pp[x].pkp = in[x].pkp;
+    }
     if (stg && (in[0].desc || (ntab > 1 && in[1].desc))) return SMJ_ERR_INVALID;  // (staged input is contiguous)
     // both tables in one launch when nothing is staged and the widths agree (no tail between them)
     const bool pa_fused = !stg && ntab == 2 && in[0].cols == in[1].cols;
@@ -2119,6 +2132,46 @@ extern "C" int smj_dev_sort_merge_join_begin(const T *R, int64_t nr, int c1, int
     return SMJ_OK;
 }
 
+// smj_dev_sort_merge_join_begin for 2-column tables of which either may be
+// packed (pkX: one word per row, smj_dev_partition_regions_pk's format with
+// bases kbX / obX), no select -- the multi-GPU driver's received stages.
+// Packed tables over kMsdSingleMax rows are SMJ_ERR_UNSUPPORTED (the caller
+// unpacks them first: smj_dev_unpack_rows).
+extern "C" int smj_dev_sort_merge_join_begin_pk(const int64_t *R, int64_t nr, int key1, int pk1, int64_t kb1, int64_t ob1,
+                                                const int64_t *S, int64_t ns, int key2, int pk2, int64_t kb2,
+                                                int64_t ob2, T *R_sorted, T *S_sorted, void *stream, void **job) {
+    if (!job) return SMJ_ERR_INVALID;
+    *job = nullptr;
+    if (!pk1 && !pk2)
+        return smj_dev_sort_merge_join_begin(R, nr, 2, 0, 0, 0, key1, S, ns, 2, 0, 0, 0, key2, R_sorted, S_sorted, stream,
+                                             job);
+    if (t_job) return SMJ_ERR_INVALID;
+    SMJ_TRY(msd_check(R, nr, 2, 0, 0, key1, R_sorted));
+    SMJ_TRY(msd_check(S, ns, 2, 0, 0, key2, S_sorted));
+    if (nr == 0 || ns == 0 || nr > kMsdSingleMax || ns > kMsdSingleMax || g_force_parts > 0)
+        return SMJ_ERR_UNSUPPORTED;
+    SmjJob *j = new (std::nothrow) SmjJob;
+    if (!j) return SMJ_ERR_NOMEM;
+    *j = SmjJob{};
+    j->s = (hipStream_t)stream;
+    j->R = R, j->S = S, j->nr = nr, j->ns = ns, j->c1 = 2, j->c2 = 2, j->key1 = key1, j->key2 = key2;
+    j->R_sorted = R_sorted, j->S_sorted = S_sorted;
+    j->whole = false;
+    j->in[0] = MsdIn{R, nr, 2, 0, 0, key1, 0, R_sorted};
+    j->in[1] = MsdIn{S, ns, 2, 0, 0, key2, 0, S_sorted};
+    j->in[0].pk = pk1, j->in[0].pkk = kb1, j->in[0].pkp = ob1;
+    j->in[1].pk = pk2, j->in[1].pkk = kb2, j->in[1].pkp = ob2;
+    const int rc = msd_front(j->in, 2, 1, key2, j->s, nullptr, &j->cx);
+    if (rc != SMJ_OK) {
+        delete j;
+        return rc;
+    }
+    t_job = j;
+    t_job_open = true;
+    *job = j;
+    return SMJ_OK;
+}
+
 extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
     SmjJob *j = (SmjJob *)job;
     if (!j || j != t_job || !h_rows) return SMJ_ERR_INVALID;
@@ -2465,9 +2518,27 @@ extern "C" int smj_dev_partition_plan(const T *in, int64_t n, int cols, int use_
     return SMJ_OK;
 }
 
+static int partition_regions_impl(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val, int key_col,
+                                  const T *h_spl, int n_split, const int64_t *h_region, T *out, int64_t *d_counts,
+                                  int pk, int64_t pkk, int64_t pkp, void *stream);
+
 extern "C" int smj_dev_partition_regions(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val,
                                          int key_col, const T *h_spl, int n_split, const int64_t *h_region, T *out,
                                          int64_t *d_counts, void *stream) {
+    return partition_regions_impl(in, n, cols, use_select, sel_col, sel_val, key_col, h_spl, n_split, h_region, out,
+                                  d_counts, 0, 0, 0, stream);
+}
+
+extern "C" int smj_dev_partition_regions_pk(const T *in, int64_t n, int use_select, int sel_col, T sel_val, int key_col,
+                                            const T *h_spl, int n_split, const int64_t *h_region, int64_t *out,
+                                            int64_t *d_counts, int64_t key_base, int64_t other_base, void *stream) {
+    return partition_regions_impl(in, n, 2, use_select, sel_col, sel_val, key_col, h_spl, n_split, h_region, out,
+                                  d_counts, 1, key_base, other_base, stream);
+}
+
+static int partition_regions_impl(const T *in, int64_t n, int cols, int use_select, int sel_col, T sel_val, int key_col,
+                                  const T *h_spl, int n_split, const int64_t *h_region, T *out, int64_t *d_counts,
+                                  int pk, int64_t pkk, int64_t pkp, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     PassSpec ps;
     SMJ_TRY(partition_spec(in, n, cols, use_select, sel_col, sel_val, key_col, h_spl, n_split, ps));
@@ -2512,8 +2583,11 @@ extern "C" int smj_dev_partition_regions(const T *in, int64_t n, int cols, int u
     p.tot = (long long *)d_counts;
     p.flags = flags;
     p.ntiles = nt;
+    p.pk = pk;
+    p.pkk = pkk;
+    p.pkp = pkp;
     {
-        ProfScope ps1("partition_1pass", 16.0 * cols * n, s);
+        ProfScope ps1("partition_1pass", (pk ? 8.0 + 8.0 * cols : 16.0 * cols) * n, s);
         HIP_TRY(launch_msd_part1(p, cols, s));
     }
     HIP_TRY(launch_p1_finish(flags, d_counts + nb, s));
@@ -2614,6 +2688,13 @@ extern "C" int smj_dev_dist_splitters(const int64_t *d_all, int world, int64_t s
     }
     a.out = d_out;
     HIP_TRY(launch_dist_select(a, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
+extern "C" int smj_dev_unpack_rows(const int64_t *d_packed, int64_t n, int key_col, int64_t key_base,
+                                   int64_t other_base, int64_t *d_out, void *stream) {
+    if (n < 0 || (n && (!d_packed || !d_out)) || key_col < 0 || key_col > 1) return SMJ_ERR_INVALID;
+    HIP_TRY(launch_unpack_rows(d_packed, n, key_col, key_base, other_base, d_out, (hipStream_t)stream));
     return SMJ_OK;
 }
 

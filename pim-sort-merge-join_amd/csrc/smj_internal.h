@@ -268,6 +268,10 @@ struct MsdTable {        // an input table as the sampler and part_a see it
     const uint64_t *desc = nullptr;  // a chunked part's tile descriptors (MsdPartAParams::desc), ntiles of tile rows
     int64_t ntiles = 0;
     int tile = 0;
+    // packed input (2-column tables, no select; smj_dev_sort_merge_join_begin_pk):
+    // row i is the one word src[i] = (int32 key - pkk) | (int32 other - pkp) << 32
+    int pk = 0;
+    int64_t pkk = 0, pkp = 0;
 };
 struct MsdSampleParams {
     MsdTable tab[2];
@@ -290,6 +294,8 @@ struct MsdPartAParams {
     // order; ntiles tiles.  nullptr: tile t = rows [t T, t T + T) of src
     const uint64_t *desc = nullptr;
     int64_t ntiles = 0;
+    int pk = 0;                  // packed input (MsdTable::pk)
+    int64_t pkk = 0, pkp = 0;
 };
 struct MsdPartA2 {       // one part_a launch over up to two tables
     MsdPartAParams t[2];
@@ -471,9 +477,17 @@ struct MsdPart1Params {
     int64_t *dst;                // staging buffer of the regions
     unsigned long long *status;  // [ntiles][nspl + 1] look-back words, zeroed
     long long *tot;              // [nspl + 1]: rows per part (written by the last tile)
-    uint32_t *flags;             // [0] tile ticket, [1] a region overflowed, [2] look-back timeout; zeroed
+    uint32_t *flags;             // [0] tile ticket, [1] a region overflowed, [2] look-back timeout,
+                                 // [3] a packed row did not fit (pk); zeroed
     int64_t ntiles;
+    // packed output (2-column tables; smj_dev_partition_regions_pk): row = one
+    // word (int32 key - pkk) | (int32 other - pkp) << 32, differences taken
+    // mod 2^64 -- a row whose differences do not fit int32 sets flags[3]
+    int pk = 0;
+    int64_t pkk = 0, pkp = 0;
 };
+hipError_t launch_unpack_rows(const int64_t *packed, int64_t n, int key_col, int64_t pkk, int64_t pkp, int64_t *out,
+                              hipStream_t s);
 hipError_t launch_msd_part1(const MsdPart1Params &p, int cols, hipStream_t s);
 // The chunked one-pass partition (msd_part1c_kernel): no look-back.  A
 // persistent grid of G workgroups; workgroup g takes the consecutive tiles

@@ -225,6 +225,21 @@ __device__ __forceinline__ uint32_t tile_digit_starts(uint32_t *s_wcnt, uint32_t
 // wave-uniform copy (SGPR) of a value loaded through a vector load
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
+// packed rows (MsdTable::pk, MsdPart1Params::pk): word = (int32 key - base_k)
+// | (int32 other - base_p) << 32, differences mod 2^64
+__device__ __forceinline__ int64_t pk_key(int64_t w, int64_t bk) {
+    return (int64_t)((uint64_t)bk + (uint64_t)(int64_t)(int32_t)(uint32_t)w);
+}
+__device__ __forceinline__ int64_t pk_other(int64_t w, int64_t bp) {
+    return (int64_t)((uint64_t)bp + (uint64_t)(int64_t)(int32_t)(uint32_t)((uint64_t)w >> 32));
+}
+// the packed word of (key, other), and whether both differences fit int32
+__device__ __forceinline__ int64_t pk_pack(int64_t key, int64_t other, int64_t bk, int64_t bp, bool &fits) {
+    const int64_t dk = (int64_t)((uint64_t)key - (uint64_t)bk), dp = (int64_t)((uint64_t)other - (uint64_t)bp);
+    fits = dk == (int64_t)(int32_t)dk && dp == (int64_t)(int32_t)dp;
+    return (int64_t)(((uint64_t)(uint32_t)dk) | ((uint64_t)(uint32_t)dp << 32));
+}
+
 // pass-A bucket of a key: pos = #{splitters < key}, or pos + 1 when the key
 // equals spl[pos] == spl[pos + 1] (a repeated splitter: a heavy key gets
 // bucket pos + 1 to itself; no other key maps there)
@@ -272,8 +287,15 @@ __global__ __launch_bounds__(256) void msd_sample_gather_kernel(const MsdSampleP
             dup = r % t.tile >= rows && jj % kSampleRun != 0;
             r = (int64_t)(d >> 16) + min(r % t.tile, rows - 1);
         }
-        const int64_t *row = t.src + r * t.cols;
-        const int64_t sv = row[t.use_sel ? t.sel_col : t.key_col], kv = row[t.key_col];
+        int64_t sv, kv;
+        if (t.pk) {  // packed input (no select)
+            kv = pk_key(t.src[r], t.pkk);
+            sv = kv;
+        } else {
+            const int64_t *row = t.src + r * t.cols;
+            sv = row[t.use_sel ? t.sel_col : t.key_col];
+            kv = row[t.key_col];
+        }
         if (!dup && (!t.use_sel || sv > t.sel_val)) {
             k = kv;
             valid = 1;
@@ -395,10 +417,22 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
     zero_counters<RADIX>(wc, lane);
     const int lrow0 = wave * ITEMS * 64 + lane;
     int64_t rows[ITEMS][COLS];
+    bool packed = false;
+    if constexpr (COLS == 2) packed = p.pk != 0;  // block-uniform
+    if (packed) {  // one word per row (MsdPartAParams::pk): both columns rebuilt here
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++)
-        if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
-        else load_row<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+        for (int it = 0; it < ITEMS; it++) {
+            const int64_t w = p.src[rs + min(lrow0 + it * 64, nrows - 1)];
+            const int64_t k = pk_key(w, p.pkk), o = pk_other(w, p.pkp);
+            rows[it][0] = p.key_col ? o : k;
+            rows[it][COLS - 1] = p.key_col ? k : o;
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++)
+            if (SMJ_PA_NTLOAD) load_row_nt<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+            else load_row<COLS>(p.src + (rs + min(lrow0 + it * 64, nrows - 1)) * COLS, rows[it]);
+    }
     __syncthreads();  // splitters
 
     uint32_t dig[ITEMS];
@@ -602,10 +636,40 @@ __global__ __launch_bounds__(kMsdThreads, p1_waves_per_eu(COLS)) void msd_part1_
             if (s_ok[b]) {
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)slot * COLS, r);
-                store_row<COLS>(p.dst + (s_gb[b] + (int64_t)slot) * COLS, r);
+                bool pk = false;
+                if constexpr (COLS == 2) pk = p.pk != 0;  // block-uniform
+                if (pk) {  // one word per row (MsdPart1Params::pk)
+                    bool fits;
+                    const int64_t w = pk_pack(p.key_col ? r[COLS - 1] : r[0], p.key_col ? r[0] : r[COLS - 1], p.pkk,
+                                              p.pkp, fits);
+                    if (!fits) atomicOr(&p.flags[3], 1u);
+                    p.dst[s_gb[b] + (int64_t)slot] = w;
+                } else {
+                    store_row<COLS>(p.dst + (s_gb[b] + (int64_t)slot) * COLS, r);
+                }
             }
         }
     }
+}
+
+// packed rows -> 2-column rows (smj_dev_unpack_rows): one row per thread, 16-B stores
+__global__ __launch_bounds__(256) void unpack_rows_kernel(const int64_t *__restrict__ in, int64_t n, int key_col,
+                                                          int64_t pkk, int64_t pkp, int64_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t w = in[i], k = pk_key(w, pkk), o = pk_other(w, pkp);
+        i64x2 r;
+        r.x = key_col ? o : k;
+        r.y = key_col ? k : o;
+        reinterpret_cast<i64x2 *>(out)[i] = r;
+    }
+}
+
+hipError_t launch_unpack_rows(const int64_t *packed, int64_t n, int key_col, int64_t pkk, int64_t pkp, int64_t *out,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+    hipLaunchKernelGGL(unpack_rows_kernel, dim3(grid), dim3(256), 0, s, packed, n, key_col, pkk, pkp, out);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -4827,9 +4891,10 @@ __global__ void p1_set_words_kernel(const P1Words w, int64_t *oc, uint32_t *flag
     if (t < 4) flags[t] = 0u;
 }
 
-// after the partition: out = overflow (bit 0) | look-back timeout (bit 1)
+// after the partition: out = overflow (bit 0) | look-back timeout (bit 1) |
+// a packed row did not fit (bit 2)
 __global__ void p1_finish_kernel(const uint32_t *flags, int64_t *out) {
-    if (threadIdx.x == 0) *out = (flags[1] ? 1 : 0) | (flags[2] ? 2 : 0);
+    if (threadIdx.x == 0) *out = (flags[1] ? 1 : 0) | (flags[2] ? 2 : 0) | (flags[3] ? 4 : 0);
 }
 
 hipError_t launch_p1_words(const P1Words &w, int64_t *oc, uint32_t *flags, hipStream_t s) {

@@ -69,6 +69,10 @@ SIGNATURES = {
     "smj_dev_digest": (_I, [_P, _L, _I, _L, _P, _P]),
     "smj_dev_dist_sample": (_I, [_P, _L, _I, _I, _P, _L, _I, _I, _I, _P, _P]),
     "smj_dev_dist_splitters": (_I, [_P, _I, _L, _I, _PI, _P, _P]),
+    "smj_dev_partition_regions_pk": (_I, [_P, _L, _I, _I, _L, _I, _P, _I, _P, _P, _P, _L, _L, _P]),
+    "smj_dev_unpack_rows": (_I, [_P, _L, _I, _L, _L, _P, _P]),
+    "smj_dev_sort_merge_join_begin_pk": (_I, [_P, _L, _I, _I, _L, _L, _P, _L, _I, _I, _L, _L, _P, _P, _P,
+                                              ctypes.POINTER(ctypes.c_void_p)]),
     "smj_debug_msd_stats": (None, [_PL]),
     "smj_debug_msd_groups": (None, [_PL]),
     "smj_debug_msd_tiers": (None, [_PL]),

@@ -130,10 +130,12 @@ class SortMergeJoinJob:
     sort_merge_join returns.  Until end() the thread must not start another
     pipeline call; the tables and the job must stay alive."""
 
-    def __init__(self, lib, handle, R, S, R_sorted, S_sorted, stream):
+    def __init__(self, lib, handle, R, S, R_sorted, S_sorted, stream, shapes=None):
         self._lib, self._h = lib, handle
         self._keep = (R, S)
         self.R_sorted, self.S_sorted, self._stream = R_sorted, S_sorted, stream
+        # (rows, columns) of R and S as tables (packed inputs hold one word per row)
+        self._shapes = shapes or (tuple(R.shape), tuple(S.shape))
 
     def end(self, out=None):
         """Finish the job.  The C job is released whatever happens here: an
@@ -142,8 +144,7 @@ class SortMergeJoinJob:
         if self._h is None:
             raise RuntimeError("job already ended")
         R, S = self._keep
-        nr, c1 = R.shape
-        ns, c2 = S.shape
+        (nr, c1), (ns, c2) = self._shapes
         h, self._h = self._h, None
         rows = (ctypes.c_int64 * 3)()
         try:
@@ -204,6 +205,56 @@ def sort_merge_join_begin(R, S, key1=0, key2=0, select1=None, select2=None, R_so
                                                  _ptr(R_sorted), _ptr(S_sorted), _stream(stream), ctypes.byref(h)),
                "smj_dev_sort_merge_join_begin")
     return SortMergeJoinJob(lib, h, R, S, R_sorted, S_sorted, stream)
+
+
+def _packed_rows(t, name):
+    if not (t.is_cuda and t.dtype == torch.int64 and t.is_contiguous() and (t.dim() == 1 or (t.dim() == 2 and
+                                                                                            t.shape[1] == 1))):
+        raise ValueError(f"{name} must be a contiguous int64 CUDA tensor of packed rows (n or n x 1)")
+    return t.shape[0]
+
+
+def sort_merge_join_begin_pk(R, S, key1=0, key2=0, pack1=None, pack2=None, R_sorted=None, S_sorted=None,
+                             stream=None):
+    """sort_merge_join_begin of two 2-column tables without a select, either
+    of which may be packed (smj_dev_sort_merge_join_begin_pk): packX = None
+    for an n x 2 table, or (key_base, other_base) for n packed words
+    (partition_regions(..., pack=...)).  Packed tables over 1.6e8 rows raise
+    (unpack_rows them first).  job.end(out) finishes it."""
+    lib = _lib.load()
+    shp = []
+    for t, pk, name in ((R, pack1, "R"), (S, pack2, "S")):
+        if pk is None:
+            _table(t, name)
+            if t.shape[1] != 2:
+                raise ValueError(f"{name} must have 2 columns")
+            shp.append((t.shape[0], 2))
+        else:
+            shp.append((_packed_rows(t, name), 2))
+    (nr, _), (ns, _) = shp
+    R_sorted = torch.empty((nr, 2), dtype=torch.int64, device=R.device) if R_sorted is None else \
+        _out(R_sorted, "R_sorted", nr, 2, R)
+    S_sorted = torch.empty((ns, 2), dtype=torch.int64, device=R.device) if S_sorted is None else \
+        _out(S_sorted, "S_sorted", ns, 2, R)
+    p1, p2 = pack1 or (0, 0), pack2 or (0, 0)
+    h = ctypes.c_void_p()
+    _lib.check(lib.smj_dev_sort_merge_join_begin_pk(_ptr(R), nr, key1, int(pack1 is not None), int(p1[0]), int(p1[1]),
+                                                    _ptr(S), ns, key2, int(pack2 is not None), int(p2[0]), int(p2[1]),
+                                                    _ptr(R_sorted), _ptr(S_sorted), _stream(stream), ctypes.byref(h)),
+               "smj_dev_sort_merge_join_begin_pk")
+    return SortMergeJoinJob(lib, h, R, S, R_sorted, S_sorted, stream, shapes=tuple(shp))
+
+
+def unpack_rows(packed, key_col, pack, out=None, stream=None):
+    """smj_dev_unpack_rows: n packed words -> an n x 2 table (the key in
+    column key_col).  pack = (key_base, other_base).  Asynchronous."""
+    lib = _lib.load()
+    n = _packed_rows(packed, "packed")
+    out = torch.empty((n, 2), dtype=torch.int64, device=packed.device) if out is None else \
+        _out(out, "out", n, 2, packed)
+    _lib.check(lib.smj_dev_unpack_rows(_ptr(packed), n, int(key_col), int(pack[0]), int(pack[1]), _ptr(out),
+                                       _stream(stream)), "smj_dev_unpack_rows")
+    return out
 
 
 def _sort_merge_join_typed(lib, R, S, key1, key2, select1, select2, R_sorted, S_sorted, out, stream, key_type):
@@ -444,11 +495,13 @@ def region_capacities(sample_keys, n, bounds, tile=4096, sigmas=8.0):
 
 
 def partition_regions(table, bounds, region, counts, key_col=0, select_col=0, select_val=None, out=None,
-                      stream=None):
+                      stream=None, pack=None):
     """One-read stable partition (smj_dev_partition_regions): bucket b's rows
     at out[region[b]: region[b] + count_b]; `counts` (a 1-D int64 CUDA tensor of
     len(bounds) + 2 entries) gets the exact counts and, last, the overflow /
-    timeout flag word.  Asynchronous.  Returns out."""
+    timeout flag word.  pack = (key_base, other_base) for a 2-column table:
+    out holds one packed word per row (smj_dev_partition_regions_pk; flag bit
+    2 = a row did not fit, out unusable).  Asynchronous.  Returns out."""
     lib = _lib.load()
     _table(table, "table")
     n, cols = table.shape
@@ -458,11 +511,20 @@ def partition_regions(table, bounds, region, counts, key_col=0, select_col=0, se
     need = max(region[b] + region[nb + b] for b in range(nb)) if n else 0
     if not (counts.is_cuda and counts.dtype == torch.int64 and counts.is_contiguous() and counts.numel() == nb + 1):
         raise ValueError("counts must be a contiguous int64 CUDA tensor of len(bounds) + 2 entries")
-    out = torch.empty((max(need, 1), cols), dtype=torch.int64, device=table.device) if out is None else \
-        _out(out, "out", need, cols, table)
+    if pack is not None and cols != 2:
+        raise ValueError("packed partitions take 2-column tables")
+    oc = 1 if pack is not None else cols
+    out = torch.empty((max(need, 1), oc), dtype=torch.int64, device=table.device) if out is None else \
+        _out(out, "out", need, oc, table)
     spl, ns = _host_splitters(bounds)
     reg = (ctypes.c_int64 * len(region))(*[int(v) for v in region])
     use = select_val is not None
+    if pack is not None:
+        _lib.check(lib.smj_dev_partition_regions_pk(_ptr(table), n, int(use), select_col, int(select_val) if use else 0,
+                                                    key_col, spl, ns, reg, _ptr(out), ctypes.c_void_p(counts.data_ptr()),
+                                                    int(pack[0]), int(pack[1]), _stream(stream)),
+                   "smj_dev_partition_regions_pk")
+        return out
     _lib.check(lib.smj_dev_partition_regions(_ptr(table), n, cols, int(use), select_col,
                                              int(select_val) if use else 0, key_col, spl, ns, reg, _ptr(out),
                                              ctypes.c_void_p(counts.data_ptr()), _stream(stream)),

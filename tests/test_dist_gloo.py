@@ -146,6 +146,11 @@ def make_tables(kind, n):
         S = rng.integers(0, 40, size=(n // 2, 3)).astype(np.int64)
         R[:, 0], S[:, 2] = np.arange(n), np.arange(n // 2) + 10 ** 6
         return R, S
+    if kind == "widepay":  # payloads over int32: the packed exchange falls back to plain rows
+        R, S = oracle.gen_uniform(n, 0, 1, 3 * n), oracle.gen_uniform(n, 0, 2, 3 * n)
+        R[:, 1] = rng.integers(-(1 << 62), 1 << 62, n)
+        S[:, 1] = rng.integers(-(1 << 62), 1 << 62, n)
+        return R, S
     if kind == "skew":  # one key carries most rows, negative keys too
         R = rng.integers(-1000, 1000, size=(n, 2)).astype(np.int64)
         S = rng.integers(-1000, 1000, size=(n, 2)).astype(np.int64)
@@ -236,6 +241,10 @@ def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
     # messages cut into 64 KiB pieces (SMJ_DIST_MAX_MSG; RCCL corrupts p2p
     # messages over ~2 GiB, profiles/r04/r04e): hundreds of pieces per stage
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "max_msg": 65536}),
+    # payloads over int32: packing falls back to plain rows on every rank
+    ("widepay", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
+    # the packed exchange turned off
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "pack": "0"}),
 ])
 def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, monkeypatch, kind, cfg):
     """The RCCL transport of smj/dist.py on the one GPU a test box has: one
@@ -245,6 +254,8 @@ def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, mo
     all run as on the 8-GPU node, bit-exact against the oracle."""
     if cfg.get("max_msg"):
         monkeypatch.setenv("SMJ_DIST_MAX_MSG", str(cfg["max_msg"]))
+    if cfg.get("pack"):
+        monkeypatch.setenv("SMJ_DIST_PACK", cfg["pack"])
     _run_and_check(tmp_path, 1, kind, dict(cfg, backend="nccl", loopback=True), 1_000_000)
 
 

@@ -407,3 +407,58 @@ def test_digest_matches_oracle(gpu, oracle_built, n, cols):
     a, b = n // 4, n // 2
     assert ops.digest(d[a:b], a) == oracle.digest(t[a:b], a)
     assert (ops.digest(d[:a]) + ops.digest(d[a:], a)) % (1 << 64) == oracle.digest(t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kc", [0, 1])
+def test_packed_exchange_rows(gpu, oracle_built, kc):
+    """The packed exchange format (smj.h smj_dev_partition_regions_pk /
+    smj_dev_unpack_rows / smj_dev_sort_merge_join_begin_pk): the packed
+    partition unpacks to the plain partition's rows exactly (keys on both
+    sides of the base, negative payloads, a WHERE), a row whose payload does
+    not fit int32 raises flag bit 2, and the pipeline on packed tables equals
+    the pipeline on the plain ones (sorted rows and joined rows)."""
+    import numpy as np
+    from smj import ops
+    from smj import dist as sdist
+    rng = np.random.default_rng(17 + kc)
+    n = 300_000
+    def table(pay_hi):
+        t = np.empty((n, 2), dtype=np.int64)
+        t[:, kc] = rng.integers(-(1 << 40), 1 << 40, n) // (1 << 10) + (1 << 40)
+        t[:, 1 - kc] = rng.integers(-pay_hi, pay_hi, n)
+        return t
+    R, S = table(1 << 30), table(1 << 31)
+    dR, dS = torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda()
+    kb = int(np.median(R[:, kc]))
+    bounds = sorted(set(int(x) for x in np.quantile(R[:, kc], [0.2, 0.5, 0.8]).astype(np.int64)))
+    reg, _ = ops.region_capacities(R[:: 97, kc], n, bounds)
+    for sel in (None, 0):
+        c0 = torch.empty(len(bounds) + 2, dtype=torch.int64, device="cuda")
+        c1 = torch.empty_like(c0)
+        a = ops.partition_regions(dR, bounds, reg, c0, kc, kc, sel)
+        b = ops.partition_regions(dR, bounds, reg, c1, kc, kc, sel, pack=(kb, 7))
+        torch.cuda.synchronize()
+        assert int(c1[-1]) == 0 and torch.equal(c0, c1)
+        nb = len(bounds) + 1
+        for q in range(nb):
+            st, cnt = reg[q], int(c0[q])
+            np.testing.assert_array_equal(ops.unpack_rows(b[st: st + cnt], kc, (kb, 7)).cpu().numpy(),
+                                          a[st: st + cnt].cpu().numpy())
+    # a payload that does not fit: flag bit 2
+    c2 = torch.empty(len(bounds) + 2, dtype=torch.int64, device="cuda")
+    dW = dR.clone()
+    dW[123, 1 - kc] = 1 << 40
+    ops.partition_regions(dW, bounds, reg, c2, kc, kc, None, pack=(kb, 0))
+    torch.cuda.synchronize()
+    assert int(c2[-1]) & 4
+    # the pipeline on packed input (both, either) = on plain input
+    pR = ops.partition_regions(dR, [], [0, n], torch.empty(2, dtype=torch.int64, device="cuda"), kc, pack=(kb, -5))
+    pS = ops.partition_regions(dS, [], [0, n], torch.empty(2, dtype=torch.int64, device="cuda"), kc, pack=(kb + 99, 0))
+    ref = ops.sort_merge_join(dR, dS, kc, kc, None, None)
+    for p1, p2 in (((kb, -5), (kb + 99, 0)), (None, (kb + 99, 0)), ((kb, -5), None)):
+        job = ops.sort_merge_join_begin_pk(pR[:n] if p1 else dR, pS[:n] if p2 else dS, kc, kc, p1, p2)
+        got = job.end()
+        for g, r in zip(got, ref):
+            assert torch.equal(g, r)
+    del sdist

@@ -126,6 +126,7 @@ for s in $STEPS; do
              SMJ_PB_ORDER=0 run c4o0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4o0_$r.out" c4_plain
            done ;;
     loop)  run loop 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop.out" loop ;;
+    loopnp) SMJ_DIST_PACK=0 run loopnp 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopnp.out" loop_nopack ;;
     loopns) SMJ_DIST_SPLIT=0 run loopns 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loopns.out" loop_nosplit ;;
     loopab) for r in 1 2 3; do
               run loop_s$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_s$r.out" loop_split
