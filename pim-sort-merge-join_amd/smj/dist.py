@@ -71,8 +71,11 @@ DEFAULT_STAGES = int(_STAGES_ENV) if _STAGES_ENV else None
 # 9.89-9.92, three stages 0.15/0.3/0.55 9.38-9.49 (the default there).  Round 5,
 # with S's partition on its own stream (profiles/r05/r05m, r05o: two rounds
 # each on two boxes): K = 2 9.00 / 8.86 / 9.11 / 9.07, K = 3 9.06 / 8.96 / 9.11
-# / 9.17, K = 4 9.22 / 9.20 / 9.46 / 9.26 ms -- two stages again.  Across GPUs
-# the exchange dominates and the stages stay equal.
+# / 9.17, K = 4 9.22 / 9.20 / 9.46 / 9.26 ms -- two stages again; then with
+# packed exchange rows (half the self-copy bytes, profiles/r05/r05zf) K = 1
+# 8.14 / 8.23, K = 2 8.42 / 8.44, K = 3 9.57 / 9.77 ms: on one GPU the copy
+# is now cheaper than a second pipeline call, so one stage.  Across GPUs the
+# exchange dominates and the stages stay equal.
 _FRAC_ENV = os.environ.get("SMJ_DIST_STAGE_FRAC")
 
 
@@ -89,7 +92,7 @@ def stage_fracs(world, K):
 
 
 def default_stages(world):
-    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (2 if world == 1 else 4)
+    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (1 if world == 1 else 4)
 # loopback: a rank's own segment also travels through the point-to-point
 # transport (send / receive to itself; RCCL only: gloo keeps the device copy)
 # instead of a device copy, and one rank runs the whole distributed path: the
@@ -524,7 +527,7 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     (optional dict) gets the rows this rank received per table and the
     max / mean load over ranks (load-balance report).  stages: key sub-ranges
     per rank whose exchange overlaps the previous one's sort + join
-    (default SMJ_DIST_STAGES, else default_stages(W): 2 on one rank, 4 at
+    (default SMJ_DIST_STAGES, else default_stages(W): 1 on one rank, 4 at
     W > 1, lowered by stage_count to what the partition fits; 1 = exchange
     everything, then compute).
     loopback (default SMJ_DIST_LOOPBACK=1): the rank's own segments also go
