@@ -91,8 +91,16 @@ def stage_fracs(world, K):
     return None
 
 
-def default_stages(world):
-    return DEFAULT_STAGES if DEFAULT_STAGES is not None else (1 if world == 1 else 4)
+def default_stages(world, rows=0):
+    """rows: the larger table's rows on this rank.  One rank (the loopback):
+    one stage while the tables fit one pipeline call, else three -- a single
+    stage of C4's 1e9-row tables held every buffer at once and ran 459 ms
+    against 90 (profiles/r05/r05zg).  More ranks: 4 (every rank alike)."""
+    if DEFAULT_STAGES is not None:
+        return DEFAULT_STAGES
+    if world == 1:
+        return 1 if rows <= PACK_MAX_ROWS else 3
+    return 4
 # loopback: a rank's own segment also travels through the point-to-point
 # transport (send / receive to itself; RCCL only: gloo keeps the device copy)
 # instead of a device copy, and one rank runs the whole distributed path: the
@@ -527,7 +535,7 @@ def sort_merge_join(R, S, select=(0, 5000, 0, 5000), keys=(0, 0), group=None, op
     (optional dict) gets the rows this rank received per table and the
     max / mean load over ranks (load-balance report).  stages: key sub-ranges
     per rank whose exchange overlaps the previous one's sort + join
-    (default SMJ_DIST_STAGES, else default_stages(W): 1 on one rank, 4 at
+    (default SMJ_DIST_STAGES, else default_stages(W): 1 on one rank (3 for tables over 1.6e8 rows), 4 at
     W > 1, lowered by stage_count to what the partition fits; 1 = exchange
     everything, then compute).
     loopback (default SMJ_DIST_LOOPBACK=1): the rank's own segments also go
@@ -686,7 +694,7 @@ class _HostGather:
 
 
 def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stats, stages, loopback, world, rank):
-    K = stage_count(world, default_stages(world) if stages is None else stages)
+    K = stage_count(world, default_stages(world, max(R.shape[0], S.shape[0])) if stages is None else stages)
     nseg = world * K
     tr = _Tracer(TRACE and R.is_cuda, rank)
 
