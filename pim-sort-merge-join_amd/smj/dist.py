@@ -114,11 +114,23 @@ TRACE_MODE = os.environ.get("SMJ_DIST_TRACE", "0")
 TRACE = TRACE_MODE in ("1", "2")
 
 
+_T_LAST = [0.0]  # the host time the previous traced call returned
+
+
 class _Tracer:
     def __init__(self, on, rank):
         import time
         self.on, self.rank, self.time = on and rank == 0, rank, time
         self.t = self.time.perf_counter() if self.on else 0.0
+        if self.on and _T_LAST[0]:
+            import sys
+            print(f"smj.dist trace: since the previous call returned: {(self.t - _T_LAST[0]) * 1e3:.2f} ms",
+                  file=sys.stderr, flush=True)
+
+    def end(self):
+        if self.on:
+            self("return")
+            _T_LAST[0] = self.time.perf_counter()
 
     def __call__(self, what):
         if not self.on:
@@ -738,8 +750,10 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         big = max(int(a[:, 1 + 2 + x].sum()) for x in range(2)) * smax / world * 1.25
         can_pack = big <= PACK_MAX_ROWS
     packs = [(_key_base(est, x), 0) if can_pack and T.shape[1] == 2 else None for x, T in enumerate((R, S))]
+    tr("bounds, regions, key bases")
     part = [_partition(ops, R, bounds, cnt[0], own[0], k1, sc1, sv1, packs[0])]
     gR = _HostGather(cnt[0], world, group)
+    tr("R partition + gather enqueued")
     if sside is not None:
         # after R's partition: the two calls share the library's partition
         # scratch (region words, look-back status words), so they must not run
@@ -783,6 +797,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         sl[t] = [slice_ranges(counts[t][r], [sum(counts[t][q][b] for q in range(r)) for b in range(nb)], cuts, nb)
                  for r in range(world)]
 
+    tr("S partition enqueued")
     allcR = gR.result()  # host sync 2 (R's counts)
     tr("partition R + counts")
     GR = [sum(allcR[r][b] for r in range(world)) for b in range(nb)]
@@ -865,6 +880,7 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         mean = sum(loads) / world
         stats.update(rows_in=rows_in, loads=loads, load_max_over_mean=(max(loads) / mean) if mean else 1.0,
                      cuts=cuts, buckets=nb, stages=K)
+    tr.end()
     if into:
         return J[:at]
     if not parts:
