@@ -198,6 +198,12 @@ for s in $STEPS; do
            r=${s#sv:}; v=${r%%:*}; q=${r#*:}; SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/$v/libsmj_hip.so SMJ_DEBUG_PART1=1 run sv_${v}_$(echo $q | tr -c 'a-z0-9' '_') 170 python -u tools/seq_sizes.py --seq $q ;;
     seq)   SMJ_DEBUG_PART1=1 SMJ_DEBUG_HOST=1 run seq 170 python -u tools/seq_sizes.py ;;
     dbg4n) SMJ_DIST_S_SIDE=0 SMJ_DIST_TRACE=1 SMJ_DEBUG_PART1=1 run dbg4n 170 python -u bench.py --loopback --workload c4 --steps 1 --warmup 0 $NOCPU ;;
+    abpk)  for r in 1 2; do  # same-box A/B of packed parts in the partitioned mode, C4 and C5
+             for w in c4 c5; do
+               run ${w}pk1_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/${w}pk1_$r.out" ${w}_packed
+               SMJ_PART_PACK=0 run ${w}pk0_$r 600 python bench.py --workload $w --steps 5 --warmup 2 $NOCPU && summ "$OUT/${w}pk0_$r.out" ${w}_plain
+             done
+           done ;;
     abh5)  for r in 1 2; do  # same-box A/B of heavy-key sub-buckets on C5
              run c5h1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5h1_$r.out" c5_heavy
              SMJ_HEAVY=0 run c5h0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5h0_$r.out" c5_noheavy
