@@ -430,3 +430,32 @@ def test_dist_splitters_kernel_many_ranks(pkg_built, world):
             out = ops.dist_splitters(torch.from_numpy(allb.reshape(-1)).cuda(), world, stride, parts, q20)
             got = out.cpu().numpy()
             assert got[:parts - 1].tolist() == ref and int(got[parts - 1]) == L, (trial, parts, fr)
+
+
+def test_key_base_and_stage_defaults():
+    """The packed exchange's key base is the middle of the gathered key
+    sample of the table (all ranks; 0 without samples, exact in int64 at the
+    extremes), and one rank runs one stage only while its tables fit one
+    pipeline call."""
+    from smj import dist as sdist
+    I64 = np.iinfo(np.int64)
+    H, cap = 5, 8
+    a = np.full((2, H + cap), I64.max, dtype=np.int64)
+    a[0, :H] = [3, 2, 1, 10, 10]
+    a[0, H:H + 3] = [-7, 5, 100]       # R: -7, 5; S: 100
+    a[1, :H] = [2, 1, 1, 10, 10]
+    a[1, H:H + 2] = [40, -300]         # R: 40; S: -300
+    est = {"all": a, "H": H, "nt": 2}
+    assert sdist._key_base(est, 0) == (-7 + 40) // 2
+    assert sdist._key_base(est, 1) == (-300 + 100) // 2
+    b = a.copy()
+    b[:, 1:3] = 0
+    assert sdist._key_base({"all": b, "H": H, "nt": 2}, 0) == 0
+    c = a.copy()
+    c[0, H] = I64.min
+    c[1, H] = I64.max - 1
+    assert sdist._key_base({"all": c, "H": H, "nt": 2}, 0) == (int(I64.min) + int(I64.max) - 1) // 2
+    if sdist.DEFAULT_STAGES is None:
+        assert sdist.default_stages(1, 100_000_000) == 1
+        assert sdist.default_stages(1, 1_000_000_000) == 3
+        assert sdist.default_stages(8, 10) == 4
