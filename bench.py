@@ -129,7 +129,7 @@ def step_single(R, S, bufs):
 MASK64 = (1 << 64) - 1
 
 
-def verify_distributed(J, rank, world, dev, full_tables):
+def verify_distributed(J, rank, world, dev, full_tables, wire=None):
     """Self-check of a distributed (or --loopback) result, after the timed
     steps: every rank digests its slice of the joined rows at its global
     position (smj_dev_digest: order-sensitive, position-mixed), the digests
@@ -138,18 +138,20 @@ def verify_distributed(J, rank, world, dev, full_tables):
     whole job's tables -- full_tables() makes them -- and digests the same
     slices of its result.  Returns (ok on every rank, details on rank 0).
     The reference order is the one the reference's host builds by
-    concatenating DPU outputs in DPU order (app.c:585-692)."""
+    concatenating DPU outputs in DPU order (app.c:585-692).  wire: the
+    device the gathers run on (cpu under gloo; default dev)."""
     t0 = time.perf_counter()
-    cnt = torch.tensor([J.shape[0]], dtype=torch.int64, device=dev)
+    wire = dev if wire is None else wire
+    cnt = torch.tensor([J.shape[0]], dtype=torch.int64, device=wire)
     allc = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(allc, cnt)
     counts = [int(c.item()) for c in allc]
     offs = [sum(counts[:r]) for r in range(world)]
-    d = ops.digest_async(J, offs[rank])
+    d = ops.digest_async(J, offs[rank]).to(wire)
     alld = [torch.zeros_like(d) for _ in range(world)]
     dist.all_gather(alld, d)
     got = [int(x.item()) & MASK64 for x in alld]
-    flag = torch.zeros(1, dtype=torch.int64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int64, device=wire)
     info = None
     if rank == 0:
         torch.cuda.empty_cache()  # the distributed path's cached blocks, for the library's own allocations
@@ -185,15 +187,26 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # SMJ_BENCH_REHEARSE=1: the N > 1 line rehearsed on fewer GPUs than ranks
+    # (tests/test_gpu_bench.py on the one-GPU test box): ranks share the
+    # visible GPUs, and the process group is gloo (RCCL takes one GPU per
+    # rank) -- smj.dist then stages the exchange through host memory.  Never
+    # a measurement: the line says so in config.parallelism.
+    rehearse = os.environ.get("SMJ_BENCH_REHEARSE", "0") != "0"
+    if rehearse:
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = "gloo" if rehearse else "nccl"
+    wire = torch.device("cpu") if backend == "gloo" else dev  # bench.py's own collectives
     if world > 1 or a.loopback:
+        kw = {} if rehearse else {"device_id": dev}
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+            dist.init_process_group(backend, rank=0, world_size=1, **kw)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group(backend, **kw)
     distributed = world > 1 or a.loopback
 
     n = a.rows
@@ -297,15 +310,15 @@ def main():
     verified, verification = None, None
     if distributed and a.verify:
         progress("verification: digests of every rank's slice, then the single-GPU call on rank 0")
-        verified, verification = verify_distributed(res, rank, world, dev, full_tables)
+        verified, verification = verify_distributed(res, rank, world, dev, full_tables, wire)
         if rank == 0:
             log(f"verification: {verification}")
     rank_rows = [nr + ns]  # every rank's generated input rows (R + S), rank order
     if world > 1:
-        got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(got, torch.tensor([nr + ns], dtype=torch.int64, device=dev))
+        got = [torch.zeros(1, dtype=torch.int64, device=wire) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([nr + ns], dtype=torch.int64, device=wire))
         rank_rows = [int(g.item()) for g in got]
-    t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, float(joined)], dtype=torch.float64, device=wire)
     if world > 1:
         tt = t.clone()
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
@@ -317,7 +330,9 @@ def main():
     value = rows_step / (dt / a.steps)
 
     # roofline of the dominant kernel: algorithmic bytes / its event time
-    dom = max(prof.items(), key=lambda kv: kv[1]["ms"]) if prof else (None, None)
+    # (kernels with algorithmic bytes only: at small test sizes a fixed-cost
+    # bookkeeping kernel can take the most time)
+    dom = max((kv for kv in prof.items() if kv[1]["bytes"] > 0), key=lambda kv: kv[1]["ms"], default=(None, None))
     roof = None
     pmc = None
     # the PMC summary is per launch of ONE configuration (profiles/pmc_traffic.json:
@@ -437,7 +452,8 @@ def main():
             "config": {"workload": workload_name(a.workload, world, distributed),
                        "rows_per_table_per_gpu": [nr, ns], "rows_per_table_total": [NR, NS],
                        "rank_input_rows": rank_rows, "key_range": key_range,
-                       "joined_rows": joined, "parallelism": f"range-partition x{world}" + (" (RCCL loopback)" if a.loopback else ""),
+                       "joined_rows": joined, "parallelism": f"range-partition x{world}" + (" (RCCL loopback)" if a.loopback else "")
+                                      + (" (REHEARSAL: gloo, ranks sharing GPUs; not a measurement)" if rehearse else ""),
                        "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
                        "rank_rows_after_exchange": lb.get("loads"),
                        "exchange_stages": lb.get("stages", 0)},

@@ -54,6 +54,7 @@ for s in $STEPS; do
     lfull) test_run lfull 900 $PYT tests/test_gpu_large.py -k "full_size" ;;
     dist)  test_run dist 600 $PYT tests/test_dist_gloo.py -m gpu ;;
     multidev) test_run multidev 600 $PYT tests/test_gpu_multidev.py ;;
+    benchtest) test_run benchtest 600 $PYT tests/test_gpu_bench.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
