@@ -109,6 +109,13 @@ for s in $STEPS; do
              SMJ_LIB=$V/p1i4/libsmj_hip.so run c4i4_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i4_$r.out" c4_p1items4
              SMJ_LIB=$V/p1i6/libsmj_hip.so run c4i6_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4i6_$r.out" c4_p1items6
            done ;;
+    abp1l) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # same-box A/B of the partition tile on the loopback C3 line
+           for r in 1 2; do
+             run lp8_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lp8_$r.out" loop_p1items8
+             for i in 4 6 12; do
+               SMJ_LIB=$V/p1i$i/libsmj_hip.so run lp${i}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lp${i}_$r.out" loop_p1items$i
+             done
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
