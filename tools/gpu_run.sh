@@ -116,6 +116,14 @@ for s in $STEPS; do
                SMJ_LIB=$V/p1i$i/libsmj_hip.so run lp${i}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lp${i}_$r.out" loop_p1items$i
              done
            done ;;
+    abp1pk) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # same-box A/B of the packed-staging partition (loopback C3)
+           for r in 1 2; do
+             SMJ_LIB=$V/p1head/libsmj_hip.so run lph_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lph_$r.out" loop_head
+             run lpk4_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpk4_$r.out" loop_pk_wpe4
+             for i in 6 8; do
+               SMJ_LIB=$V/p1pk$i/libsmj_hip.so run lpk${i}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpk${i}_$r.out" loop_pk_wpe$i
+             done
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
