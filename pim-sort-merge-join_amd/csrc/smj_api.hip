@@ -527,6 +527,7 @@ std::map<int, MsdScratch> g_msd;
 int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD-fallback groups, m_R, m_S
 int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
 int64_t g_msd_bigdev = 0;                // last pipeline: oversized multi-key groups sorted on the device
+int64_t g_msd_packb = 0;                 // last pipeline: pass-B rows packed (MsdPlan::packB)
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -952,6 +953,10 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         if (in[x].pk && (in[x].cols != 2 || in[x].use_sel || in[x].desc || stg)) return SMJ_ERR_INVALID;
     MsdScratch *ms;
     SMJ_TRY(msd_scratch(&ms));
+    // packed pass-B rows (MsdPlan::packB; decided on the device from the data)
+    int pack_mode = msd_packb_mode();  // 0 off, 1 unskewed tables, 2 forced (tests)
+    for (int x = 0; x < ntab; x++) pack_mode = in[x].cols == 2 ? pack_mode : 0;
+    const bool pack_ok = pack_mode != 0;
     int T_[2] = {1, 1}, TB_[2] = {1, 1};  // pass-A / pass-B tile rows
     int64_t tilesA[2] = {0, 0}, maxB[2] = {0, 0};
     for (int x = 0; x < ntab; x++) {
@@ -962,7 +967,9 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         tilesA[x] = t.desc ? t.ntiles : (t.n + T_[x] - 1) / T_[x];
         maxB[x] = (t.n + TB_[x] - 1) / TB_[x] + kBucketsA;  // every bucket adds <= 1 partial pass-B tile
         const size_t W = (size_t)t.cols * 8;
-        SMJ_TRY(grow(&ts.tempA, &ts.c_tempA, (size_t)std::max<int64_t>(1, std::max(t.n, tilesA[x] * T_[x])) * W));
+        // (with packed pass-B rows tempA is also the unpacked shadow of tempB: >= its rows)
+        SMJ_TRY(grow(&ts.tempA, &ts.c_tempA,
+                     (size_t)std::max<int64_t>({(int64_t)1, t.n, tilesA[x] * T_[x], pack_ok ? maxB[x] * TB_[x] : 0}) * W));
         SMJ_TRY(grow(&ts.tempB, &ts.c_tempB, (size_t)maxB[x] * TB_[x] * W));
         SMJ_TRY(grow(&ts.offsA, &ts.c_offsA, std::max<int64_t>(1, tilesA[x]) * kOffsARow * 4));
         SMJ_TRY(grow(&ts.tmm, &ts.c_tmm, std::max<int64_t>(1, tilesA[x]) * 16));
@@ -1021,6 +1028,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         pp[x].pk = in[x].pk;
         pp[x].pkk = in[x].pkk;
         pp[x].pkp = in[x].pkp;
+        pp[x].nopack = pack_ok ? &ms->plan->nopack : nullptr;
     }
     if (stg && (in[0].desc || (ntab > 1 && in[1].desc))) return SMJ_ERR_INVALID;  // (staged input is contiguous)
     // both tables in one launch when nothing is staged and the widths agree (no tail between them)
@@ -1116,6 +1124,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         bp.combined = msd_combined(in, ntab);
         bp.spl = ms->spl;
         bp.plan = ms->plan;
+        bp.pack_ok = pack_mode;
         HIP_TRY(launch_msd_bases(bp, s));
         HIP_TRY(launch_msd_runs_apply(ra, s));
     }
@@ -1166,6 +1175,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
     fp.counts = ms->counts;
     fp.plan = ms->plan;
     fp.big_list = ms->big_list;
+    fp.single_list = ms->single_list;
     fp.wide_list = ms->wide_list;
     fp.radix_list = ms->radix_list;
     fp.giant = nullptr;  // the job split's buffers: sized and set by msd_fallback
@@ -1178,6 +1188,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
     fp.join = join;
     fp.combined = msd_combined(in, ntab);
     fp.key2 = key2;
+    for (int x = 0; x < ntab; x++) fp.shadow[x] = pack_ok ? (int64_t *)ms->t[x].tempA : nullptr;
     if (t_slot < 0) g_fin_last = fp;
     {
         ProfScope ps("msd_final", 0, s);
@@ -1244,9 +1255,13 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
         g_msd_groups[2] = ms->h_plan->nwide;
         g_msd_bigdev = ms->h_plan->nbigdev;
         g_msd_groups[3] = ms->h_plan->nlsd;
+        g_msd_packb = ms->h_plan->packB;
     }
     bool redo = false;
-    SMJ_TRY(msd_fallback(ms, in, ntab, join, fp, out_j, s, &redo));
+    MsdFinalParams ff = fp;  // the host-launched tiers read 16-B rows: the shadow when pass-B rows were packed
+    if (ms->h_plan->packB)
+        for (int x = 0; x < ntab; x++) ff.tab[x].tempB = fp.shadow[x];
+    SMJ_TRY(msd_fallback(ms, in, ntab, join, ff, out_j, s, &redo));
     if (redo) {
         SMJ_TRY(compact(1));
         pc = prof_last();
@@ -2034,6 +2049,8 @@ extern "C" void smj_debug_msd_tiers(int64_t *out4) {
 // Diagnostic only (not part of smj.h): oversized multi-key groups of the last
 // pipeline call that msd_big_stage_kernel sorted (the rest: host fallback)
 extern "C" int64_t smj_debug_msd_bigdev(void) { return g_msd_bigdev; }
+// Diagnostic only: 1 if the last pipeline call packed its pass-B rows
+extern "C" int64_t smj_debug_msd_packb(void) { return g_msd_packb; }
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {
     for (int i = 0; i < 4; i++) out4[i] = g_msd_stats[i];

@@ -296,6 +296,7 @@ struct MsdPartAParams {
     int64_t ntiles = 0;
     int pk = 0;                  // packed input (MsdTable::pk)
     int64_t pkk = 0, pkp = 0;
+    uint32_t *nopack = nullptr;  // 2-column tables: MsdPlan::nopack, set when a row's other column does not fit int32
 };
 struct MsdPartA2 {       // one part_a launch over up to two tables
     MsdPartAParams t[2];
@@ -363,6 +364,18 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
                          // (msd_plan_failed), so a failed plan never drives a gather or a store.
     uint32_t gticket;    // msd_group_kernel: bucket tickets, taken in the order workgroups start
     uint32_t skew;       // msd_sample_select: sampled keys that another sample repeats (skew: msd_heavy_kernel runs)
+    // Packed pass-B rows (2-column tables): part_b writes each row as ONE word
+    // (uint32) key | (uint32) other << 32 -- the key's low 32 bits and the
+    // other column, which must fit int32 -- so it writes, and the staged final
+    // kernel gathers, 8 B per row instead of 16.  A key is rebuilt from its
+    // group's base: base + (uint32)(lo32 - (uint32)base), exact while
+    // key - base < 2^32 (the staged kernel's groups span <= 4096 keys; every
+    // group lies in [gmin, gmax], so packB requires gmax - gmin < 2^32).  The
+    // other final tiers read 16-B rows that msd_unpack_groups_kernel expands
+    // into tempA (dead after part_b) for exactly the groups the staged kernel
+    // does not take.
+    uint32_t nopack;     // part_a: a selected row's other column does not fit int32
+    uint32_t packB;      // msd_bases: pass-B rows are packed in this call
 };
 // A kernel launched after msd_group_kernel reads the plan's error word first:
 // a set bit means the dense group array may hold slots this call never wrote.
@@ -382,6 +395,7 @@ struct MsdBasesParams {
     const int64_t *spl;
     MsdBucket *bk[2];
     MsdPlan *plan;
+    int pack_ok;               // msd_packb_mode() with 2-column tables: MsdPlan::packB may be set (2: despite skew)
     const uint32_t *nheavy;    // [kBucketsA] heavy keys per bucket (msd_heavy_kernel), nullptr = none
 };
 struct MsdPartBParams {
@@ -435,6 +449,7 @@ struct MsdFinalParams {
     uint32_t *counts;
     MsdPlan *plan;
     uint32_t *big_list;
+    uint32_t *single_list = nullptr;  // msd_group's single-key groups (msd_unpack_groups_kernel)
     uint32_t *wide_list; // dense indices of groups for msd_final_wide_kernel
     uint32_t *radix_list;// groups for the radix tier (msd_final_kernel in list mode; nullptr = contiguous mode)
     uint4 *giant;        // groups over kBgMaxRows rows: {dense group, first job, jobs}
@@ -443,6 +458,10 @@ struct MsdFinalParams {
     uint32_t bg_max, bg_seg;  // msd_bg_limits()
     int ntab, join, key2, dbg;
     int combined;        // the group kernel packed combined groups (staged kernel: R rows then S rows in one sort)
+    int64_t *shadow[2] = {nullptr, nullptr};  // packB: 16-B rows of the groups the staged kernel does not take
+                                              // (tempA, >= capB rows); nullptr: packing off for the call
+    int pk_mode = -1;    // a tier launched before the host knows MsdPlan::packB: run only if packB == pk_mode
+                         // (tab[].tempB then holds packed words (1) or rows (0)); -1: always
 };
 
 // ---- C-ABI internals shared by smj_api.hip and smj_host.hip -------------------
@@ -556,6 +575,7 @@ hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
+int msd_packb_mode();  // packed pass-B rows (MsdPlan::packB): 0 off, 1 on unskewed tables, 2 forced (SMJ_PACKB)
 hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
 // out[i] = groups[list[i]] over the single-key then oversized list entries

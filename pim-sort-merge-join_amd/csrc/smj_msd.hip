@@ -449,6 +449,18 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
         mn = v ? min(mn, k) : mn;
         mx = v ? max(mx, k) : mx;
     }
+    if constexpr (COLS == 2) {
+        if (p.nopack) {  // packed pass-B rows need the other column in int32 (MsdPlan::packB)
+            bool bad = false;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const int64_t o = rows[it][1 - p.key_col];
+                bad = bad || (((vmask >> it) & 1u) && (int64_t)(int32_t)o != o);
+            }
+            const uint64_t bm = __ballot(bad);
+            if (bm && lane == __builtin_ctzll(bm)) atomicOr(p.nopack, 1u);
+        }
+    }
     wave_rank<ITEMS, kBitsA>(dig, vmask, wc, lane);
     __syncthreads();
     const uint32_t total = tile_digit_starts<RADIX, NT>(s_wcnt, s_bin, s_wsum);
@@ -1044,6 +1056,16 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
         mn = min(mn, s_mm[w]);
         mx = max(mx, s_mm[kBasesWaves + w]);
     }
+    // packed pass-B rows: other columns in int32, every key within 2^32 of
+    // any group base, and no heavy keys (msd_heavy_kernel's, or a repeated
+    // splitter: they make single-key / oversized groups, whose rows the other
+    // tiers read through the unpacked copy)
+    const bool hv = a < kBucketsA && ((p.nheavy && p.nheavy[a] != 0u) || (a + 1 < kSplA && p.spl[a] == p.spl[a + 1]));
+    const bool any_heavy = __syncthreads_or(hv) != 0;
+    if (a == 0)
+        p.plan->packB = p.pack_ok && p.plan->nopack == 0u && (p.pack_ok == 2 || !any_heavy) && mn <= mx &&
+                                (uint64_t)mx - (uint64_t)mn < (1ull << 32)
+                            ? 1u : 0u;
     // rows of bucket a per table
     uint32_t Lt[2] = {0u, 0u};
     if (a < kBucketsA)
@@ -1622,8 +1644,18 @@ __device__ __forceinline__ void pb_marks(const uint2 *lst, uint32_t *bm, uint16_
     }
 }
 
-template <int COLS>
+// the packed pass-B word of a 2-column row (MsdPlan::packB): the key's low 32
+// bits, the other column's low 32 bits above them
+__device__ __forceinline__ uint64_t pb_word(const int64_t (&r)[2], int key_col) {
+    return (uint64_t)(uint32_t)r[key_col] | ((uint64_t)(uint32_t)r[1 - key_col] << 32);
+}
+
+// PK: this instantiation writes packed words.  Both are launched; the one
+// whose PK is not MsdPlan::packB returns at once (the flag is set on the
+// device by msd_bases, after the host has enqueued the call)
+template <int COLS, bool PK = false>
 __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(const MsdPartBParams p) {
+    static_assert(!PK || COLS == 2, "packed rows: 2-column tables");
     constexpr int NT = pb_threads(COLS), NW = NT / 64, T = msd_tile_b(COLS), ITEMS = T / NT, RADIX = kRadB;
     constexpr int DPT = RADIX / NT;
     static_assert(T % NT == 0 && RADIX % (2 * NT) == 0, "tile / histogram split");
@@ -1648,6 +1680,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
     uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + BMB);
     uint32_t *s_q = reinterpret_cast<uint32_t *>(s_u + QOFF);
 
+    if (COLS == 2 && (p.plan->packB != 0u) != PK) return;
     const int64_t ntl = (int64_t)p.plan->ntilesB[p.x];
     int64_t g = blockIdx.x;
     if (g >= ntl) return;
@@ -1917,7 +1950,11 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                 const int s = min(tid + it * NT, nrows - 1);
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)s * COLS, r);
-                store_row_nt<COLS>(dst + (size_t)s * COLS, r);
+                if constexpr (PK) {  // one word per row: tile g's words at [g T, g T + rows) of the u64 view
+                    __builtin_nontemporal_store(pb_word(r, p.key_col), reinterpret_cast<uint64_t *>(p.out) + g * T + s);
+                } else {
+                    store_row_nt<COLS>(dst + (size_t)s * COLS, r);
+                }
             }
         }
         __syncthreads();  // staging region read out
@@ -3019,6 +3056,7 @@ template <int C1, int C2>
 __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p) {
     __shared__ FinSmem sm;
     if (msd_plan_failed(p.plan)) return;
+    if (p.pk_mode >= 0 && (int)(p.plan->packB != 0u) != p.pk_mode) return;  // the other layout's launch
     unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     // contiguous mode: workgroup b walks a range of dense groups (pipelined one
     // group deep); list mode: the groups msd_final_stage_kernel handed over
@@ -3198,7 +3236,7 @@ __device__ unsigned long long g_st_sub[8];
         st_t = t_;                                                  \
     }
 
-template <bool COMB>
+template <bool COMB, bool PK>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                                const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
                                                StSmem &sm);
@@ -3209,7 +3247,7 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
 // non-empty range starting in (64b, v] (bitmap word + at[]; the list also
 // holds the group's empty ranges, so a popcount of the bitmap would not
 // index it).  S's ranges start at group row nR + their table row.
-template <bool COMB>
+template <bool COMB, bool PK>
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                          const uint32_t (&o1)[2], i64x2 (&rows)[kStIt], StSmem &sm, int &wsb) {
     const uint32_t tid = opaque_tid();
@@ -3218,12 +3256,14 @@ __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup
     uint32_t tot;
     const uint32_t ex = block_excl_scan_nb<kStWaves>(len[0] | (len[1] << 16), sm.wsum[wsb], &tot);  // + barrier
     wsb ^= 1;
-    st_issue_lists<COMB>(p, g, o0, o1, ex, rows, sm);
+    st_issue_lists<COMB, PK>(p, g, o0, o1, ex, rows, sm);
 }
 
 // st_issue after the run-length scan: ex = this thread's exclusive prefix of
-// (len R | len S << 16), the start bitmap zeroed and ordered by a barrier
-template <bool COMB>
+// (len R | len S << 16), the start bitmap zeroed and ordered by a barrier.
+// PK: tempB holds packed words (MsdPlan::packB); a row is rebuilt from its
+// word and the group's base (the group spans <= kStRange keys)
+template <bool COMB, bool PK>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                                const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
                                                StSmem &sm) {
@@ -3274,7 +3314,15 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
                     atomicOr(&p.plan->err, 2u);
                     ix = 0;
                 }
-                r = (x ? tB1 : tB0)[ix];
+                if constexpr (PK) {
+                    const uint64_t w = reinterpret_cast<const uint64_t *>(x ? p.tab[1].tempB : p.tab[0].tempB)[ix];
+                    const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
+                    const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
+                    const bool kc = (x ? p.tab[1].key : p.tab[0].key) != 0;
+                    r = {kc ? oth : key, kc ? key : oth};
+                } else {
+                    r = (x ? tB1 : tB0)[ix];
+                }
             }
         }
         rows[k] = r;
@@ -3691,10 +3739,11 @@ constexpr int kXcdSlots = 8;
 #ifndef SMJ_ST_MINW
 #define SMJ_ST_MINW 6
 #endif
-template <bool COMB>
+template <bool COMB, bool PK = false>
 __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
     __shared__ StSmem sm;
     if (msd_plan_failed(p.plan)) return;
+    if ((p.plan->packB != 0u) != PK) return;  // both are launched: the other layout's instantiation
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
     const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
@@ -3742,7 +3791,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         if (!have) {
             uint32_t o0[2], o1[2];
             st_load_offs(p, g, o0, o1);
-            st_issue<COMB>(p, g, o0, o1, cur, sm, wsb);
+            st_issue<COMB, PK>(p, g, o0, o1, cur, sm, wsb);
             __syncthreads();  // the list region is reused by the join
         }
         FIN_STAMP(0);
@@ -3767,7 +3816,7 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         // wave reaches after its st_issue_lists reads.  Without a next group
         // one barrier does both.
         if (nfit)  // the next group's rows: in flight while this one is written out
-            st_issue_lists<COMB>(p, gn, o0, o1, nex, cur, sm);
+            st_issue_lists<COMB, PK>(p, gn, o0, o1, nex, cur, sm);
         else
             __syncthreads();
         FIN_STAMP(3);
@@ -3787,12 +3836,55 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
 
+// Packed pass-B rows (MsdPlan::packB): the rows of every group the staged
+// kernel does not take -- msd_group's single-key and oversized lists and the
+// radix list the staged kernel handed over (the wide tier's and the late
+// oversized groups are taken from that list) -- expanded to 16-B rows at the
+// same row index of p.shadow[x] (tempA), which those tiers then read as their
+// tempB.  Launched after the staged kernel; a workgroup per listed group in
+// turn, a wave per pass-B tile run (every row lands at its own index).
+constexpr int kUnpackGrid = 1024;
+__global__ __launch_bounds__(256) void msd_unpack_groups_kernel(const MsdFinalParams p) {
+    if (msd_plan_failed(p.plan) || p.plan->packB == 0u) return;
+    const uint32_t ns = p.plan->nsingle, nb = p.plan->nbig, nr = p.plan->nradix;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t e = blockIdx.x; e < ns + nb + nr; e += gridDim.x) {
+        const uint32_t gi = e < ns ? p.single_list[e] : e < ns + nb ? p.big_list[e - ns] : p.radix_list[e - ns - nb];
+        const MsdGroup g = p.groups[gi];
+        for (int x = 0; x < p.ntab; x++) {
+            const MsdTab &tb = p.tab[x];
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(tb.tempB);
+            i64x2 *dst = reinterpret_cast<i64x2 *>(p.shadow[x]);
+            const bool kc = tb.key != 0;
+            auto put = [&](int64_t ix) {
+                const uint64_t w = src[ix];
+                const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
+                const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
+                dst[ix] = i64x2{kc ? oth : key, kc ? key : oth};
+            };
+            const MsdBucket bk = tb.bk[g.a];
+            if ((bk.one_key & 1u) && g.b0 == 0) {  // a single-key bucket's full tiles (group_gather)
+                const int64_t base = (int64_t)bk.tile_base * tb.tile, n = x ? g.nS : g.nR;
+                for (int64_t v = tid; v < n; v += 256) put(base + v);
+                continue;
+            }
+            const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
+            for (uint32_t i = (uint32_t)wave; i < K; i += 4) {
+                const int64_t id = (int64_t)bk.tile_base + i;
+                const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
+                for (uint32_t o = lo + (uint32_t)lane; o < hi; o += 64) put(id * tb.tile + o);
+            }
+        }
+    }
+}
+
 // groups of the wide list (key range over 22 bits, or a bucket with more than
 // kFinThreads pass-B tiles): the generic 64-bit path, persistent over the list
 template <int C1, int C2>
 __global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const MsdFinalParams p) {
     __shared__ FinalSmem sm;
     if (msd_plan_failed(p.plan)) return;
+    if (p.pk_mode >= 0 && (int)(p.plan->packB != 0u) != p.pk_mode) return;  // the other layout's launch
     const uint32_t nw = p.plan->nwide;
     for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
         final_group<C1, C2>(p, p.wide_list[i], sm);
@@ -5033,6 +5125,15 @@ static int64_t resident_blocks(K kernel, int threads, size_t dyn_lds) {
     return c;
 }
 
+// packed pass-B rows are written by the pipelined part_b only (2-column
+// tables); SMJ_PACKB=0 turns them off (A/B), =2 packs skewed tables too
+// (tests: the unpacked copy for the single-key / oversized tiers)
+int msd_packb_mode() {
+    const char *e = getenv("SMJ_PACKB");
+    const int m = e ? atoi(e) : 1;
+    return SMJ_PB_PIPE && m >= 0 && m <= 2 ? m : 0;
+}
+
 hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_tiles, hipStream_t s) {
     if (max_tiles <= 0) return hipSuccess;
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
@@ -5046,7 +5147,9 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
         if (C == 2 && SMJ_PB_PIPE) {
             const unsigned gp = (unsigned)std::min<int64_t>(
                 max_tiles, resident_blocks(msd_part_b_pipe_kernel<2>, pb_threads(2), pad));
-            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
+            // rows or packed words (MsdPlan::packB, known on the device only): the other returns at once
+            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, false>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
+            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, true>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
         } else {
             hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(pb_threads(C)), pad, s, p);
         }
@@ -5084,16 +5187,31 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
     if (two) {
         constexpr int kStGrid = SMJ_ST_GRID;
         static_assert(kStGrid % kXcdSlots == 0, "whole XCD sets");
-        if (p.combined)
-            hipLaunchKernelGGL(msd_final_stage_kernel<true>, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads), pad,
-                               s, p);
-        else
-            hipLaunchKernelGGL(msd_final_stage_kernel<false>, dim3(pad ? kStGrid / 2 : kStGrid), dim3(kStThreads), pad,
-                               s, p);
+        const unsigned sg = pad ? kStGrid / 2 : kStGrid;
+        // rows or packed words in tempB (MsdPlan::packB, set on the device):
+        // both layouts' launches go in, the other returns at entry
+        if (p.combined) {
+            hipLaunchKernelGGL((msd_final_stage_kernel<true, false>), dim3(sg), dim3(kStThreads), pad, s, p);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<true, true>), dim3(sg), dim3(kStThreads), pad, s, p);
+        } else {
+            hipLaunchKernelGGL((msd_final_stage_kernel<false, false>), dim3(sg), dim3(kStThreads), pad, s, p);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, true>), dim3(sg), dim3(kStThreads), pad, s, p);
+        }
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
-        hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
-        q.radix_list = nullptr;
-        hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+        if (p.shadow[0]) {  // packed: the other tiers' groups as rows in the shadow, then those tiers on it
+            hipLaunchKernelGGL(msd_unpack_groups_kernel, dim3(kUnpackGrid), dim3(256), 0, s, p);
+            q.pk_mode = 0;
+        }
+        for (int m = 0; m < (p.shadow[0] ? 2 : 1); m++) {
+            if (m == 1) {
+                q.pk_mode = 1;
+                for (int x = 0; x < 2; x++) q.tab[x].tempB = p.shadow[x];
+            }
+            q.radix_list = p.radix_list;
+            hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
+            q.radix_list = nullptr;
+            hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+        }
     } else {
         MsdFinalParams q = p;
         q.radix_list = nullptr;  // contiguous mode

@@ -287,6 +287,14 @@ def msd_stats():
     return tuple(int(v) for v in out)
 
 
+def msd_packb():
+    """1 if the last MSD pipeline call wrote packed pass-B rows (one 8-B word
+    per row, MsdPlan::packB in smj_internal.h), else 0."""
+    lib = _lib.load()
+    lib.smj_debug_msd_packb.restype = ctypes.c_int64
+    return int(lib.smj_debug_msd_packb())
+
+
 def msd_bigdev():
     """Oversized multi-key groups of the last MSD pipeline call sorted on the
     device (msd_big_stage_kernel); the other oversized ones took the host-driven

@@ -102,6 +102,49 @@ def test_fused_pipeline_matches_oracle(gpu, oracle_built, nr, ns, c1, c2, k1, k2
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, c1 + c2 - 1))
 
 
+PACKB_CASES = [
+    # SMJ_PACKB, nr, ns, kind, key1, key2, payload0 of S, select1, expect packed pass-B rows
+    ("1", 300_000, 300_000, "uniform", 0, 0, 10 ** 9, (0, 5000), 1),
+    ("1", 300_000, 200_000, "uniform", 1, 1, 10 ** 9, None, 1),           # key in column 1
+    ("1", 200_000, 200_000, "uniform", 0, 0, -(10 ** 9), None, 1),         # negative payloads (sign extension)
+    ("1", 100_000, 100_000, "uniform", 0, 0, 2 ** 31 - 50_000, None, 0),   # a payload over int32: rows
+    ("1", 100_000, 100_000, "wide", 0, 0, 10 ** 9, None, 0),               # keys over 2^32 apart: rows
+    ("1", 300_000, 300_000, "spread", 0, 0, 10 ** 9, None, 1),             # sub-buckets over 4096 keys: radix tier
+    ("2", 250_000, 250_000, "zipf", 0, 0, 10 ** 9, None, 1),               # single-key / oversized groups
+    ("2", 400_000, 25_000, "zipf", 0, 0, 10 ** 9, (0, 50), 1),             # combined groups
+    ("2", 200_000, 200_000, "dups", 0, 0, 10 ** 9, None, 1),
+    ("2", 120_000, 80_000, "extremes", 0, 0, 10 ** 9, None, 0),
+    ("0", 300_000, 300_000, "uniform", 0, 0, 10 ** 9, None, 0),
+]
+
+
+@pytest.mark.parametrize("mode,nr,ns,kind,k1,k2,pay0,s1,expect", PACKB_CASES)
+def test_packed_pass_b_rows(gpu, oracle_built, monkeypatch, mode, nr, ns, kind, k1, k2, pay0, s1, expect):
+    """Packed pass-B rows (MsdPlan::packB: part_b writes one 8-B word per row,
+    the staged final kernel rebuilds the row from the word and its group's
+    base, the other tiers read an unpacked copy): packed exactly when every
+    other column fits int32 and the keys span < 2^32 (SMJ_PACKB=2 packs skewed
+    tables too, so the single-key / oversized / radix tiers run on the
+    unpacked copy), and bit-exact either way."""
+    from smj import ops
+    monkeypatch.setenv("SMJ_PACKB", mode)
+    rng = np.random.default_rng(nr + ns + int(mode))
+    if kind == "spread":  # keys over [0, 2^31): pass-B sub-buckets of ~4100 keys, wider than the staged range
+        R = np.stack([rng.integers(0, 2 ** 31, nr), np.arange(nr)], axis=1).astype(np.int64)
+        S = np.stack([rng.integers(0, 2 ** 31, ns), pay0 + np.arange(ns)], axis=1).astype(np.int64)
+    else:
+        R = table(rng, nr, 2, kind, k1, 0)
+        S = table(rng, ns, 2, kind, k2, pay0)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, None)
+    assert ops.msd_packb() == expect, (ops.msd_packb(), ops.msd_groups())
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    if kind == "spread":
+        assert ops.msd_groups()[1] > 0  # the radix tier ran on the unpacked copy
+
+
 @pytest.mark.parametrize("nr,ns,kind,parts", [
     (300_000, 300_000, "uniform", 0),   # per-table staged groups
     (40_000, 400_000, "zipf", 0),       # combined groups + oversized groups (the device big tiers)

@@ -55,6 +55,9 @@ for s in $STEPS; do
     dist)  test_run dist 600 $PYT tests/test_dist_gloo.py -m gpu ;;
     multidev) test_run multidev 600 $PYT tests/test_gpu_multidev.py ;;
     benchtest) test_run benchtest 600 $PYT tests/test_gpu_bench.py ;;
+    pkt)   test_run pkt 600 $PYT tests/test_gpu_msd.py -k packed_pass_b ;;
+    msdpk2) SMJ_PACKB=2 test_run msdpk2 600 $PYT tests/test_gpu_msd.py ;;
+    msdpk0) SMJ_PACKB=0 test_run msdpk0 600 $PYT tests/test_gpu_msd.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
@@ -123,6 +126,16 @@ for s in $STEPS; do
              for i in 6 8; do
                SMJ_LIB=$V/p1pk$i/libsmj_hip.so run lpk${i}_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpk${i}_$r.out" loop_pk_wpe$i
              done
+           done ;;
+    abpkb) for r in 1 2; do  # same-box A/B of packed pass-B rows (SMJ_PACKB)
+             run c3pk1_$r 300 python bench.py $NOCPU && summ "$OUT/c3pk1_$r.out" c3_packb
+             SMJ_PACKB=0 run c3pk0_$r 300 python bench.py $NOCPU && summ "$OUT/c3pk0_$r.out" c3_rows
+           done
+           for r in 1 2; do
+             run c4pk1_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pk1_$r.out" c4_packb
+             SMJ_PACKB=0 run c4pk0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pk0_$r.out" c4_rows
+             run c5pk1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5pk1_$r.out" c5_packb
+             SMJ_PACKB=0 run c5pk0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5pk0_$r.out" c5_rows
            done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
