@@ -460,8 +460,8 @@ struct MsdFinalParams {
     int combined;        // the group kernel packed combined groups (staged kernel: R rows then S rows in one sort)
     int64_t *shadow[2] = {nullptr, nullptr};  // packB: 16-B rows of the groups the staged kernel does not take
                                               // (tempA, >= capB rows); nullptr: packing off for the call
-    int pk_mode = -1;    // a tier launched before the host knows MsdPlan::packB: run only if packB == pk_mode
-                         // (tab[].tempB then holds packed words (1) or rows (0)); -1: always
+    int pk_mode = -1;    // 2: the call may pack its pass-B rows (MsdPlan::packB, known on the device only) --
+                         // the radix / wide tiers then read p.shadow; -1: rows
 };
 
 // ---- C-ABI internals shared by smj_api.hip and smj_host.hip -------------------
@@ -572,10 +572,13 @@ hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int n
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
 hipError_t launch_msd_heavy(const MsdHeavyParams &p, hipStream_t s);
 hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s);
-hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s);
+// pb_pack: the call may pack its pass-B rows (MsdPlan::packB decides on the device)
+hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s, bool pb_pack = false);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
-int msd_packb_mode();  // packed pass-B rows (MsdPlan::packB): 0 off, 1 on unskewed tables, 2 forced (SMJ_PACKB)
+int msd_packb_mode();
+// the single-key / oversized groups' rows unpacked into MsdFinalParams::shadow (packed calls)
+hipError_t launch_msd_unpack_groups(const MsdFinalParams &p, hipStream_t s);  // packed pass-B rows (MsdPlan::packB): 0 off, 1 on unskewed tables, 2 forced (SMJ_PACKB)
 hipError_t launch_msd_big(const MsdFinalParams &p, hipStream_t s);
 hipError_t launch_msd_single(const MsdFinalParams &p, const uint2 *work, int64_t nwork, hipStream_t s);
 // out[i] = groups[list[i]] over the single-key then oversized list entries

@@ -1650,12 +1650,11 @@ __device__ __forceinline__ uint64_t pb_word(const int64_t (&r)[2], int key_col) 
     return (uint64_t)(uint32_t)r[key_col] | ((uint64_t)(uint32_t)r[1 - key_col] << 32);
 }
 
-// PK: this instantiation writes packed words.  Both are launched; the one
-// whose PK is not MsdPlan::packB returns at once (the flag is set on the
-// device by msd_bases, after the host has enqueued the call)
-template <int COLS, bool PK = false>
+// PKM: 0 rows, 2 packed words when MsdPlan::packB (set on the device by
+// msd_bases, after the host has enqueued the call: a block-uniform branch)
+template <int COLS, int PKM = 0>
 __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(const MsdPartBParams p) {
-    static_assert(!PK || COLS == 2, "packed rows: 2-column tables");
+    static_assert(PKM == 0 || COLS == 2, "packed rows: 2-column tables");
     constexpr int NT = pb_threads(COLS), NW = NT / 64, T = msd_tile_b(COLS), ITEMS = T / NT, RADIX = kRadB;
     constexpr int DPT = RADIX / NT;
     static_assert(T % NT == 0 && RADIX % (2 * NT) == 0, "tile / histogram split");
@@ -1680,7 +1679,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
     uint16_t *s_bt = reinterpret_cast<uint16_t *>(s_u + LISTB + BMB);
     uint32_t *s_q = reinterpret_cast<uint32_t *>(s_u + QOFF);
 
-    if (COLS == 2 && (p.plan->packB != 0u) != PK) return;
+    const bool PK = PKM == 2 && uni32(p.plan->packB) != 0u;
     const int64_t ntl = (int64_t)p.plan->ntilesB[p.x];
     int64_t g = blockIdx.x;
     if (g >= ntl) return;
@@ -1950,7 +1949,7 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                 const int s = min(tid + it * NT, nrows - 1);
                 int64_t r[COLS];
                 load_row<COLS>(s_rows + (size_t)s * COLS, r);
-                if constexpr (PK) {  // one word per row: tile g's words at [g T, g T + rows) of the u64 view
+                if (PK) {  // one word per row: tile g's words at [g T, g T + rows) of the u64 view
                     __builtin_nontemporal_store(pb_word(r, p.key_col), reinterpret_cast<uint64_t *>(p.out) + g * T + s);
                 } else {
                     store_row_nt<COLS>(dst + (size_t)s * COLS, r);
@@ -3050,13 +3049,60 @@ __device__ unsigned long long g_fin_phase[16];
         ph_t = t_;                                                  \
     }
 
+// Packed pass-B rows (MsdPlan::packB): group g's rows of every table
+// expanded from their words in tempB to 16-B rows at the same row index of
+// p.shadow[x] (tempA, dead after part_b), for the tiers other than the staged
+// kernel.  NT threads, a wave per pass-B tile run (every row lands at its own
+// index, so the order does not matter).
+template <int NT>
+__device__ __forceinline__ void unpack_group(const MsdFinalParams &p, const MsdGroup &g) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int x = 0; x < p.ntab; x++) {
+        const MsdTab &tb = p.tab[x];
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(tb.tempB);
+        i64x2 *dst = reinterpret_cast<i64x2 *>(p.shadow[x]);
+        const bool kc = tb.key != 0;
+        auto put = [&](int64_t ix) {
+            const uint64_t w = src[ix];
+            const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
+            const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
+            dst[ix] = i64x2{kc ? oth : key, kc ? key : oth};
+        };
+        const MsdBucket bk = tb.bk[g.a];
+        if ((bk.one_key & 1u) && g.b0 == 0) {  // a single-key bucket's full tiles (group_gather)
+            const int64_t base = (int64_t)bk.tile_base * tb.tile, n = x ? g.nS : g.nR;
+            for (int64_t v = tid; v < n; v += NT) put(base + v);
+            continue;
+        }
+        const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
+        for (uint32_t i = (uint32_t)wave; i < K; i += NT / 64) {
+            const int64_t id = (int64_t)bk.tile_base + i;
+            const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
+            for (uint32_t o = lo + (uint32_t)lane; o < hi; o += 64) put(id * tb.tile + o);
+        }
+    }
+}
+
+// the tiers after the staged kernel read 16-B rows: with MsdPlan::packB
+// (p.pk_mode == 2: the call may pack, known on the device only) those of
+// p.shadow, where unpack_group expanded their groups
+__device__ __forceinline__ MsdFinalParams rows_view(const MsdFinalParams &p_in) {
+    MsdFinalParams p = p_in;
+    if (p_in.pk_mode == 2 && uni32(p_in.plan->packB)) {
+        p.tab[0].tempB = p_in.shadow[0];
+        p.tab[1].tempB = p_in.shadow[1];
+    }
+    return p;
+}
+
 // persistent: workgroup b takes a contiguous range of dense groups (key
 // order), so consecutive groups share their bucket's tiles
 template <int C1, int C2>
-__global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p) {
+__global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFinalParams p_in) {
     __shared__ FinSmem sm;
-    if (msd_plan_failed(p.plan)) return;
-    if (p.pk_mode >= 0 && (int)(p.plan->packB != 0u) != p.pk_mode) return;  // the other layout's launch
+    if (msd_plan_failed(p_in.plan)) return;
+    const bool unpack = C1 == 2 && p_in.pk_mode == 2 && uni32(p_in.plan->packB) != 0u;
+    const MsdFinalParams p = rows_view(p_in);
     unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     // contiguous mode: workgroup b walks a range of dense groups (pipelined one
     // group deep); list mode: the groups msd_final_stage_kernel handed over
@@ -3072,6 +3118,14 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
         ge = min(ng, gb + per);
         step = 1;
     }
+    if (unpack) {  // this workgroup's groups first (list mode: packing implies 2-column tables)
+        for (int64_t it = gb; it < ge; it += step) {
+            const MsdGroup g = p.groups[lm ? (int64_t)p.radix_list[it] : it];
+            if (!g.flags) unpack_group<kFinThreads>(p_in, g);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
     FinalPref f;
     int wsb = 0;
     bool have = false;  // f holds the keys of group gi
@@ -3082,6 +3136,7 @@ __global__ __launch_bounds__(kFinThreads, 4) void msd_final_kernel(const MsdFina
             have = false;
             continue;
         }
+
         if (!fin_fast(p, g)) {
             if (threadIdx.x == 0) p.wide_list[atomicAdd(&p.plan->nwide, 1u)] = (uint32_t)gi;
             have = false;
@@ -3739,11 +3794,8 @@ constexpr int kXcdSlots = 8;
 #ifndef SMJ_ST_MINW
 #define SMJ_ST_MINW 6
 #endif
-template <bool COMB, bool PK = false>
-__global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
-    __shared__ StSmem sm;
-    if (msd_plan_failed(p.plan)) return;
-    if ((p.plan->packB != 0u) != PK) return;  // both are launched: the other layout's instantiation
+template <bool COMB, bool PK>
+__device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;  // blocks per XCD set
     const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
@@ -3836,55 +3888,43 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
 
-// Packed pass-B rows (MsdPlan::packB): the rows of every group the staged
-// kernel does not take -- msd_group's single-key and oversized lists and the
-// radix list the staged kernel handed over (the wide tier's and the late
-// oversized groups are taken from that list) -- expanded to 16-B rows at the
-// same row index of p.shadow[x] (tempA), which those tiers then read as their
-// tempB.  Launched after the staged kernel; a workgroup per listed group in
-// turn, a wave per pass-B tile run (every row lands at its own index).
+template <bool COMB, int PKM = 0>
+__global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kernel(const MsdFinalParams p) {
+    __shared__ StSmem sm;
+    if (msd_plan_failed(p.plan)) return;
+    constexpr bool PK = PKM == 1;
+    if (PKM == 2) {  // the layout is known on the device only: both bodies, one block-uniform branch
+        if (uni32(p.plan->packB)) st_body<COMB, true>(p, sm);
+        else st_body<COMB, false>(p, sm);
+        return;
+    }
+    st_body<COMB, PK>(p, sm);
+}
+
+// Packed pass-B rows: the single-key and oversized groups (msd_group's
+// lists) unpacked for the host-launched tiers (smj_api.hip msd_fallback,
+// which launches this only when the call packed and has such groups); the
+// radix tier unpacks its own groups.
 constexpr int kUnpackGrid = 1024;
 __global__ __launch_bounds__(256) void msd_unpack_groups_kernel(const MsdFinalParams p) {
     if (msd_plan_failed(p.plan) || p.plan->packB == 0u) return;
-    const uint32_t ns = p.plan->nsingle, nb = p.plan->nbig, nr = p.plan->nradix;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t e = blockIdx.x; e < ns + nb + nr; e += gridDim.x) {
-        const uint32_t gi = e < ns ? p.single_list[e] : e < ns + nb ? p.big_list[e - ns] : p.radix_list[e - ns - nb];
-        const MsdGroup g = p.groups[gi];
-        for (int x = 0; x < p.ntab; x++) {
-            const MsdTab &tb = p.tab[x];
-            const uint64_t *src = reinterpret_cast<const uint64_t *>(tb.tempB);
-            i64x2 *dst = reinterpret_cast<i64x2 *>(p.shadow[x]);
-            const bool kc = tb.key != 0;
-            auto put = [&](int64_t ix) {
-                const uint64_t w = src[ix];
-                const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
-                const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
-                dst[ix] = i64x2{kc ? oth : key, kc ? key : oth};
-            };
-            const MsdBucket bk = tb.bk[g.a];
-            if ((bk.one_key & 1u) && g.b0 == 0) {  // a single-key bucket's full tiles (group_gather)
-                const int64_t base = (int64_t)bk.tile_base * tb.tile, n = x ? g.nS : g.nR;
-                for (int64_t v = tid; v < n; v += 256) put(base + v);
-                continue;
-            }
-            const uint32_t K = (bk.L + (uint32_t)tb.tile - 1) / (uint32_t)tb.tile;
-            for (uint32_t i = (uint32_t)wave; i < K; i += 4) {
-                const int64_t id = (int64_t)bk.tile_base + i;
-                const uint32_t lo = tb.offs[id * kOffsB + g.b0], hi = tb.offs[id * kOffsB + g.b1];
-                for (uint32_t o = lo + (uint32_t)lane; o < hi; o += 64) put(id * tb.tile + o);
-            }
-        }
-    }
+    const uint32_t ns = p.plan->nsingle, nb = p.plan->nbig;
+    for (uint32_t e = blockIdx.x; e < ns + nb; e += gridDim.x)
+        unpack_group<256>(p, p.groups[e < ns ? p.single_list[e] : p.big_list[e - ns]]);
+}
+
+hipError_t launch_msd_unpack_groups(const MsdFinalParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(msd_unpack_groups_kernel, dim3(kUnpackGrid), dim3(256), 0, s, p);
+    return hipGetLastError();
 }
 
 // groups of the wide list (key range over 22 bits, or a bucket with more than
 // kFinThreads pass-B tiles): the generic 64-bit path, persistent over the list
 template <int C1, int C2>
-__global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const MsdFinalParams p) {
+__global__ __launch_bounds__(kMsdThreads, 2) void msd_final_wide_kernel(const MsdFinalParams p_in) {
     __shared__ FinalSmem sm;
-    if (msd_plan_failed(p.plan)) return;
-    if (p.pk_mode >= 0 && (int)(p.plan->packB != 0u) != p.pk_mode) return;  // the other layout's launch
+    if (msd_plan_failed(p_in.plan)) return;
+    const MsdFinalParams p = rows_view(p_in);  // (its groups come from the radix list: unpacked there)
     const uint32_t nw = p.plan->nwide;
     for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
         final_group<C1, C2>(p, p.wide_list[i], sm);
@@ -5134,7 +5174,7 @@ int msd_packb_mode() {
     return SMJ_PB_PIPE && m >= 0 && m <= 2 ? m : 0;
 }
 
-hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_tiles, hipStream_t s) {
+hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_tiles, hipStream_t s, bool pb_pack) {
     if (max_tiles <= 0) return hipSuccess;
     static const int dbg = getenv("SMJ_DEBUG_MSD") ? atoi(getenv("SMJ_DEBUG_MSD")) : 0;
     MsdPartBParams p = p_in;
@@ -5147,9 +5187,9 @@ hipError_t launch_msd_part_b(const MsdPartBParams &p_in, int cols, int64_t max_t
         if (C == 2 && SMJ_PB_PIPE) {
             const unsigned gp = (unsigned)std::min<int64_t>(
                 max_tiles, resident_blocks(msd_part_b_pipe_kernel<2>, pb_threads(2), pad));
-            // rows or packed words (MsdPlan::packB, known on the device only): the other returns at once
-            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, false>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
-            hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, true>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
+            // rows, or packed words when MsdPlan::packB (known on the device only)
+            if (pb_pack) hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, 2>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
+            else hipLaunchKernelGGL((msd_part_b_pipe_kernel<2, 0>), dim3(gp), dim3(pb_threads(2)), pad, s, p);
         } else {
             hipLaunchKernelGGL((msd_part_b_kernel<C>), dim3(grid), dim3(pb_threads(C)), pad, s, p);
         }
@@ -5191,27 +5231,17 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
         // rows or packed words in tempB (MsdPlan::packB, set on the device):
         // both layouts' launches go in, the other returns at entry
         if (p.combined) {
-            hipLaunchKernelGGL((msd_final_stage_kernel<true, false>), dim3(sg), dim3(kStThreads), pad, s, p);
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<true, true>), dim3(sg), dim3(kStThreads), pad, s, p);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<true, 2>), dim3(sg), dim3(kStThreads), pad, s, p);
+            else hipLaunchKernelGGL((msd_final_stage_kernel<true, 0>), dim3(sg), dim3(kStThreads), pad, s, p);
         } else {
-            hipLaunchKernelGGL((msd_final_stage_kernel<false, false>), dim3(sg), dim3(kStThreads), pad, s, p);
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, true>), dim3(sg), dim3(kStThreads), pad, s, p);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, 2>), dim3(sg), dim3(kStThreads), pad, s, p);
+            else hipLaunchKernelGGL((msd_final_stage_kernel<false, 0>), dim3(sg), dim3(kStThreads), pad, s, p);
         }
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
-        if (p.shadow[0]) {  // packed: the other tiers' groups as rows in the shadow, then those tiers on it
-            hipLaunchKernelGGL(msd_unpack_groups_kernel, dim3(kUnpackGrid), dim3(256), 0, s, p);
-            q.pk_mode = 0;
-        }
-        for (int m = 0; m < (p.shadow[0] ? 2 : 1); m++) {
-            if (m == 1) {
-                q.pk_mode = 1;
-                for (int x = 0; x < 2; x++) q.tab[x].tempB = p.shadow[x];
-            }
-            q.radix_list = p.radix_list;
-            hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
-            q.radix_list = nullptr;
-            hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
-        }
+        q.pk_mode = p.shadow[0] ? 2 : -1;  // packed rows possible: the tiers unpack / read the shadow on the device
+        hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
+        q.radix_list = nullptr;
+        hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
     } else {
         MsdFinalParams q = p;
         q.radix_list = nullptr;  // contiguous mode

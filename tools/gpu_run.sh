@@ -58,6 +58,7 @@ for s in $STEPS; do
     pkt)   test_run pkt 600 $PYT tests/test_gpu_msd.py -k packed_pass_b ;;
     msdpk2) SMJ_PACKB=2 test_run msdpk2 600 $PYT tests/test_gpu_msd.py ;;
     msdpk0) SMJ_PACKB=0 test_run msdpk0 600 $PYT tests/test_gpu_msd.py ;;
+    largepk2) SMJ_PACKB=2 test_run largepk2 900 $PYT tests/test_gpu_large.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
@@ -136,6 +137,18 @@ for s in $STEPS; do
              SMJ_PACKB=0 run c4pk0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4pk0_$r.out" c4_rows
              run c5pk1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5pk1_$r.out" c5_packb
              SMJ_PACKB=0 run c5pk0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5pk0_$r.out" c5_rows
+           done ;;
+    abpkr) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # packed pass-B rows: runtime-branch kernels vs dual launches vs rows
+           for r in 1 2; do
+             run c3r_$r 300 python bench.py $NOCPU && summ "$OUT/c3r_$r.out" c3_pk_runtime
+             SMJ_LIB=$V/pkdual/libsmj_hip.so run c3d_$r 300 python bench.py $NOCPU && summ "$OUT/c3d_$r.out" c3_pk_dual
+             SMJ_PACKB=0 run c3o_$r 300 python bench.py $NOCPU && summ "$OUT/c3o_$r.out" c3_rows
+           done
+           for r in 1 2; do
+             run c4r_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4r_$r.out" c4_pk_runtime
+             SMJ_PACKB=0 run c4o_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4o_$r.out" c4_rows
+             run c5r_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5r_$r.out" c5_pk_runtime
+             SMJ_PACKB=0 run c5o_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5o_$r.out" c5_rows
            done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
