@@ -150,6 +150,16 @@ for s in $STEPS; do
              run c5r_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5r_$r.out" c5_pk_runtime
              SMJ_PACKB=0 run c5o_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5o_$r.out" c5_rows
            done ;;
+    abpka) for r in 1 2; do  # same-box A/B of packed pass-A tiles (SMJ_PACKA)
+             run c3a1_$r 300 python bench.py $NOCPU && summ "$OUT/c3a1_$r.out" c3_packa
+             SMJ_PACKA=0 run c3a0_$r 300 python bench.py $NOCPU && summ "$OUT/c3a0_$r.out" c3_rowsa
+           done
+           for r in 1 2; do
+             run c4a1_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4a1_$r.out" c4_packa
+             SMJ_PACKA=0 run c4a0_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4a0_$r.out" c4_rowsa
+             run c5a1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a1_$r.out" c5_packa
+             SMJ_PACKA=0 run c5a0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a0_$r.out" c5_rowsa
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
