@@ -449,18 +449,6 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
         mn = v ? min(mn, k) : mn;
         mx = v ? max(mx, k) : mx;
     }
-    if constexpr (COLS == 2) {
-        if (p.nopack) {  // packed pass-B rows need the other column in int32 (MsdPlan::packB)
-            bool bad = false;
-#pragma unroll
-            for (int it = 0; it < ITEMS; it++) {
-                const int64_t o = rows[it][1 - p.key_col];
-                bad = bad || (((vmask >> it) & 1u) && (int64_t)(int32_t)o != o);
-            }
-            const uint64_t bm = __ballot(bad);
-            if (bm && lane == __builtin_ctzll(bm)) atomicOr(p.nopack, 1u);
-        }
-    }
     wave_rank<ITEMS, kBitsA>(dig, vmask, wc, lane);
     __syncthreads();
     const uint32_t total = tile_digit_starts<RADIX, NT>(s_wcnt, s_bin, s_wsum);
@@ -473,6 +461,19 @@ __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_p
 #pragma unroll
     for (int it = 0; it < ITEMS; it++)
         if ((vmask >> it) & 1u) store_row<COLS>(s_rows + (size_t)dig[it] * COLS, rows[it]);
+    // (after the staging stores: off the loads -> ranks chain)
+    if constexpr (COLS == 2) {
+        if (p.nopack) {  // packed pass-B rows need the other column in int32 (MsdPlan::packB)
+            bool bad = false;
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const int64_t o = rows[it][1 - p.key_col];
+                bad = bad || (((vmask >> it) & 1u) && (int64_t)(int32_t)o != o);
+            }
+            const uint64_t bm = __ballot(bad);
+            if (bm && lane == __builtin_ctzll(bm)) atomicOr(p.nopack, 1u);
+        }
+    }
     static_assert(RADIX < kOffsARow, "the offsA row holds the starts and the count");
     for (int i = tid; i <= RADIX; i += NT) p.offs[t * kOffsARow + i] = s_bin[i];  // s_bin[RADIX] = the tile's selected rows
     if (tid == 0) {

@@ -160,6 +160,11 @@ for s in $STEPS; do
              run c5a1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a1_$r.out" c5_packa
              SMJ_PACKA=0 run c5a0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a0_$r.out" c5_rowsa
            done ;;
+    abhv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # working tree vs the HEAD build (headv), C3, three rounds
+           for r in 1 2 3; do
+             run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
@@ -189,6 +194,11 @@ for s in $STEPS; do
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
                python3 "$ROOT/bench.py" --steps 10 --warmup 2 $NOCPU
            rm -f "$OUT/prof/c3_kernel_trace.csv" ;;
+    prof4pk) for m in 2 1; do  # C4 kernel stats with the parts' pass-B rows packed (2) / not (1)
+               SMJ_PACKB=$m run prof4pk$m 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4pk$m" -o c4 -- \
+                 python3 "$ROOT/bench.py" --workload c4 --steps 3 --warmup 1 $NOCPU
+               rm -f "$OUT/prof4pk$m/c4_kernel_trace.csv"
+             done ;;
     prof5) run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o c5 -- \
                python3 "$ROOT/bench.py" --workload c5 --steps 2 --warmup 1 $NOCPU
            rm -f "$OUT/prof5/c5_kernel_trace.csv" ;;
