@@ -165,6 +165,13 @@ for s in $STEPS; do
              run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
              SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
            done ;;
+    abst)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # staged-kernel grid / record-ring variants, C3
+           for r in 1 2 3; do
+             run st0_$r 300 python bench.py $NOCPU && summ "$OUT/st0_$r.out" c3_grid768
+             for n in stg1024 stg1536 strec8; do
+               SMJ_LIB=$V/$n/libsmj_hip.so run ${n}_$r 300 python bench.py $NOCPU && summ "$OUT/${n}_$r.out" c3_$n
+             done
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
