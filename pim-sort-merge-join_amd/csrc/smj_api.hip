@@ -638,11 +638,6 @@ struct MsdIn {            // one input table of the pipeline
     int64_t ntiles = 0;
     int pk = 0;                      // packed input (MsdTable::pk): one word per row, cols == 2, no select
     int64_t pkk = 0, pkp = 0;
-    // a part of the partitioned mode (msd_large): its pass-B rows stay 16-B
-    // rows -- packed ones ran C4 0.6-2 ms/step slower (the staged kernel's
-    // packed gathers +1 ms over its 20 parts, part_a's int32 check +0.5 ms
-    // against part_b -1.4 ms; profiles/r05/r05zy)
-    int part = 0;
 };
 
 // Records the index of the last profiling record (to patch its byte count
@@ -960,7 +955,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
     SMJ_TRY(msd_scratch(&ms));
     // packed pass-B rows (MsdPlan::packB; decided on the device from the data)
     int pack_mode = msd_packb_mode();  // 0 off, 1 unskewed tables, 2 forced (tests)
-    for (int x = 0; x < ntab; x++) pack_mode = in[x].cols == 2 && (!in[x].part || pack_mode == 2) ? pack_mode : 0;
+    for (int x = 0; x < ntab; x++) pack_mode = in[x].cols == 2 ? pack_mode : 0;
     const bool pack_ok = pack_mode != 0;
     int T_[2] = {1, 1}, TB_[2] = {1, 1};  // pass-A / pass-B tile rows
     int64_t tilesA[2] = {0, 0}, maxB[2] = {0, 0};
@@ -1773,7 +1768,6 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
             const T *src = staged ? (const T *)ms->pst[x] + roff[x][p] * in[x].cols : base;
             part[np++] = MsdIn{src, cnt[x][p], in[x].cols, 0, 0, in[x].key, 0, base};
         }
-        for (int i = 0; i < np; i++) part[i].part = 1;
         all_joined &= np == 2;
     }
     if (all_joined && !g_prof_on && msd_overlap_on()) {

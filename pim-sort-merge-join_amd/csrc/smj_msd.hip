@@ -3363,19 +3363,17 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
             const uint32_t vt = v - (x ? L.sp : 0u);  // table row
             if (ST_ABL(4)) {
                 const int64_t kk = g.base + (int64_t)((v * 3u) % max(g.span, 1u));
-                r = {p.tab[x].key ? (int64_t)v : kk, p.tab[x].key ? kk : (int64_t)v};
+                if (PK) r = {(int64_t)((uint64_t)(uint32_t)kk | ((uint64_t)v << 32)), 0};
+                else r = {p.tab[x].key ? (int64_t)v : kk, p.tab[x].key ? kk : (int64_t)v};
             } else {
                 int64_t ix = (int64_t)le.x + (vt - le.y);
                 if (SMJ_BOUNDS && (ix < 0 || ix >= p.tab[x].capB)) {
                     atomicOr(&p.plan->err, 2u);
                     ix = 0;
                 }
-                if constexpr (PK) {
-                    const uint64_t w = reinterpret_cast<const uint64_t *>(x ? p.tab[1].tempB : p.tab[0].tempB)[ix];
-                    const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
-                    const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
-                    const bool kc = (x ? p.tab[1].key : p.tab[0].key) != 0;
-                    r = {kc ? oth : key, kc ? key : oth};
+                if constexpr (PK) {  // the raw word: decoded where st_sort consumes it (a decode here
+                                     // would wait for the gather before this group's rows are written)
+                    r = {(int64_t)reinterpret_cast<const uint64_t *>(x ? p.tab[1].tempB : p.tab[0].tempB)[ix], 0};
                 } else {
                     r = (x ? tB1 : tB0)[ix];
                 }
@@ -3464,7 +3462,7 @@ __device__ __forceinline__ void st_lsd(uint32_t (&cur)[kStIt], uint32_t nR, uint
 
 // stage + counting sort of group g whose rows are in `rows`, then the zip
 // join lookups (mmask / part)
-template <bool COMB>
+template <bool COMB, bool PK>
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
@@ -3491,11 +3489,14 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
         if (L.valid(k, (uint32_t)v)) {
             const bool x = L.is_s(k, (uint32_t)v);
             const int kc = x ? kc1 : kc0;
-            sm.pay[v] = kc ? rows[k].x : rows[k].y;
+            // PK: rows[k].x is the packed word -- other column in its high half,
+            // the key's low 32 bits (residual from the group base: span <= kStRange)
+            sm.pay[v] = PK ? (int64_t)(int32_t)(uint32_t)((uint64_t)rows[k].x >> 32) : kc ? rows[k].x : rows[k].y;
             if (one) {
                 sm.key[v] = (uint32_t)v;
             } else {
-                const uint32_t res = (uint32_t)((uint64_t)st_key(rows[k], kc) - (uint64_t)g.base);
+                const uint32_t res = PK ? (uint32_t)rows[k].x - (uint32_t)g.base
+                                        : (uint32_t)((uint64_t)st_key(rows[k], kc) - (uint64_t)g.base);
                 const uint32_t sh = 16u * (res & 1u);
                 w[k] = (res << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][res >> 1], 1u << sh) >> sh) & 0xffffu);
             }
@@ -3859,7 +3860,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
         uint32_t mmask = 0, part[kStIt];
         uint32_t nex;  // the next group's run-length prefix, scanned with this group's bins
         uint32_t mex = 0;  // this thread's exclusive prefix of join rows within its wave (SMJ_ST_FOLDSCAN)
-        const bool ok = st_sort<COMB>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex, mex);  // cur is staged in LDS here
+        const bool ok = st_sort<COMB, PK>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex, mex);  // cur is staged in LDS here
         FIN_STAMP(2);
         // st_issue_lists writes only the list region (unused by the sort; its
         // start bitmap was zeroed, and its run lengths scanned, inside

@@ -172,6 +172,21 @@ for s in $STEPS; do
                SMJ_LIB=$V/$n/libsmj_hip.so run ${n}_$r 300 python bench.py $NOCPU && summ "$OUT/${n}_$r.out" c3_$n
              done
            done ;;
+    abdef) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # deferred packed-word decode vs HEAD (headv); C4 with packed parts too
+           for r in 1 2 3; do
+             run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
+           done
+           for r in 1 2; do
+             SMJ_PACKB=2 run c4n2_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4n2_$r.out" c4_new_packedparts
+             run c4n_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4n_$r.out" c4_new
+           done ;;
+    abc5l) for r in 1 2; do  # C5 and the loopback line: packed pass-B rows allowed (default) vs off
+             run c5d_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5d_$r.out" c5_default
+             SMJ_PACKB=0 run c5o_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5o_$r.out" c5_packb0
+             run lpd_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpd_$r.out" loop_default
+             SMJ_PACKB=0 run lpo_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpo_$r.out" loop_packb0
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
@@ -248,6 +263,9 @@ for s in $STEPS; do
     pmclist) run pmclist 60 rocprofv3 -L ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
+    finv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # phases (stamps build) + ablation (ablate build) on HEAD
+           SMJ_LIB=$V/stamps/libsmj_hip.so run phasesv 300 python tools/msd_phases.py && \
+           SMJ_LIB=$V/ablate/libsmj_hip.so run finabv 300 python tools/final_ablate.py ;;
     pbab)  run pbab 300 python tools/pb_ablate.py ;;
     t:*)   # t:FILE[:KEXPR] -- one test file, optionally filtered by -k (underscores kept, '+' = space)
            spec=${s#t:}; f=${spec%%:*}; k=""; [ "$spec" != "$f" ] && k=${spec#*:}
