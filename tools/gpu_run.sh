@@ -187,6 +187,13 @@ for s in $STEPS; do
              run lpd_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpd_$r.out" loop_default
              SMJ_PACKB=0 run lpo_$r 300 python bench.py --loopback $NOCPU && summ "$OUT/lpo_$r.out" loop_packb0
            done ;;
+    abearly) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # equal-key rounds: early exit (default) vs all fl rounds
+           for r in 1 2 3; do
+             run c3e_$r 300 python bench.py $NOCPU && summ "$OUT/c3e_$r.out" c3_early
+             SMJ_LIB=$V/noearly/libsmj_hip.so run c3f_$r 300 python bench.py $NOCPU && summ "$OUT/c3f_$r.out" c3_allrounds
+           done
+           run c5e 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5e.out" c5_early
+           SMJ_LIB=$V/noearly/libsmj_hip.so run c5f 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5f.out" c5_allrounds ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
