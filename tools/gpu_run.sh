@@ -194,6 +194,15 @@ for s in $STEPS; do
            done
            run c5e 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5e.out" c5_early
            SMJ_LIB=$V/noearly/libsmj_hip.so run c5f 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5f.out" c5_allrounds ;;
+    abei)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # early issue of the next group's gathers vs HEAD (headv)
+           for r in 1 2 3; do
+             run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
+           done
+           for r in 1 2; do
+             run c4n_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4n_$r.out" c4_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c4h_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4h_$r.out" c4_head
+           done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
              run c3new_$r 300 python bench.py $NOCPU && summ "$OUT/c3new_$r.out" c3_new
