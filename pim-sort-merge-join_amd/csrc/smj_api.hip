@@ -745,6 +745,10 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
         SMJ_TRY(grow(&ms->gmap, &ms->c_gmap, (size_t)(njobs + 1) * 4));
         SMJ_TRY(grow(&ms->gh, &ms->c_gh, (size_t)(njobs + 1) * 2 * kStageRange * 4));
         MsdFinalParams fb = fp;
+        if (fp.pk_mode == 3) {  // packed pass-B rows: the unpacked copy of the oversized groups
+            for (int x = 0; x < ntab; x++) fb.tab[x].tempB = fp.shadow[x];
+            fb.pk_mode = -1;
+        }
         fb.giant = (uint4 *)ms->giant;
         fb.gmap = (uint32_t *)ms->gmap;
         fb.gh = (uint32_t *)ms->gh;
@@ -832,7 +836,9 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
             SMJ_TRY(grow(&ts.fb2, &ts.c_fb2, (size_t)tot[x] * in[x].cols * 8));
             {
                 ProfScope ps("msd_big", 16.0 * in[x].cols * tot[x], s);
-                HIP_TRY(launch_msd_gather_list(fp.tab[x], ms->groups, dw + at[x], (int64_t)gw[x].size(),
+                MsdTab tbx = fp.tab[x];  // packed pass-B rows: the unpacked copy (oversized groups)
+                if (fp.pk_mode == 3) tbx.tempB = fp.shadow[x];
+                HIP_TRY(launch_msd_gather_list(tbx, ms->groups, dw + at[x], (int64_t)gw[x].size(),
                                                (int64_t *)ts.fb, s));
             }
             int64_t m = 0;
@@ -1258,12 +1264,10 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
         g_msd_packb = ms->h_plan->packB;
     }
     bool redo = false;
-    MsdFinalParams ff = fp;  // the host-launched tiers read 16-B rows: the shadow when pass-B rows were packed
-    if (ms->h_plan->packB) {
-        if (ms->h_plan->nsingle + ms->h_plan->nbig) HIP_TRY(launch_msd_unpack_groups(fp, s));
-        for (int x = 0; x < ntab; x++) ff.tab[x].tempB = fp.shadow[x];
-        ff.pk_mode = -1;
-    }
+    MsdFinalParams ff = fp;  // packed pass-B rows: the single-key tier reads the words (pk_mode 3), the
+                             // others read the shadow, which the unpack kernel fills for the oversized groups
+    ff.pk_mode = ms->h_plan->packB ? 3 : -1;
+    if (ms->h_plan->packB && ms->h_plan->nbig) HIP_TRY(launch_msd_unpack_groups(fp, s));
     SMJ_TRY(msd_fallback(ms, in, ntab, join, ff, out_j, s, &redo));
     if (redo) {
         SMJ_TRY(compact(1));

@@ -1031,6 +1031,9 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
 
 // one workgroup of kOffsA threads: thread = bucket.  Bucket sizes / bases of
 // both tables, the global key range, and the pass-B digit of every bucket.
+#ifndef SMJ_PACK_HEAVY
+#define SMJ_PACK_HEAVY 0  // 1: packed pass-B rows with heavy keys too (C5 +1.7 ms, r05zzp; the single-key tier reads words)
+#endif
 constexpr int kBasesWaves = kOffsA / 64;
 __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams p) {
     __shared__ uint32_t s_wsum[kBasesWaves];
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     const bool hv = a < kBucketsA && ((p.nheavy && p.nheavy[a] != 0u) || (a + 1 < kSplA && p.spl[a] == p.spl[a + 1]));
     const bool any_heavy = __syncthreads_or(hv) != 0;
     if (a == 0)
-        p.plan->packB = p.pack_ok && p.plan->nopack == 0u && (p.pack_ok == 2 || !any_heavy) && mn <= mx &&
+        p.plan->packB = p.pack_ok && p.plan->nopack == 0u && (p.pack_ok == 2 || !any_heavy || SMJ_PACK_HEAVY) && mn <= mx &&
                                 (uint64_t)mx - (uint64_t)mn < (1ull << 32)
                             ? 1u : 0u;
     // rows of bucket a per table
@@ -3910,9 +3913,9 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
 constexpr int kUnpackGrid = 1024;
 __global__ __launch_bounds__(256) void msd_unpack_groups_kernel(const MsdFinalParams p) {
     if (msd_plan_failed(p.plan) || p.plan->packB == 0u) return;
-    const uint32_t ns = p.plan->nsingle, nb = p.plan->nbig;
-    for (uint32_t e = blockIdx.x; e < ns + nb; e += gridDim.x)
-        unpack_group<256>(p, p.groups[e < ns ? p.single_list[e] : p.big_list[e - ns]]);
+    // (the single-key tier reads the packed words itself: MsdFinalParams::pk_mode 3)
+    const uint32_t nb = p.plan->nbig;
+    for (uint32_t e = blockIdx.x; e < nb; e += gridDim.x) unpack_group<256>(p, p.groups[p.big_list[e]]);
 }
 
 hipError_t launch_msd_unpack_groups(const MsdFinalParams &p, hipStream_t s) {
@@ -4632,7 +4635,19 @@ hipError_t read_msd_phases(unsigned long long *out16) {
 // ---------------------------------------------------------------------------
 // single-key oversized groups: already in stable order; copy and zip
 // ---------------------------------------------------------------------------
-// grid = work items (dense group, chunk of kGroupCap group rows)
+// row ix of table tb's pass-B rows: a packed word (MsdPlan::packB, pk) rebuilt
+// from group g's base, or the 16-B row
+__device__ __forceinline__ i64x2 pb_row(const MsdTab &tb, const MsdGroup &g, int64_t ix, bool pk) {
+    if (!pk) return reinterpret_cast<const i64x2 *>(tb.tempB)[ix];
+    const uint64_t w = reinterpret_cast<const uint64_t *>(tb.tempB)[ix];
+    const int64_t key = g.base + (int64_t)(uint32_t)((uint32_t)w - (uint32_t)g.base);
+    const int64_t oth = (int64_t)(int32_t)(uint32_t)(w >> 32);
+    return tb.key ? i64x2{oth, key} : i64x2{key, oth};
+}
+
+// grid = work items (dense group, chunk of kGroupCap group rows).  With
+// p.pk_mode == 3 the pass-B rows are packed words (2-column tables), read
+// and rebuilt here (no unpacked copy for this tier)
 template <int C1, int C2>
 __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalParams p, const uint2 *work) {
     __shared__ uint64_t s_tmp[kGroupCap];
@@ -4685,7 +4700,9 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
                     const uint2 e = s_run[j];
                     const uint32_t r0 = e.y < V0 ? V0 - e.y : 0u, r1 = min(s_len[j], V1 > e.y ? V1 - e.y : 0u);
                     for (uint32_t r = r0 + (uint32_t)lane; r < r1; r += 64) {
-                        if constexpr (C1 > 0) {
+                        if constexpr (C1 == 2 && C2 == 2) {
+                            reinterpret_cast<i64x2 *>(dst)[e.y + r] = pb_row(tb, g, (int64_t)(e.x + r), p.pk_mode == 3);
+                        } else if constexpr (C1 > 0) {
                             if (x) copy_row<C2>(tb.tempB + (int64_t)(e.x + r) * C2, dst + (int64_t)(e.y + r) * C2, C2);
                             else copy_row<C1>(tb.tempB + (int64_t)(e.x + r) * C1, dst + (int64_t)(e.y + r) * C1, C1);
                         } else {
@@ -4729,7 +4746,9 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
         int64_t *dst = tb.out + (int64_t)(x ? g.outS : g.outR) * cols;
         for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads) {
             const uint32_t src = s_addr[x][v - V0];
-            if constexpr (C1 > 0) {
+            if constexpr (C1 == 2 && C2 == 2) {
+                reinterpret_cast<i64x2 *>(dst)[v] = pb_row(tb, g, (int64_t)src, p.pk_mode == 3);
+            } else if constexpr (C1 > 0) {
                 if (x) copy_row<C2>(tb.tempB + (int64_t)src * C2, dst + (int64_t)v * C2, C2);
                 else copy_row<C1>(tb.tempB + (int64_t)src * C1, dst + (int64_t)v * C1, C1);
             } else {
@@ -4743,10 +4762,22 @@ __global__ __launch_bounds__(kMsdThreads) void msd_single_kernel(const MsdFinalP
     const uint32_t V1 = min(V0 + (uint32_t)kGroupCap, m);
     const int c1 = C1 > 0 ? C1 : p.tab[0].cols, c2 = C2 > 0 ? C2 : p.tab[1].cols, tc = c1 + c2 - 1;
     int64_t *dst = p.slots + (int64_t)g.outR * tc;
-    for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads)
+    for (uint32_t v = V0 + tid; v < V1; v += kMsdThreads) {
+        if constexpr (C1 == 2 && C2 == 2) {
+            if (p.pk_mode == 3) {  // packed rows: rebuilt (emit_join_row's 2-column layout)
+                const i64x2 rv = pb_row(p.tab[0], g, (int64_t)s_addr[0][v - V0], true);
+                const i64x2 sv = pb_row(p.tab[1], g, (int64_t)s_addr[1][v - V0], true);
+                int64_t *d = dst + (int64_t)v * tc;
+                d[0] = rv.x;
+                d[1] = rv.y;
+                d[2] = p.key2 ? sv.x : sv.y;
+                continue;
+            }
+        }
         emit_join_row<C1, C2>(p.tab[0].tempB + (int64_t)s_addr[0][v - V0] * c1,
                               p.tab[1].tempB + (int64_t)s_addr[1][v - V0] * c2, dst + (int64_t)v * tc, c1, c2,
                               p.key2);
+    }
 }
 
 // Batched fallback for oversized multi-key groups (smj_api.hip msd_fallback):

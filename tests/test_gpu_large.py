@@ -294,7 +294,9 @@ def test_repeated_partitioned_calls_agree(gpu):
     fresh repetition of itself by the order-sensitive digest of all three
     outputs (r05f-r05j: a racy staged-kernel change showed up here as a wrong
     join count and inconsistent run metadata, tools/seq_sizes.py)."""
-    from smj import ops
+    from smj import _lib, ops
+    _lib.load().smj_finalize()  # the earlier tests' scratch back to the device (this test reuses its own)
+    torch.cuda.empty_cache()
     ref = {}
     for n, prof in ((292_000_000, False), (559_000_000, False), (292_000_000, True), (559_000_000, True),
                     (559_000_000, True)):

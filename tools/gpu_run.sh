@@ -59,6 +59,7 @@ for s in $STEPS; do
     msdpk2) SMJ_PACKB=2 test_run msdpk2 600 $PYT tests/test_gpu_msd.py ;;
     msdpk0) SMJ_PACKB=0 test_run msdpk0 600 $PYT tests/test_gpu_msd.py ;;
     largepk2) SMJ_PACKB=2 test_run largepk2 900 $PYT tests/test_gpu_large.py ;;
+    largeh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so test_run largeh 900 $PYT tests/test_gpu_large.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
@@ -202,6 +203,22 @@ for s in $STEPS; do
            for r in 1 2; do
              run c4n_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4n_$r.out" c4_new
              SMJ_LIB=$V/headv/libsmj_hip.so run c4h_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4h_$r.out" c4_head
+           done ;;
+    abph)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # packed pass-B rows with heavy keys (C5) vs HEAD (headv)
+           for r in 1 2; do
+             run c5n_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5n_$r.out" c5_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c5h_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5h_$r.out" c5_head
+           done
+           run c3n 300 python bench.py $NOCPU && summ "$OUT/c3n.out" c3_new
+           SMJ_LIB=$V/headv/libsmj_hip.so run c3h 300 python bench.py $NOCPU && summ "$OUT/c3h.out" c3_head ;;
+    abph2) V=$ROOT/pim-sort-merge-join_amd/lib/variants  # working tree vs HEAD (headv): C3 x3, C5 x2
+           for r in 1 2 3; do
+             run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
+           done
+           for r in 1 2; do
+             run c5n_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5n_$r.out" c5_new
+             SMJ_LIB=$V/headv/libsmj_hip.so run c5h_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5h_$r.out" c5_head
            done ;;
     abbase) V=$ROOT/pim-sort-merge-join_amd/lib/variants/base/libsmj_hip.so
            for r in 1 2 3; do
