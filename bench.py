@@ -18,7 +18,10 @@ of the previous stage (smj/dist.py).
 value = (|R| + |S| over all ranks) / max-over-ranks seconds per step.
 
 --workload c4 / c5 times the other BASELINE tables: C4's 1e9 x 1e9 uniform
-tables (configs[3]), C5's 1e8 x 1e9 Zipf(0.9) tables (configs[4]).  On one GPU
+tables (configs[3]), C5's 1e8 x 1e9 Zipf(0.9) tables (configs[4]); --workload
+c3w SURVEY 8(d)'s C3-wide stress input (C3's sizes, full-range signed int64
+keys, S planted with R's keys in a random third of its rows, WHERE col0 >
+INT64_MIN so that every row passes).  On one GPU
 they run through the library's partitioned mode; under torchrun (or
 --loopback) they are STRONG-scaled: the job's tables are fixed and rank r
 generates its contiguous slice, global rows [r n / W, (r + 1) n / W) (row0 =
@@ -28,9 +31,9 @@ depend on W), then the range partition + RCCL exchange of smj/dist.py.
 Every line carries "verified" (after the timed steps, outside them): under
 torchrun / --loopback each rank digests its slice of the joined rows at its
 global position (smj_dev_digest, order-sensitive) and rank 0 compares them with
-the single-GPU call on the whole job's tables; at N = 1 the timed step's sorted
-tables and joined rows are compared with the CPU port's (oracle/cpu_mt.cpp, the
-cpu_baseline_mt leg).  A mismatch prints the line with "verified": false and
+the single-GPU call on the whole job's tables; at N = 1 (every workload) the
+timed step's sorted tables and joined rows are compared with the CPU port's
+(oracle/cpu_mt.cpp on the full tables, the cpu_baseline_mt leg).  A mismatch prints the line with "verified": false and
 exits 3 on every rank.
 """
 import argparse
@@ -50,6 +53,7 @@ from smj import dist as sdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SELECT = (0, 5000, 0, 5000)    # user.h SELECT_COL1/VAL1, SELECT_COL2/VAL2
+SELECT_WIDE = (0, -(1 << 63), 0, -(1 << 63))  # C3-wide: WHERE col0 > INT64_MIN (~every row)
 KEYS = (0, 0)                  # user.h JOIN_KEY1/2
 METRIC = "joined rows/sec on |R|=|S|=1e8 int64-key tables; achieved HBM GB/s vs peak"
 
@@ -83,8 +87,9 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per table per GPU")
-    p.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
-                   help="c3 (default, the metric's config); c4 / c5: BASELINE's 1e9-row tables on one GPU")
+    p.add_argument("--workload", default="c3", choices=["c3", "c3w", "c4", "c5"],
+                   help="c3 (default, the metric's config); c3w: C3-wide (full-range keys); "
+                        "c4 / c5: BASELINE's 1e9-row tables on one GPU")
     p.add_argument("--cpu-sample", type=int, default=196608,
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
     p.add_argument("--cpu-mt", type=int, default=1,
@@ -107,9 +112,12 @@ def parse():
 
 def workload_name(w, world, distributed):
     """config.workload: the BASELINE.json config the line measures."""
-    if w == "c3":
-        return ("C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, JOIN_KEY 0"
-                + ("; range partition + RCCL exchange, weak scaling (|R|=|S|=%d x 1e8)" % world if distributed else ""))
+    if w in ("c3", "c3w"):
+        head = ("C3 |R|=|S|=1e8 per GPU, (int64 key, int64 payload), WHERE col0 > 5000, JOIN_KEY 0" if w == "c3" else
+                "C3-wide (SURVEY 8(d) stress input) |R|=|S|=1e8 per GPU, full-range signed int64 keys, S planted "
+                "with R's keys in a random third of its rows, WHERE col0 > INT64_MIN, JOIN_KEY 0")
+        return head + ("; range partition + RCCL exchange, weak scaling (|R|=|S|=%d x 1e8)" % world
+                       if distributed else "")
     base = {"c4": "C4 (BASELINE configs[3]) 1B x 1B rows, uniform int64 keys in [1,3e9]",
             "c5": "C5 (BASELINE configs[4]) 100M x 1B rows, Zipf(0.9) keys over 1e8 values"}[w]
     if distributed:
@@ -180,7 +188,10 @@ def verify_distributed(J, rank, world, dev, full_tables, wire=None):
 
 
 def main():
+    global SELECT
     a = parse()
+    if a.workload == "c3w":
+        SELECT = SELECT_WIDE
     _claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -210,14 +221,14 @@ def main():
     distributed = world > 1 or a.loopback
 
     n = a.rows
-    strong = a.workload != "c3"  # C4 / C5: the job's tables are fixed (BASELINE configs[3], [4])
-    if a.workload == "c3":
+    strong = a.workload in ("c4", "c5")  # C4 / C5: the job's tables are fixed (BASELINE configs[3], [4])
+    if a.workload in ("c3", "c3w"):
         NR = NS = n * world       # weak: n rows per table per GPU
     elif a.workload == "c4":
         NR = NS = 1_000_000_000
     else:
         NR, NS = 100_000_000, 1_000_000_000
-    key_range = 3 * NR if a.workload != "c5" else 100_000_000  # C5: the Zipf domain
+    key_range = {"c5": 100_000_000, "c3w": None}.get(a.workload, 3 * NR)  # C5: the Zipf domain; c3w: 2^64
 
     def shard(N):  # this rank's contiguous slice of a table of N global rows
         if not strong:
@@ -229,6 +240,9 @@ def main():
     if a.workload == "c5":
         R = ops.gen_zipf(nr, row0=r0R, seed=3, domain=100_000_000, theta=0.9, device=dev)
         S = ops.gen_zipf(ns, row0=r0S, seed=4, domain=100_000_000, theta=0.9, device=dev)
+    elif a.workload == "c3w":
+        R = ops.gen_wide(nr, row0=r0R, seed=1, device=dev)
+        S = ops.gen_wide(ns, row0=r0S, seed=2, plant_seed=1, plant_rows=NR, device=dev)
     else:
         R = ops.gen_uniform(nr, row0=r0R, seed=1, key_range=key_range, device=dev)
         S = ops.gen_uniform(ns, row0=r0S, seed=2, key_range=key_range, device=dev)
@@ -292,6 +306,9 @@ def main():
     ops.prof_enable(False)
     progress(f"{a.steps} timed + {psteps} profiled steps done ({dt / a.steps * 1e3:.3f} ms/step)")
     prof = ops.prof_report()
+    # pass-B row layout of the last pipeline call (MsdPlan::packB: one 8-B word per
+    # row when the payload fits int32 and the selected keys span < 2^32, else 16-B rows)
+    packb = ops.msd_packb() if not distributed else None
     if world == 1:
         log(f"msd stats (single-key groups, LSD-fallback groups, mR, mS): {ops.msd_stats()}; "
             f"(groups, radix-tier, wide-tier, in-LDS LSD): {ops.msd_groups()}")
@@ -304,6 +321,9 @@ def main():
         if a.workload == "c5":
             return (ops.gen_zipf(NR, row0=0, seed=3, domain=100_000_000, theta=0.9, device=dev),
                     ops.gen_zipf(NS, row0=0, seed=4, domain=100_000_000, theta=0.9, device=dev))
+        if a.workload == "c3w":
+            return (ops.gen_wide(NR, row0=0, seed=1, device=dev),
+                    ops.gen_wide(NS, row0=0, seed=2, plant_seed=1, plant_rows=NR, device=dev))
         return (ops.gen_uniform(NR, row0=0, seed=1, key_range=key_range, device=dev),
                 ops.gen_uniform(NS, row0=0, seed=2, key_range=key_range, device=dev))
 
@@ -335,6 +355,8 @@ def main():
     dom = max((kv for kv in prof.items() if kv[1]["bytes"] > 0), key=lambda kv: kv[1]["ms"], default=(None, None))
     roof = None
     pmc = None
+    from smj._lib import source_sha as _source_sha
+    source_sha = _source_sha()
     # the PMC summary is per launch of ONE configuration (profiles/pmc_traffic.json:
     # the single-GPU C3 call): its bytes are attached only to a line timing the
     # same launches -- never to the dist / loopback stages (half-size launches)
@@ -343,6 +365,11 @@ def main():
         with open(a.pmc) as f:
             pmc = json.load(f)
         if pmc.get("rows_per_table") != n or pmc.get("workload", "c3") != a.workload:
+            pmc = None
+        elif pmc.get("source_sha") != source_sha:
+            # the summary was collected on another build of the library: its bytes
+            # may describe kernels that no longer exist
+            log(f"PMC summary {a.pmc}: source_sha {pmc.get('source_sha')} != this tree's {source_sha}: not attached")
             pmc = None
     if pmc and pmc.get("runs"):
         # ... and with the same launches per step (the partitioned mode's part
@@ -392,7 +419,7 @@ def main():
     pipe_gbs = b_alg / (dt / a.steps) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0 and a.workload == "c3":
+    if rank == 0 and world == 1 and a.cpu_sample > 0 and a.workload in ("c3", "c3w") and not distributed:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline leg only
         m = min(a.cpu_sample, n)
@@ -404,7 +431,8 @@ def main():
         # time extrapolated as (n / m)^2 from the measured sample
         full_s = secs * (n / m) ** 2
         cpu = {"value": round(2 * m / secs, 1), "unit": "rows/s", "cores": 1, "kind": kind,
-               "sample": f"first {m} rows of R and of S of this workload (keys in [1,{key_range}]); "
+               "sample": f"first {m} rows of R and of S of this workload "
+                         f"({'keys in [1,%d]' % key_range if key_range else 'full-range int64 keys'}); "
                          f"cpu_app.c select + O(n^2) insertion sort + zip join, 1 thread, gcc -O2; "
                          f"{secs:.2f} s, {jrows} joined rows",
                "n2_extrapolation": {"rows_per_table": n, "seconds": round(full_s, 1), "days": round(full_s / 86400, 2),
@@ -412,7 +440,7 @@ def main():
                                     "basis": f"measured {secs:.2f} s at {m} rows/table x ({n}/{m})^2"}}
 
     cpu_mt = None
-    if rank == 0 and world == 1 and a.cpu_mt and a.workload == "c3":
+    if rank == 0 and world == 1 and a.cpu_mt and not distributed:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline leg only
         # the host cores this process may use: the CPU share granted to this GPU's job
@@ -421,8 +449,8 @@ def main():
         threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or usable, usable)
         secs, rows, outs = oracle.mt_pipeline(R.cpu().numpy(), S.cpu().numpy(), SELECT, KEYS, threads,
                                               outputs=True)
-        cpu_mt = {"value": round(2 * n / secs, 1), "unit": "rows/s", "cores": threads, "kind": "port",
-                  "sample": f"the full workload ({n} x {n} rows): oracle/cpu_mt.cpp, cpu_app.c's select + "
+        cpu_mt = {"value": round(rows_step / secs, 1), "unit": "rows/s", "cores": threads, "kind": "port",
+                  "sample": f"the full workload ({NR} x {NS} rows): oracle/cpu_mt.cpp, cpu_app.c's select + "
                             f"stable sort + zip join on {threads} threads (the host cores granted to this GPU's "
                             f"job; {usable} usable, {os.cpu_count()} in the node) (chunk sort + merge rounds), g++ -O3; "
                             f"{secs:.2f} s, {rows[2]} joined rows"}
@@ -448,7 +476,12 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic: splitmix64 keys iid uniform in [1,3n], payload = global row index (generated on device)",
+            "data": {"c3w": "synthetic: splitmix64 full-range signed int64 keys, S planted with R's keys in a random "
+                            "third of its rows (smj_dev_gen_wide), payload = global row index (generated on device)",
+                     "c5": "synthetic: Zipf(0.9) keys over 1e8 values (smj_dev_gen_zipf), payload = global row index "
+                           "(generated on device)"}.get(
+                a.workload, "synthetic: splitmix64 keys iid uniform in [1,3n], payload = global row index "
+                            "(generated on device)"),
             "config": {"workload": workload_name(a.workload, world, distributed),
                        "rows_per_table_per_gpu": [nr, ns], "rows_per_table_total": [NR, NS],
                        "rank_input_rows": rank_rows, "key_range": key_range,
@@ -456,7 +489,10 @@ def main():
                                       + (" (REHEARSAL: gloo, ranks sharing GPUs; not a measurement)" if rehearse else ""),
                        "load_max_over_mean": round(lb.get("load_max_over_mean", 1.0), 4),
                        "rank_rows_after_exchange": lb.get("loads"),
-                       "exchange_stages": lb.get("stages", 0)},
+                       "exchange_stages": lb.get("stages", 0),
+                       "select": list(SELECT),
+                       "pass_b_layout": None if packb is None else ("packed 8-B words" if packb else "16-B rows"),
+                       "source_sha": source_sha},
             "roofline": roof,
             "pipeline_roofline": {"alg_bytes_per_step": b_alg, "achieved": round(pipe_gbs, 1),
                                   "peak": HBM_PEAK_GBS * world, "unit": "GB/s",

@@ -24,10 +24,11 @@
  *     range-partitioned on the key inside the library (in one pass into
  *     part regions of ~1.3-1.6x the table of library scratch when the device
  *     has room, else counted and scattered in place; the regions stay
- *     allocated for the next call until smj_finalize, and are released
- *     when they cannot all be had; two parts are in flight at once, on two
- *     library streams with two sets of per-part scratch, both kept until
- *     smj_finalize -- ~5 GB each at 1e9 x 1e9), tables over 8 columns
+ *     allocated for the next call until smj_trim / smj_finalize (or a
+ *     budget, smj_set_scratch_limit), and are released when they cannot all
+ *     be had; two parts are in flight at once, on two library streams with
+ *     two sets of per-part scratch, both kept the same way -- ~5 GB each at
+ *     1e9 x 1e9), tables over 8 columns
  *     are sorted as (key, row id) pairs and gathered; the
  *     LSD and partition entry points take 1..8 columns (else
  *     SMJ_ERR_UNSUPPORTED).
@@ -106,6 +107,20 @@ int smj_device_count(void);
 /* Replaces dpu_free(set) (include/dpu/dpu.h:189; app.c:307,402,503,761):
  * releases the device set and every library-owned buffer. */
 void smj_finalize(void);
+/* Returns every device buffer the library holds -- per-call scratch, the
+ * partitioned mode's part regions and second scratch set, the device set's
+ * staging buffers -- once the work on them has drained (it synchronises the
+ * devices).  The device set and its streams stay; the next call allocates
+ * again.  The per-phase dpu_free of the reference (app.c:307,402,503,761)
+ * without ending the set.  SMJ_ERR_INVALID while a
+ * smj_dev_sort_merge_join_begin job is open. */
+int smj_trim(void);
+/* Device bytes the library holds now (scratch of every kind). */
+int64_t smj_scratch_bytes(void);
+/* A byte budget: a pipeline call that ends with the library holding more
+ * than `bytes` trims (smj_trim) before it returns.  -1 (the default, or the
+ * environment's SMJ_SCRATCH_LIMIT): keep scratch for the next call. */
+void smj_set_scratch_limit(int64_t bytes);
 /* Version string of the library build. */
 const char *smj_version(void);
 
@@ -297,6 +312,16 @@ int smj_dev_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, in
                      double theta, double zeta_n, void *stream);
 /* sum_{i=1..n} i^-theta (host). */
 double smj_zipf_zeta(int64_t n, double theta);
+
+/* C3-wide (SURVEY 8(d) stress input): full-range signed int64 keys.  Row g's
+ * own key is (int64) h with h = splitmix64(g + seed * 0xD1B54A32D192ED03);
+ * when plant_rows > 0, a third of the rows (d = splitmix64(h ^
+ * 0x2545F4914F6CDD1D), mulhi(d, 3) == 0) instead take the key row
+ * r = mulhi(splitmix64(d), plant_rows) has in the table generated with
+ * plant_seed (R), so they join.  payload = g.  Identical to the oracle's
+ * smj_ref_gen_wide.  Async. */
+int smj_dev_gen_wide(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed,
+                     int64_t plant_rows, void *stream);
 
 /* Order-sensitive digest of a row-major table slice whose first row sits at
  * global position pos0:

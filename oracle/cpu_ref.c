@@ -340,3 +340,28 @@ void smj_ref_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t seed, int64_t
         out[2 * i + 1] = (T)g;
     }
 }
+
+/* C3-wide (SURVEY 8(d) stress input), the restatement of the device generator
+ * gen_wide_kernel (pim-sort-merge-join_amd/csrc/smj_kernels.hip, smj.h
+ * smj_dev_gen_wide): row g's own key is the full 64-bit splitmix64(g + seed *
+ * 0xD1B54A32D192ED03) read as a signed int64; with plant_rows > 0 a third of
+ * the rows (d = splitmix64(key ^ 0x2545F4914F6CDD1D), floor(3 d / 2^64) == 0)
+ * take the key of row floor(splitmix64(d) * plant_rows / 2^64) of the
+ * plant_seed table instead.  payload = g. */
+void smj_ref_gen_wide(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed, int64_t plant_rows)
+{
+    const uint64_t salt = seed * 0xD1B54A32D192ED03ULL, psalt = plant_seed * 0xD1B54A32D192ED03ULL;
+    for (int64_t i = 0; i < rows; i++) {
+        const uint64_t g = (uint64_t)(row0 + i);
+        uint64_t key = smj_ref_splitmix64(g + salt);
+        if (plant_rows > 0) {
+            const uint64_t d = smj_ref_splitmix64(key ^ 0x2545F4914F6CDD1DULL);
+            if ((uint64_t)(((unsigned __int128)d * 3u) >> 64) == 0) {
+                const uint64_t r = (uint64_t)(((unsigned __int128)smj_ref_splitmix64(d) * (uint64_t)plant_rows) >> 64);
+                key = smj_ref_splitmix64(r + psalt);
+            }
+        }
+        out[2 * i] = (T)(int64_t)key;
+        out[2 * i + 1] = (T)g;
+    }
+}

@@ -71,6 +71,8 @@ int64_t smj_ref_pipeline_csv(const char *path1, const char *path2, const char *o
                              int key1, int key2, int use_insertion, double *elapsed_ms);
 
 /* ---- synthetic tables (build-owned) ----------------------- */
+/* C3-wide synthetic keys (the device's smj_dev_gen_wide). */
+void smj_ref_gen_wide(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed, int64_t plant_rows);
 /* splitmix64 finaliser. */
 uint64_t smj_ref_splitmix64(uint64_t x);
 /* Fill rows [row0, row0 + rows) of a 2-column table (key, payload): the key of

@@ -67,6 +67,8 @@ def _bind(l, ktype):
     l.smj_ref_gen_uniform.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64]
     l.smj_ref_gen_zipf.restype = None
     l.smj_ref_gen_zipf.argtypes = [_P, _L, _L, ctypes.c_uint64, _L, ctypes.c_double, ctypes.c_double]
+    l.smj_ref_gen_wide.restype = None
+    l.smj_ref_gen_wide.argtypes = [_P, _L, _L, ctypes.c_uint64, ctypes.c_uint64, _L]
     l.smj_ref_digest.restype = ctypes.c_uint64
     l.smj_ref_digest.argtypes = [_P, _L, ctypes.c_int, _L]
     l.smj_ref_csv_size.restype = ctypes.c_int
@@ -143,6 +145,15 @@ def gen_uniform(rows, row0=0, seed=1, key_range=None):
         key_range = 3 * rows
     out = np.empty((rows, 2), dtype=np.int64)
     lib().smj_ref_gen_uniform(out.ctypes.data_as(_P), row0, rows, seed, key_range)
+    return out
+
+
+def gen_wide(rows, row0=0, seed=1, plant_seed=1, plant_rows=0):
+    """C3-wide keys: full-range signed int64; plant_rows > 0
+    plants R's keys (table plant_seed, plant_rows rows) in a random third of
+    the rows (smj_ref_gen_wide)."""
+    out = np.empty((rows, 2), dtype=np.int64)
+    lib().smj_ref_gen_wide(out.ctypes.data_as(_P), row0, rows, seed, plant_seed, plant_rows)
     return out
 
 

@@ -13,8 +13,10 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <new>
 #include <mutex>
@@ -218,13 +220,21 @@ int grow_host(void **p, size_t *cap, size_t need) {
     return SMJ_OK;
 }
 
+// smj_debug_fail_front: the next grow() of this thread fails with
+// SMJ_ERR_NOMEM (the partitioned mode's no-room path)
+thread_local bool t_fail_grow = false;
+
 int grow(void **p, size_t *cap, size_t need) {
+    if (t_fail_grow) {
+        t_fail_grow = false;
+        return SMJ_ERR_NOMEM;
+    }
     if (need <= *cap) return SMJ_OK;
-    if (*p) HIP_TRY(hipFree(*p));
+    if (*p) HIP_TRY(dev_free(*p));
     *p = nullptr;
     *cap = 0;
     size_t n = std::max(need, (size_t)1 << 20);
-    HIP_TRY(hipMalloc(p, n));
+    HIP_TRY(dev_alloc(p, n));
     *cap = n;
     return SMJ_OK;
 }
@@ -236,13 +246,13 @@ int scratch(DevScratch **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DevScratch &s = g_scratch[key];
     if (s.dev < 0) {
-        HIP_TRY(hipMalloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
-        HIP_TRY(hipMalloc(&s.plan, sizeof(SortPlan)));
-        HIP_TRY(hipMalloc(&s.ctr, sizeof(Counters) * 8));
+        HIP_TRY(dev_alloc(&s.hist, sizeof(uint32_t) * kNumPos * kRadix));
+        HIP_TRY(dev_alloc(&s.plan, sizeof(SortPlan)));
+        HIP_TRY(dev_alloc(&s.ctr, sizeof(Counters) * 8));
         HIP_TRY(hipMemset(s.ctr, 0, sizeof(Counters) * 8));
-        HIP_TRY(hipMalloc(&s.dcount, sizeof(int64_t) * 256));
-        HIP_TRY(hipMalloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
-        HIP_TRY(hipMalloc(&s.trash, sizeof(int64_t) * kSortThreads * 16));
+        HIP_TRY(dev_alloc(&s.dcount, sizeof(int64_t) * 256));
+        HIP_TRY(dev_alloc(&s.segsum, sizeof(uint32_t) * kScanSegs * kRadix));
+        HIP_TRY(dev_alloc(&s.trash, sizeof(int64_t) * kSortThreads * 16));
         HIP_TRY(hipHostMalloc(&s.h_plan, sizeof(SortPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&s.h_small, sizeof(int64_t) * 256, hipHostMallocDefault));
         s.dev = dev;  // only once every buffer exists
@@ -528,6 +538,7 @@ int64_t g_msd_stats[4] = {0, 0, 0, 0};  // last pipeline: single-key groups, LSD
 int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-tier, wide-tier, in-LDS LSD groups
 int64_t g_msd_bigdev = 0;                // last pipeline: oversized multi-key groups sorted on the device
 int64_t g_msd_packb = 0;                 // last pipeline: pass-B rows packed (MsdPlan::packB)
+int64_t g_msd_wstage = 0;                // last pipeline: groups the wide-span staged kernel took (MsdPlan::nwst)
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -555,26 +566,26 @@ int msd_scratch(MsdScratch **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     MsdScratch &m = g_msd[key];
     if (m.dev < 0) {
-        HIP_TRY(hipMalloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
-        HIP_TRY(hipMalloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
-        HIP_TRY(hipMalloc(&m.groups, sizeof(MsdGroup) * kSlots));
-        HIP_TRY(hipMalloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
-        HIP_TRY(hipMalloc(&m.ngrp, sizeof(uint32_t) * kOffsA));
-        HIP_TRY(hipMalloc(&m.cpart, sizeof(uint32_t) * 256));
-        HIP_TRY(hipMalloc(&m.counts, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.offs, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.single_list, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.big_list, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.wide_list, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.radix_list, sizeof(uint32_t) * kSlots));
-        HIP_TRY(hipMalloc(&m.plan, sizeof(MsdPlan)));
-        HIP_TRY(hipMalloc(&m.d_tmp, sizeof(int64_t) * 8));
-        HIP_TRY(hipMalloc(&m.lspl, sizeof(int64_t) * 64));
-        HIP_TRY(hipMalloc(&m.p1d, sizeof(int64_t) * 2 * kP1Words));
+        HIP_TRY(dev_alloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
+        HIP_TRY(dev_alloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
+        HIP_TRY(dev_alloc(&m.groups, sizeof(MsdGroup) * kSlots));
+        HIP_TRY(dev_alloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
+        HIP_TRY(dev_alloc(&m.ngrp, sizeof(uint32_t) * kOffsA));
+        HIP_TRY(dev_alloc(&m.cpart, sizeof(uint32_t) * 256));
+        HIP_TRY(dev_alloc(&m.counts, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.offs, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.single_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.big_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.wide_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.radix_list, sizeof(uint32_t) * kSlots));
+        HIP_TRY(dev_alloc(&m.plan, sizeof(MsdPlan)));
+        HIP_TRY(dev_alloc(&m.d_tmp, sizeof(int64_t) * 8));
+        HIP_TRY(dev_alloc(&m.lspl, sizeof(int64_t) * 64));
+        HIP_TRY(dev_alloc(&m.p1d, sizeof(int64_t) * 2 * kP1Words));
         HIP_TRY(hipHostMalloc(&m.p1h, sizeof(int64_t) * 2 * kP1Words, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&m.p1c, sizeof(uint32_t) * 2 * kP1cWords));
-        HIP_TRY(hipMalloc(&m.heavy, sizeof(int64_t) * kBucketsA * kHeavyMax));
-        HIP_TRY(hipMalloc(&m.nheavy, sizeof(uint32_t) * kBucketsA));
+        HIP_TRY(dev_alloc(&m.p1c, sizeof(uint32_t) * 2 * kP1cWords));
+        HIP_TRY(dev_alloc(&m.heavy, sizeof(int64_t) * kBucketsA * kHeavyMax));
+        HIP_TRY(dev_alloc(&m.nheavy, sizeof(uint32_t) * kBucketsA));
         HIP_TRY(hipHostMalloc(&m.h_p1c, sizeof(uint32_t) * 2 * kP1cWords, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
@@ -585,17 +596,19 @@ int msd_scratch(MsdScratch **out) {
 }
 
 std::map<int, std::array<hipStream_t, 2>> g_part_streams;  // msd_large's part streams per scratch key
+int g_fail_front = -1;  // smj_debug_fail_front: msd_large's front of this part fails for want of scratch
+int g_seq_from = -1;    // the part from which the last partitioned call ran its parts in turn (-1: none)
 
 void msd_free_one(MsdScratch &m) {  // also a set whose creation failed half-way (dev still -1)
     if (m.dev >= 0) hipSetDevice(m.dev);
     for (auto &t : m.t)
         for (void *p : {t.tempA, t.tempB, t.offsA, t.tmm, t.list, t.tinfo, t.offsB, t.seg, t.bk, t.fb, t.fb2})
-            hipFree(p);
+            dev_free(p);
     for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                     (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                     (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
                     (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy})
-        hipFree(p);
+        dev_free(p);
     hipHostFree(m.p1h);
     hipHostFree(m.h_p1c);
     hipHostFree(m.h_pick);
@@ -949,6 +962,7 @@ struct MsdCtx {
 };
 
 thread_local bool t_job_open = false;  // smj_dev_sort_merge_join_begin's job, until its _end
+std::atomic<int> g_open_jobs{0};       // begun jobs of every thread (smj_trim refuses while one is open)
 
 int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, const MsdStage *stg, MsdCtx *cx) {
     if (t_job_open) return SMJ_ERR_INVALID;  // a begun job owns this thread's scratch until its _end
@@ -1262,6 +1276,7 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
         g_msd_bigdev = ms->h_plan->nbigdev;
         g_msd_groups[3] = ms->h_plan->nlsd;
         g_msd_packb = ms->h_plan->packB;
+        g_msd_wstage = ms->h_plan->nwst;
     }
     bool redo = false;
     MsdFinalParams ff = fp;  // packed pass-B rows: the single-key tier reads the words (pk_mode 3), the
@@ -1372,15 +1387,15 @@ bool msd_part1_on(const MsdIn *in, int ntab) {
 // -- and by smj_finalize.
 void msd_part1_release(MsdScratch *ms) {
     for (int x = 0; x < 2; x++) {
-        if (ms->pst[x]) hipFree(ms->pst[x]);
+        if (ms->pst[x]) dev_free(ms->pst[x]);
         ms->pst[x] = nullptr;
         ms->c_pst[x] = 0;
     }
-    if (ms->p1st) hipFree(ms->p1st);
+    if (ms->p1st) dev_free(ms->p1st);
     ms->p1st = nullptr;
     ms->c_p1st = 0;
     for (int x = 0; x < 2; x++) {
-        if (ms->p1desc[x]) hipFree(ms->p1desc[x]);
+        if (ms->p1desc[x]) dev_free(ms->p1desc[x]);
         ms->p1desc[x] = nullptr;
         ms->c_p1desc[x] = 0;
     }
@@ -1807,6 +1822,7 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
         static const bool chain = getenv("SMJ_PART_CHAIN") && getenv("SMJ_PART_CHAIN")[0] == '1';
         auto front = [&](int p) -> int {
             t_msd_var = p & 1;
+            if (p == g_fail_front) t_fail_grow = true;  // (a test: this part's scratch "cannot be had")
             if (p > 0 && chain) HIP_TRY(hipStreamWaitEvent(ps[p & 1], fe[(p - 1) & 1], 0));
             SMJ_TRY(msd_front(&parts[2 * (size_t)p], 2, 1, key2, ps[p & 1], nullptr, &cx[p]));
             HIP_TRY(hipEventRecord(fe[p & 1], ps[p & 1]));
@@ -1830,8 +1846,13 @@ int msd_large(const MsdIn *in, int ntab, int join, int key2, T *out_j, int64_t *
             }
             if (p < nspl) {
                 const int rc = front(p + 1);
-                if (rc == SMJ_ERR_NOMEM) seq = true;
-                else SMJ_TRY(rc);
+                t_fail_grow = false;
+                if (rc == SMJ_ERR_NOMEM) {
+                    seq = true;
+                    g_seq_from = p + 1;
+                } else {
+                    SMJ_TRY(rc);
+                }
             }
             t_msd_var = p & 1;
             SMJ_TRY(msd_back(cx[p], out_j + J * tc, rows, ps[p & 1]));
@@ -1902,7 +1923,7 @@ void idx_free_all() {
     for (auto &kv : g_idx) {
         if (kv.second.dev < 0) continue;
         hipSetDevice(kv.second.dev);
-        for (void *q : {kv.second.pr[0], kv.second.pr[1], kv.second.ps[0], kv.second.ps[1], kv.second.jp}) hipFree(q);
+        for (void *q : {kv.second.pr[0], kv.second.pr[1], kv.second.ps[0], kv.second.ps[1], kv.second.jp}) dev_free(q);
     }
     g_idx.clear();
 }
@@ -2058,12 +2079,19 @@ extern "C" void smj_debug_msd_tiers(int64_t *out4) {
 extern "C" int64_t smj_debug_msd_bigdev(void) { return g_msd_bigdev; }
 // Diagnostic only: 1 if the last pipeline call packed its pass-B rows
 extern "C" int64_t smj_debug_msd_packb(void) { return g_msd_packb; }
+// Diagnostic only: groups of the last pipeline call that the wide-span staged
+// kernel took (msd_final_wstage_kernel: key spans over kStageRange)
+extern "C" int64_t smj_debug_msd_wstage(void) { return g_msd_wstage; }
+// Diagnostic only: the wide-span staged kernel hands a group to the radix tier
+// when a bin holds more than `rows` rows (-1: the built-in SMJ_ST_MAXRUN; 0:
+// every group -- the tests' way to the hand-over path)
+extern "C" void smj_debug_wide_maxrun(int rows) { g_wide_maxrun = rows; }
 
 extern "C" void smj_debug_msd_stats(int64_t *out4) {
     for (int i = 0; i < 4; i++) out4[i] = g_msd_stats[i];
 }
 
-extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+static int smj_dev_select_sort_impl(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
                                    T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
                                    void *stream) {
     (void)key_base;  // the MSD pipeline derives its digits from the data
@@ -2081,7 +2109,16 @@ extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int
     return SMJ_OK;
 }
 
-extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
+
+extern "C" int smj_dev_select_sort(const T *in, int64_t n_rows, int col_num, int use_select, int select_col,
+                                   T select_val, int key_col, uint64_t key_base, T *out, int64_t *out_rows,
+                                   void *stream) {
+    const int rc = smj_dev_select_sort_impl(in, n_rows, col_num, use_select, select_col, select_val, key_col, key_base, out, out_rows, stream);
+    if (rc == SMJ_OK) trim_if_over_limit();
+    return rc;
+}
+
+static int smj_dev_sort_merge_join_impl(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
                                        int key1, const T *S, int64_t ns, int c2, int use_sel2, int sel_col2,
                                        T sel_val2, int key2, T *R_sorted, T *S_sorted, T *out, int64_t *h_rows,
                                        void *stream) {
@@ -2100,6 +2137,16 @@ extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_s
                         {S, ns, c2, use_sel2, sel_col2, key2, sel_val2, S_sorted}};
     if (c1 > kDirectCols || c2 > kDirectCols) return msd_indexed(t, 2, 1, key2, SMJ_KEY_INT64, out, h_rows, s);
     return msd_any(t, 2, 1, key2, out, h_rows, s);
+}
+
+
+extern "C" int smj_dev_sort_merge_join(const T *R, int64_t nr, int c1, int use_sel1, int sel_col1, T sel_val1,
+                                       int key1, const T *S, int64_t ns, int c2, int use_sel2, int sel_col2,
+                                       T sel_val2, int key2, T *R_sorted, T *S_sorted, T *out, int64_t *h_rows,
+                                       void *stream) {
+    const int rc = smj_dev_sort_merge_join_impl(R, nr, c1, use_sel1, sel_col1, sel_val1, key1, S, ns, c2, use_sel2, sel_col2, sel_val2, key2, R_sorted, S_sorted, out, h_rows, stream);
+    if (rc == SMJ_OK) trim_if_over_limit();
+    return rc;
 }
 
 // The fused call in two halves (smj.h): _begin launches the pipeline up to
@@ -2152,6 +2199,7 @@ extern "C" int smj_dev_sort_merge_join_begin(const T *R, int64_t nr, int c1, int
     }
     t_job = j;
     t_job_open = true;
+    g_open_jobs++;
     *job = j;
     return SMJ_OK;
 }
@@ -2192,15 +2240,17 @@ extern "C" int smj_dev_sort_merge_join_begin_pk(const int64_t *R, int64_t nr, in
     }
     t_job = j;
     t_job_open = true;
+    g_open_jobs++;
     *job = j;
     return SMJ_OK;
 }
 
-extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
+static int smj_dev_sort_merge_join_end_impl(void *job, T *out, int64_t *h_rows) {
     SmjJob *j = (SmjJob *)job;
     if (!j || j != t_job || !h_rows) return SMJ_ERR_INVALID;
     t_job = nullptr;
     t_job_open = false;
+    g_open_jobs--;
     std::unique_ptr<SmjJob> own(j);
     h_rows[0] = h_rows[1] = h_rows[2] = 0;
     if (j->whole)
@@ -2212,6 +2262,13 @@ extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
         return SMJ_ERR_INVALID;
     }
     return msd_back(j->cx, out, h_rows, j->s);
+}
+
+
+extern "C" int smj_dev_sort_merge_join_end(void *job, T *out, int64_t *h_rows) {
+    const int rc = smj_dev_sort_merge_join_end_impl(job, out, h_rows);
+    if (rc == SMJ_OK) trim_if_over_limit();
+    return rc;
 }
 
 // The host-pointer path with staged input (smj_host.hip): R and S are
@@ -2240,6 +2297,17 @@ int smj::msd_staged_sort_merge_join(const int64_t *hR, int64_t nr, int c1, int s
 // partitioned mode with `parts` parts (0 = automatic: tables over 1.6e8 rows).
 extern "C" void smj_debug_force_parts(int parts) { g_force_parts = parts > 0 ? parts : 0; }
 
+// Diagnostic only (not part of smj.h): in the partitioned mode's overlapped
+// order, the front phase of part `part` fails as if its scratch set could not
+// be allocated (-1: never); returns the part from which the previous
+// partitioned call ran its parts one at a time on one set (-1: it did not).
+extern "C" int smj_debug_fail_front(int part) {
+    const int r = g_seq_from;
+    g_fail_front = part;
+    g_seq_from = -1;
+    return r;
+}
+
 extern "C" void smj_debug_spin_limit(int64_t polls) {
     g_spin_limit = polls < 0 ? kMsdSpinLimit : (uint32_t)std::min<int64_t>(polls, UINT32_MAX);
 }
@@ -2264,8 +2332,8 @@ void typed_free_all() {
     for (auto &kv : g_typed) {
         if (kv.second.dev < 0) continue;
         hipSetDevice(kv.second.dev);
-        hipFree(kv.second.r);
-        hipFree(kv.second.s);
+        dev_free(kv.second.r);
+        dev_free(kv.second.s);
     }
     g_typed.clear();
 }
@@ -2278,7 +2346,7 @@ int64_t key_fwd_host(uint64_t u, int ktype) {
 uint32_t cols_mask(int key, int use_sel, int sel_col) { return (1u << key) | (use_sel ? 1u << sel_col : 0u); }
 }  // namespace
 
-extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_t nr, int c1, int use_sel1,
+static int smj_dev_sort_merge_join_typed_impl(int key_type, const void *R, int64_t nr, int c1, int use_sel1,
                                              int sel_col1, uint64_t sel_bits1, int key1, const void *S, int64_t ns,
                                              int c2, int use_sel2, int sel_col2, uint64_t sel_bits2, int key2,
                                              void *R_sorted, void *S_sorted, void *out, int64_t *h_rows,
@@ -2338,6 +2406,17 @@ extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_
     }
     HIP_TRY(hipStreamSynchronize(st));
     return SMJ_OK;
+}
+
+
+extern "C" int smj_dev_sort_merge_join_typed(int key_type, const void *R, int64_t nr, int c1, int use_sel1,
+                                             int sel_col1, uint64_t sel_bits1, int key1, const void *S, int64_t ns,
+                                             int c2, int use_sel2, int sel_col2, uint64_t sel_bits2, int key2,
+                                             void *R_sorted, void *S_sorted, void *out, int64_t *h_rows,
+                                             void *stream) {
+    const int rc = smj_dev_sort_merge_join_typed_impl(key_type, R, nr, c1, use_sel1, sel_col1, sel_bits1, key1, S, ns, c2, use_sel2, sel_col2, sel_bits2, key2, R_sorted, S_sorted, out, h_rows, stream);
+    if (rc == SMJ_OK) trim_if_over_limit();
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -2585,7 +2664,7 @@ static int partition_regions_impl(const T *in, int64_t n, int cols, int use_sele
     for (int i = 0; i < n_split; i++) w.v[128 + i] = h_spl[i];
     DevScratch *sc;
     SMJ_TRY(scratch(&sc));
-    if (!sc->rwords) HIP_TRY(hipMalloc(&sc->rwords, sizeof(int64_t) * (192 + 2)));
+    if (!sc->rwords) HIP_TRY(dev_alloc(&sc->rwords, sizeof(int64_t) * (192 + 2)));
     const int64_t tile = p1_tile(cols), nt = (n + tile - 1) / tile;
     SMJ_TRY(grow(&sc->rst, &sc->c_rst, (size_t)nt * nb * 8));
     uint32_t *flags = (uint32_t *)(sc->rwords + 192);
@@ -2668,6 +2747,14 @@ extern "C" int smj_dev_gen_zipf(T *out, int64_t row0, int64_t rows, uint64_t see
     return SMJ_OK;
 }
 
+extern "C" int smj_dev_gen_wide(T *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed,
+                                int64_t plant_rows, void *stream) {
+    if (rows < 0 || (rows && !out) || plant_rows < 0 || row0 < 0) return SMJ_ERR_INVALID;
+    if (rows == 0) return SMJ_OK;
+    HIP_TRY(launch_gen_wide(out, row0, rows, seed, plant_seed, plant_rows, (hipStream_t)stream));
+    return SMJ_OK;
+}
+
 extern "C" int smj_dev_digest(const T *rows, int64_t n_rows, int col_num, int64_t pos0, uint64_t *d_digest,
                               void *stream) {
     if (n_rows < 0 || (n_rows && !rows) || !d_digest || col_num < 1 || col_num > SMJ_MAX_COLS || pos0 < 0)
@@ -2723,6 +2810,70 @@ extern "C" int smj_dev_unpack_rows(const int64_t *d_packed, int64_t n, int key_c
 }
 
 // ---------------------------------------------------------------------------
+// device memory account (smj_scratch_bytes, smj_set_scratch_limit, smj_trim)
+// ---------------------------------------------------------------------------
+namespace {
+std::mutex g_alloc_mu;
+std::unordered_map<void *, size_t> g_alloc;
+int64_t g_held = 0;
+int64_t g_scratch_limit = -1;  // bytes; -1 = none (SMJ_SCRATCH_LIMIT)
+bool g_limit_read = false;
+}  // namespace
+
+hipError_t smj::dev_alloc_raw(void **p, size_t n) {
+    const hipError_t e = hipMalloc(p, n);
+    if (e == hipSuccess && *p) {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        g_alloc[*p] = n;
+        g_held += (int64_t)n;
+    }
+    return e;
+}
+
+hipError_t smj::dev_free(void *p) {
+    if (!p) return hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        auto it = g_alloc.find(p);
+        if (it != g_alloc.end()) {
+            g_held -= (int64_t)it->second;
+            g_alloc.erase(it);
+        }
+    }
+    return hipFree(p);
+}
+
+int64_t smj::dev_held_bytes() {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    return g_held;
+}
+
+extern "C" int64_t smj_scratch_bytes(void) { return dev_held_bytes(); }
+
+extern "C" void smj_set_scratch_limit(int64_t bytes) {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_scratch_limit = bytes < 0 ? -1 : bytes;
+    g_limit_read = true;
+}
+
+int smj::open_jobs() { return g_open_jobs.load(); }
+
+void smj::trim_if_over_limit() {
+    int64_t lim, held;
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        if (!g_limit_read) {
+            const char *e = getenv("SMJ_SCRATCH_LIMIT");
+            g_scratch_limit = e ? atoll(e) : -1;
+            g_limit_read = true;
+        }
+        lim = g_scratch_limit;
+        held = g_held;
+    }
+    if (lim >= 0 && held > lim && g_open_jobs.load() == 0) smj_trim();
+}
+
+// ---------------------------------------------------------------------------
 // release of every library-owned buffer (smj_finalize, smj_host.hip)
 // ---------------------------------------------------------------------------
 void smj::api_free_all() {
@@ -2733,7 +2884,7 @@ void smj::api_free_all() {
         hipSetDevice(s.dev);
         for (void *q : {s.tmp, s.status, s.apart, (void *)s.hist, (void *)s.plan, (void *)s.ctr, (void *)s.dcount,
                         (void *)s.segsum, (void *)s.trash, s.rst, (void *)s.rwords})
-            hipFree(q);
+            dev_free(q);
         hipHostFree(s.h_plan);
         hipHostFree(s.h_small);
     }

@@ -90,10 +90,10 @@ int g_shard_n = 0;
 int hgrow(HostDev &d, int i, size_t need) {
     need = std::max<size_t>(need, 64);
     if (need <= d.c[i]) return SMJ_OK;
-    if (d.b[i]) HIP_TRY(hipFree(d.b[i]));
+    if (d.b[i]) HIP_TRY(dev_free(d.b[i]));
     d.b[i] = nullptr;
     d.c[i] = 0;
-    HIP_TRY(hipMalloc(&d.b[i], need));
+    HIP_TRY(dev_alloc(&d.b[i], need));
     d.c[i] = need;
     return SMJ_OK;
 }
@@ -337,10 +337,37 @@ extern "C" int smj_debug_shard_rows(int64_t *out, int max) {
     return g_shard_n;
 }
 
+// Returns every device buffer the library holds (scratch sets, partition
+// staging, the device set's staging buffers) once the work on them has
+// drained; later calls allocate again.  The device set and its streams stay.
+// Refused (SMJ_ERR_INVALID) while a smj_dev_sort_merge_join_begin job is open.
+// Replaces the reference's per-phase dpu_free (app.c:307,402,503,761).
+extern "C" int smj_trim(void) {
+    if (open_jobs() > 0) return SMJ_ERR_INVALID;
+    int cur = -1;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (auto &d : g_devs) {
+        hipSetDevice(d.phys);
+        HIP_TRY(hipDeviceSynchronize());
+        for (int i = 0; i < B_N; i++) {
+            dev_free(d.b[i]);
+            d.b[i] = nullptr;
+            d.c[i] = 0;
+        }
+    }
+    if (have_cur) {
+        hipSetDevice(cur);
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    api_free_all();
+    if (have_cur) hipSetDevice(cur);
+    return SMJ_OK;
+}
+
 extern "C" void smj_finalize(void) {
     for (auto &d : g_devs) {
         hipSetDevice(d.phys);
-        for (int i = 0; i < B_N; i++) hipFree(d.b[i]);
+        for (int i = 0; i < B_N; i++) dev_free(d.b[i]);
         hipStreamDestroy(d.st);
         hipStreamDestroy(d.cp);
         for (auto e : d.in_ev) hipEventDestroy(e);

@@ -141,6 +141,8 @@ hipError_t launch_join_gather(const int64_t *R, int c1, const int64_t *S, int c2
                               int64_t J, int64_t *out, hipStream_t s);
 hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t seed,
                               uint64_t key_range, hipStream_t s);
+hipError_t launch_gen_wide(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed,
+                           int64_t plant_rows, hipStream_t s);
 hipError_t launch_gen_zipf(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t domain,
                            double theta, double zeta_n, hipStream_t s);
 // distributed splitters (smj_dev_dist_sample / smj_dev_dist_splitters)
@@ -238,6 +240,8 @@ __host__ __device__ inline bool msd_big_on_device(uint32_t span, uint32_t ktR, u
 // the thresholds in force: kBgMaxRows / kBgSeg, or SMJ_BG_MAX_ROWS / SMJ_BG_SEG
 // from the environment (tests: giant groups at small sizes; the segment a
 // multiple of kGroupCap)
+// smj_debug_wide_maxrun: msd_final_wstage_kernel's bin limit override (-1: none)
+extern int g_wide_maxrun;
 struct MsdBgLimits {
     uint32_t max_rows, seg;
 };
@@ -376,6 +380,8 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     // does not take.
     uint32_t nopack;     // part_a: a selected row's other column does not fit int32
     uint32_t packB;      // msd_bases: pass-B rows are packed in this call
+    uint32_t nwst;       // groups of a key span over kStageRange left by the staged kernel to
+                         // msd_final_wstage_kernel (full-range keys: SURVEY 8(d)'s C3-wide)
 };
 // A kernel launched after msd_group_kernel reads the plan's error word first:
 // a set bit means the dense group array may hold slots this call never wrote.
@@ -417,7 +423,8 @@ struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
     uint32_t kt[2];      // pass-B tiles of the bucket, per table
     int64_t base;        // smallest key the group's sub-buckets can hold
     uint32_t span;       // keys the group's sub-buckets can hold (saturated): key - base < span
-    uint32_t pad[3];
+    uint32_t pad[3];     // [0]: 1 = one heavy key's sub-bucket (msd_single); [1], [2]: a group spanning
+                         // over kStageRange keys, the low / high half of its bin scale (msd_final_wstage_kernel)
 };
 struct MsdGroupParams {
     const uint16_t *offs[2];
@@ -467,6 +474,17 @@ struct MsdFinalParams {
 // ---- C-ABI internals shared by smj_api.hip and smj_host.hip -------------------
 // frees every library-owned device / pinned buffer (smj_finalize)
 void api_free_all();
+// Device memory the library owns goes through these: hipMalloc / hipFree plus
+// the held-byte account behind smj_scratch_bytes / smj_set_scratch_limit.
+hipError_t dev_alloc_raw(void **p, size_t n);
+hipError_t dev_free(void *p);
+template <class X>
+inline hipError_t dev_alloc(X **p, size_t n) { return dev_alloc_raw(reinterpret_cast<void **>(p), n); }
+int64_t dev_held_bytes();
+// after a top-level call: release every scratch buffer when the library holds
+// more than the caller's limit (smj_set_scratch_limit); the call's work is done
+void trim_if_over_limit();
+int open_jobs();  // smj_dev_sort_merge_join_begin jobs not yet ended (all threads)
 // worker threads of the multi-device host API give each device of the set its
 // own scratch (several may map to one physical device); -1 = per device
 void set_scratch_slot(int slot);

@@ -1020,6 +1020,26 @@ __global__ void gen_uniform_kernel(int64_t *out, int64_t row0, int64_t rows, uin
     }
 }
 
+// C3-wide: full-range signed keys; with plant_rows > 0 a third
+// of the rows take the key of a random row of the plant_seed table (smj.h)
+__global__ void gen_wide_kernel(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed,
+                                uint64_t plant_rows) {
+    const uint64_t salt = seed * 0xD1B54A32D192ED03ull, psalt = plant_seed * 0xD1B54A32D192ED03ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = (uint64_t)(row0 + i);
+        uint64_t key = splitmix64(g + salt);
+        if (plant_rows) {
+            const uint64_t d = splitmix64(key ^ 0x2545F4914F6CDD1Dull);
+            if (__umul64hi(d, 3ull) == 0) key = splitmix64(__umul64hi(splitmix64(d), plant_rows) + psalt);
+        }
+        i64x2 v;
+        v.x = (long long)key;
+        v.y = (long long)g;
+        reinterpret_cast<i64x2 *>(out)[i] = v;
+    }
+}
+
 __global__ void gen_zipf_kernel(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, int64_t n,
                                 double theta, double zetan) {
     const uint64_t salt = seed * 0xD1B54A32D192ED03ull;
@@ -1369,6 +1389,14 @@ hipError_t launch_gen_uniform(int64_t *out, int64_t row0, int64_t rows, uint64_t
                               hipStream_t s) {
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(rows, 256), 8192));
     hipLaunchKernelGGL(gen_uniform_kernel, dim3(grid), dim3(256), 0, s, out, row0, rows, seed, key_range);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_wide(int64_t *out, int64_t row0, int64_t rows, uint64_t seed, uint64_t plant_seed,
+                           int64_t plant_rows, hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks_for(rows, 256), 8192));
+    hipLaunchKernelGGL(gen_wide_kernel, dim3(grid), dim3(256), 0, s, out, row0, rows, seed, plant_seed,
+                       (uint64_t)plant_rows);
     return hipGetLastError();
 }
 

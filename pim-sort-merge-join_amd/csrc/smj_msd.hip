@@ -2307,6 +2307,13 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         gr.base = (int64_t)((uint64_t)p.bk[0][a].lo + (uint64_t)r0);
         const unsigned __int128 sp = r1 - r0;
         gr.span = sp > 0xffffffffu ? 0xffffffffu : (uint32_t)sp;
+        if (sp > (unsigned __int128)kStageRange) {
+            // a wide group (msd_final_wstage_kernel): its kStageRange bins are
+            // bin(key) = mulhi64(key - base, bscale) < kStageRange over the interval
+            const uint64_t bs = (uint64_t)(((unsigned __int128)kStageRange << 64) / sp);
+            gr.pad[1] = (uint32_t)bs;
+            gr.pad[2] = (uint32_t)(bs >> 32);
+        }
         if (hv_only) {
             gr.base = s_hk[hj];
             gr.span = 1;
@@ -2613,17 +2620,6 @@ static_assert(kGroupCap == (1 << kFinIdxBits), "sort word = residual << 10 | gro
 
 constexpr int kCountRange = 4096;  // counting-sort residual range (packed u16 bins)
 constexpr int kMaxDupRun = 32;     // longest equal-key run the counting path re-orders
-#ifndef SMJ_ST_FOLDSCAN
-#define SMJ_ST_FOLDSCAN 0  // the staged kernel's join-row scan sharing the st_issue_lists barrier: off --
-                           // neutral in the same-box A/B (r05d), and the size-sequence probe
-                           // (tools/seq_sizes.py, r05i/r05j) caught it with a wrong join count and
-                           // inconsistent run metadata on repeated partitioned calls; off, the probe
-                           // is clean (a race not yet understood)
-#endif
-#ifndef SMJ_ST_RUNFIX
-#define SMJ_ST_RUNFIX 0  // the staged kernel: groups whose longest equal-key run is <= this sort runs in one pass
-                         // (off: r05d same-box A/B, msd_final 1.78 -> 1.86 ms at 8 -- one lane holding its wave)
-#endif
 #ifndef SMJ_ST_MAXRUN
 #define SMJ_ST_MAXRUN kMaxDupRun  // the staged kernel: longer runs take the in-LDS LSD (<= kMaxDupRun)
 #endif
@@ -3273,6 +3269,16 @@ __device__ __forceinline__ bool st_ok(const MsdFinalParams &p, const MsdGroup &g
            (COMB ? g.nR + nS <= (uint32_t)kStRows : g.nR <= (uint32_t)kGroupCap && nS <= (uint32_t)kGroupCap);
 }
 
+// a group the staged kernel leaves to msd_final_wstage_kernel: it would fit
+// but for its key span (over kStRange values)
+template <bool COMB>
+__device__ __forceinline__ bool stw_ok(const MsdFinalParams &p, const MsdGroup &g) {
+    const uint32_t nS = p.ntab > 1 ? g.nS : 0u;
+    return !g.flags && g.span > (uint32_t)kStRange && g.kt[0] <= (uint32_t)kStList &&
+           (p.ntab < 2 || g.kt[1] <= (uint32_t)kStList) &&
+           (COMB ? g.nR + nS <= (uint32_t)kStRows : g.nR <= (uint32_t)kGroupCap && nS <= (uint32_t)kGroupCap);
+}
+
 __device__ __forceinline__ void st_load_offs(const MsdFinalParams &p, const MsdGroup &g, uint32_t (&o0)[2],
                                              uint32_t (&o1)[2]) {
     const uint32_t tid = opaque_tid();
@@ -3469,7 +3475,7 @@ template <bool COMB, bool PK>
 __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup &g, int64_t gi,
                                         const i64x2 (&rows)[kStIt], StSmem &sm, int &wsb, uint32_t &mmask,
                                         uint32_t (&part)[kStIt], const uint32_t (&no0)[2], const uint32_t (&no1)[2],
-                                        uint32_t &nex, uint32_t &mex) {
+                                        uint32_t &nex) {
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const StSplit<COMB> L(p, g);
@@ -3591,48 +3597,10 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     // run, r01k; the run's first thread insertion-sorting the run, r01ah:
     // 2.81 vs 2.32 ms.)
     static_assert(kStRows / 2 == 2 * kStThreads, "two compare-exchanges per thread and round");
-    // Runs of at most SMJ_ST_RUNFIX rows (block-uniform fl: the longest run):
-    // one pass instead of fl rounds -- the thread holding a run's first
-    // position (read off the histogram starts) sorts the run by group row on
-    // its own (a compare-exchange for two rows, an insertion sort for more),
-    // then one barrier.  C3's longest run per group is ~4 (Poisson(1/3) keys
-    // per table): 1 barrier instead of ~4.
-    const bool runfix = SMJ_ST_RUNFIX > 1 && !lsd && !ST_ABL(16) && fl > 1u && fl <= (uint32_t)SMJ_ST_RUNFIX;
-    if (runfix) {
-#pragma unroll
-        for (int k = 0; k < kStIt; k++) {
-            const uint32_t q = (uint32_t)tid + (uint32_t)k * kStThreads;
-            if (!L.valid_pos(q)) continue;
-            const uint32_t x = q >= sp ? 1u : 0u, pq = q - (x ? sp : 0u);
-            const uint32_t w0 = sm.key[q], res = w0 >> kStIdx, sh = 16u * (res & 1u);
-            const uint32_t hw = sm.hist[x][res >> 1];
-            if (((hw >> sh) & 0xffffu) != pq) continue;  // not the first position of its run
-            const uint32_t nx = x ? nS : nR;
-            const uint32_t end = (res & 1u) ? ((res + 1u < (uint32_t)kStRange) ? (sm.hist[x][(res + 1) >> 1] & 0xffffu) : nx)
-                                            : (hw >> 16);
-            const uint32_t len = end - pq;
-            if (len < 2) continue;
-            if (len == 2) {
-                const uint32_t b = sm.key[q + 1];
-                if (w0 > b) {
-                    sm.key[q] = b;
-                    sm.key[q + 1] = w0;
-                }
-            } else {
-                for (uint32_t i = 1; i < len; i++) {
-                    const uint32_t v = sm.key[q + i];
-                    uint32_t j = i;
-                    while (j > 0 && sm.key[q + j - 1] > v) {
-                        sm.key[q + j] = sm.key[q + j - 1];
-                        j--;
-                    }
-                    sm.key[q + j] = v;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd || runfix) ? 0u : fl); rd++) {
+    // (Measured and dropped in round 5: runs of <= 8 rows ordered in one pass
+    // by the thread holding a run's first position, +0.08 ms -- one lane
+    // holds its wave; profiles/r05/r05d.)
+    for (uint32_t rd = 0; rd < ((ST_ABL(16) || lsd) ? 0u : fl); rd++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint32_t q = 2u * (uint32_t)(tid + h * kStThreads) + (rd & 1u);
@@ -3686,23 +3654,17 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
             }
         }
     }
-    if (SMJ_ST_FOLDSCAN) {
-        // the join rows' block scan, first half: wave totals published here,
-        // read by st_emit after the barrier that separates the two (in
-        // st_issue_lists, or the kernel's own when there is no next group) --
-        // one barrier per group less than a scan of its own
-        const uint32_t c = (uint32_t)__popc(mmask), inc = wave_incl_scan(c, lane);
-        if (lane == 63) sm.wsum[wsb][wave] = inc;
-        mex = inc - c;
-    }
     return true;
 }
 
 // sorted rows out (coalesced), join rows out (word-coalesced); the histogram
 // is zeroed for the next group here (no one reads it after the lookups)
-template <bool COMB>
+// WIDE (msd_final_wstage_kernel): keys come from k64 (group-row order), not
+// from the group base and the sort word's residual
+template <bool COMB, bool WIDE = false>
 __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, StSmem &sm,
-                                        int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt], uint32_t mex) {
+                                        int &wsb, uint32_t mmask, const uint32_t (&part)[kStIt],
+                                        const int64_t *k64 = nullptr) {
     const int tid = opaque_tid();
     const StSplit<COMB> L(p, g);
     {
@@ -3718,7 +3680,8 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
         if (L.valid(k, q) && !ST_ABL(2)) {
             const bool x = L.is_s(k, q);
             const uint32_t w = sm.key[q];
-            const int64_t key = g.base + (int64_t)(w >> kStIdx), pay = sm.pay[w & kStIdxMask];
+            const int64_t key = WIDE ? k64[w & kStIdxMask] : g.base + (int64_t)(w >> kStIdx);
+            const int64_t pay = sm.pay[w & kStIdxMask];
             const int kc = x ? kc1 : kc0;
             i64x2 r;
             r.x = kc ? pay : key;
@@ -3728,21 +3691,8 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
     }
     if (!p.join || ST_ABL(8)) return;
     const uint32_t *kS = sm.key + L.sp;
-    uint32_t total, o;
-    if (SMJ_ST_FOLDSCAN) {  // the wave totals st_sort published (a barrier ago)
-        const int wave = tid >> 6;
-        uint32_t before = 0, all = 0;
-#pragma unroll
-        for (int u = 0; u < kStWaves; u++) {
-            const uint32_t x = sm.wsum[wsb][u];
-            before += u < wave ? x : 0u;
-            all += x;
-        }
-        total = all;
-        o = before + mex;
-    } else {
-        o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
-    }
+    uint32_t total;
+    uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
     wsb ^= 1;
     if (tid == 0) p.counts[gi] = total;
     if (total == 0) return;
@@ -3764,7 +3714,8 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
             int64_t val;
             if (c < 2) {  // R's columns: the key from the sort word, the payload staged
                 const uint32_t w = sm.key[m >> kStIdx];
-                val = (int)c == kc0 ? g.base + (int64_t)(w >> kStIdx) : sm.pay[w & kStIdxMask];
+                val = (int)c == kc0 ? (WIDE ? k64[w & kStIdxMask] : g.base + (int64_t)(w >> kStIdx))
+                                    : sm.pay[w & kStIdxMask];
             } else {      // S's column other than key2: its payload
                 val = sm.pay[kS[m & kStIdxMask] & kStIdxMask];
             }
@@ -3817,6 +3768,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
     __syncthreads();
     i64x2 cur[kStIt];
     int wsb = 0;
+    uint32_t nwst = 0;  // wide groups left to msd_final_wstage_kernel (block-uniform)
     bool have = false;  // cur holds the rows of group gi
     for (int64_t li = 0; li < cnt; li++) {
         const int64_t gi = g0 + li * gs;
@@ -3832,6 +3784,11 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
             continue;
         }
         if (!st_ok<COMB>(p, g)) {
+            if (stw_ok<COMB>(p, g)) {  // a wide group: msd_final_wstage_kernel's (launched next)
+                nwst++;
+                have = false;
+                continue;
+            }
             // (the group kernel packs over kGroupCap rows of a table only where
             // every group fits this kernel: the radix tier takes <= kGroupCap)
             if (opaque_tid() == 0) {
@@ -3862,8 +3819,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
         FIN_STAMP(1);
         uint32_t mmask = 0, part[kStIt];
         uint32_t nex;  // the next group's run-length prefix, scanned with this group's bins
-        uint32_t mex = 0;  // this thread's exclusive prefix of join rows within its wave (SMJ_ST_FOLDSCAN)
-        const bool ok = st_sort<COMB, PK>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex, mex);  // cur is staged in LDS here
+        const bool ok = st_sort<COMB, PK>(p, g, gi, cur, sm, wsb, mmask, part, o0, o1, nex);  // cur is staged in LDS here
         FIN_STAMP(2);
         // st_issue_lists writes only the list region (unused by the sort; its
         // start bitmap was zeroed, and its run lengths scanned, inside
@@ -3878,7 +3834,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
             __syncthreads();
         FIN_STAMP(3);
         if (ok) {
-            st_emit<COMB>(p, g, gi, sm, wsb, mmask, part, mex);
+            st_emit<COMB>(p, g, gi, sm, wsb, mmask, part);
         } else {  // hand-over: the histogram still needs zeroing
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
             for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
@@ -3889,6 +3845,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
         FIN_STAMP(5);
         if (SMJ_STAMPS && (p.dbg & 1)) ph[9]++;
     }
+    if (nwst && opaque_tid() == 0) atomicAdd(&p.plan->nwst, nwst);
     if (SMJ_STAMPS && (p.dbg & 1) && opaque_tid() == 0)
         for (int k = 0; k < 10; k++) atomicAdd(&g_fin_phase[k], ph[k]);
 }
@@ -3904,6 +3861,256 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
         return;
     }
     st_body<COMB, PK>(p, sm);
+}
+
+// ---- wide-span staged path (round 6) ----------------------------------------
+// Groups whose keys span more than kStRange values -- every group of a table
+// with full-range int64 keys (SURVEY 8(d)'s C3-wide: a pass-B sub-bucket then
+// spans ~2^45 keys) -- went to the radix tier, which handed them to the 64-bit
+// LSD kernel (msd_final_wide_kernel: C3-wide msd_final 9.7 ms).  Here they
+// take the staged kernel's shape: rows gathered once into registers (the next
+// group's during this one's emit), staged in LDS with their FULL keys (k64),
+// a counting sort over kStRange monotone bins bin(key) = mulhi64(key - base,
+// bscale) (MsdGroup::pad[1..2], msd_group_kernel), then odd-even rounds that
+// order each bin by (key, group row) -- the narrow kernel's equal-residual
+// rounds with a key compare -- and the zip join by key within each bin
+// (cpu_app.c:204-266: occurrence i of a key in R pairs with occurrence i in
+// S).  The full keys cost 16 KiB of LDS: two workgroups per CU.  A bin over
+// SMJ_ST_MAXRUN rows (keys clustered inside the group's interval) hands the
+// group to the radix tier before anything is written.
+struct StwSmem : StSmem {
+    int64_t k64[kStRows];  // keys, group-row order
+};
+
+// stage + bin sort + in-bin rounds of wide group g, then the zip join lookups
+template <bool COMB, bool PK>
+__device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup &g, const i64x2 (&rows)[kStIt],
+                                         StwSmem &sm, int &wsb, uint32_t &mmask, uint32_t (&part)[kStIt],
+                                         const uint32_t (&no0)[2], const uint32_t (&no1)[2], uint32_t &nex) {
+    const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+    const StSplit<COMB> L(p, g);
+    const uint32_t nR = L.nR, nS = L.nS, sp = L.sp;
+    const uint64_t bscale = (uint64_t)g.pad[1] | ((uint64_t)g.pad[2] << 32);
+    uint32_t w[kStIt];  // bin << 16 | atomic rank among its table's rows of that bin (~0u: no row)
+    for (int i = tid; i < kStRows / 32; i += kStThreads) sm.L.starts[i] = 0;  // for the next st_issue_lists
+    const int kc0 = p.tab[0].key, kc1 = p.tab[1].key;
+#pragma unroll
+    for (int k = 0; k < kStIt; k++) {
+        const int v = tid + k * kStThreads;
+        w[k] = ~0u;
+        if (L.valid(k, (uint32_t)v)) {
+            const bool x = L.is_s(k, (uint32_t)v);
+            const int kc = x ? kc1 : kc0;
+            // PK: the packed word's key half is exact from the base (packB: every key
+            // within 2^32 of every group base)
+            const int64_t key = PK ? g.base + (int64_t)(uint32_t)((uint32_t)rows[k].x - (uint32_t)g.base)
+                                   : st_key(rows[k], kc);
+            sm.pay[v] = PK ? (int64_t)(int32_t)(uint32_t)((uint64_t)rows[k].x >> 32) : kc ? rows[k].x : rows[k].y;
+            sm.k64[v] = key;
+            const uint32_t bin = min((uint32_t)__umul64hi((uint64_t)key - (uint64_t)g.base, bscale),
+                                     (uint32_t)kStRange - 1u);
+            const uint32_t sh = 16u * (bin & 1u);
+            w[k] = (bin << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][bin >> 1], 1u << sh) >> sh) & 0xffffu);
+        }
+    }
+    __syncthreads();
+    constexpr int W = kStRange / 2 / kStThreads;
+    uint32_t tot = 0, mrun = 0;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i], lo = h & 0xffffu, hi = h >> 16;
+            mrun = max(mrun, max(lo, hi));
+            t += lo + hi;
+        }
+        tot |= t << (16 * x);
+    }
+    mrun = wave_incl_max(mrun);
+    const uint32_t lens = (no1[0] - no0[0]) | ((no1[1] - no0[1]) << 16);
+    const uint32_t i1 = wave_incl_scan(tot, lane), i2 = wave_incl_scan(lens, lane);
+    if (lane == 63) {
+        sm.wsum[wsb][wave] = i1;
+        sm.wlen[wave] = i2;
+        sm.wmax[wsb][wave] = mrun;
+    }
+    __syncthreads();
+    uint32_t b1 = 0, b2 = 0;
+#pragma unroll
+    for (int u = 0; u < kStWaves; u++) {
+        b1 += u < wave ? sm.wsum[wsb][u] : 0u;
+        b2 += u < wave ? sm.wlen[u] : 0u;
+    }
+    uint32_t ex = b1 + i1 - tot;
+    nex = b2 + i2 - lens;
+    asm volatile("" : "+v"(ex), "+v"(nex));
+    uint32_t fl = 0;
+#pragma unroll
+    for (int u = 0; u < kStWaves; u++) fl = max(fl, sm.wmax[wsb][u]);
+    wsb ^= 1;
+    // block-uniform: the radix tier sorts it (p.dbg bits 16..23: a test's lower limit + 1)
+    const uint32_t maxrun = (p.dbg >> 16) & 0xff ? (uint32_t)((p.dbg >> 16) & 0xff) - 1u : (uint32_t)SMJ_ST_MAXRUN;
+    if (fl > maxrun) return false;
+    fl = fl > 1u ? fl : 0u;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const uint32_t h = sm.hist[x][tid * W + i];
+            sm.hist[x][tid * W + i] = run | ((run + (h & 0xffffu)) << 16);
+            run += (h & 0xffffu) + (h >> 16);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kStIt; k++)
+        if (w[k] != ~0u) {
+            const uint32_t v = (uint32_t)(tid + k * kStThreads), x = L.is_s(k, v) ? 1u : 0u;
+            const uint32_t bin = w[k] >> 16, sh = 16u * (bin & 1u);
+            sm.key[(x ? sp : 0u) + ((sm.hist[x][bin >> 1] >> sh) & 0xffffu) + (w[k] & 0xffffu)] = (bin << kStIdx) | v;
+        }
+    __syncthreads();
+    // rows of one bin were placed in atomic order: odd-even rounds (as many as
+    // the longest bin) order each bin by (key, group row) -- group rows ascend
+    // in input order within a table, so this is the stable order.  A pair
+    // across the R / S boundary never swaps.
+    for (uint32_t rd = 0; rd < fl; rd++) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t q = 2u * (uint32_t)(tid + h * kStThreads) + (rd & 1u);
+            if (L.valid_pos(q) && L.valid_pos(q + 1) && (q < sp) == (q + 1 < sp)) {
+                const uint32_t a = sm.key[q], b = sm.key[q + 1];
+                if ((a >> kStIdx) == (b >> kStIdx)) {
+                    const int64_t ka = sm.k64[a & kStIdxMask], kb = sm.k64[b & kStIdxMask];
+                    if (ka > kb || (ka == kb && a > b)) {
+                        sm.key[q] = b;
+                        sm.key[q + 1] = a;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // zip join: R position i holding key k is occurrence occ = i - (first R
+    // position of k) of its key; it pairs with S position (first S position
+    // of k) + occ while that still holds k.  Keys are sorted within a bin and a
+    // key never leaves its bin, so both searches stay inside the bin (<=
+    // SMJ_ST_MAXRUN positions).
+    mmask = 0;
+    constexpr int JI = COMB ? kStIt : kStIt / 2;
+#pragma unroll
+    for (int q = 0; q < kStIt; q++) part[q] = 0;
+    if (p.join && nR > 0 && nS > 0) {
+        const uint32_t *kS = sm.key + sp;
+#pragma unroll
+        for (int q = 0; q < JI; q++) {
+            const uint32_t i = (uint32_t)tid * JI + q;
+            if (i < nR) {
+                const uint32_t wi = sm.key[i], bin = wi >> kStIdx, sh = 16u * (bin & 1u);
+                const uint32_t hS = sm.hist[1][bin >> 1];
+                const uint32_t sS = (hS >> sh) & 0xffffu;
+                const uint32_t eS = (bin & 1u) ? ((bin + 1u < (uint32_t)kStRange) ? (sm.hist[1][(bin + 1) >> 1] & 0xffffu)
+                                                                                 : nS)
+                                               : (hS >> 16);
+                if (sS == eS) continue;  // no S row in the bin
+                const int64_t kk = sm.k64[wi & kStIdxMask];
+                const uint32_t sR = (sm.hist[0][bin >> 1] >> sh) & 0xffffu;
+                uint32_t f = i;
+                while (f > sR && sm.k64[sm.key[f - 1] & kStIdxMask] == kk) f--;
+                const uint32_t occ = i - f;
+                uint32_t j = sS;
+                while (j < eS && sm.k64[kS[j] & kStIdxMask] < kk) j++;
+                if (j + occ < eS && sm.k64[kS[j + occ] & kStIdxMask] == kk) {
+                    part[q] = j + occ;
+                    mmask |= 1u << q;
+                }
+            }
+        }
+    }
+    return true;
+}
+
+// persistent over the dense groups with the staged kernel's XCD-aware
+// schedule, taking only the wide groups (stw_ok) the staged kernel skipped
+constexpr int kStwGrid = 512;  // two workgroups per CU (LDS)
+int g_wide_maxrun = -1;
+template <bool COMB, bool PK>
+__device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
+    const int64_t ng = p.plan->ngroups;
+    const int64_t gs = gridDim.x / kXcdSlots;
+    const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
+    const int64_t x0 = (int64_t)(blockIdx.x % kXcdSlots) * xr, x1 = min(ng, x0 + xr);
+    const int64_t g0 = x0 + blockIdx.x / kXcdSlots;
+    const int64_t cnt = x1 > g0 ? (x1 - g0 + gs - 1) / gs : 0;
+    {
+        uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+        for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+    }
+    if (0 < cnt) st_load_recs(p, g0, gs, 0, cnt, sm, 0);
+    if (kStRecs < cnt) st_load_recs(p, g0, gs, kStRecs, cnt, sm, 1);
+    __syncthreads();
+    i64x2 cur[kStIt];
+    int wsb = 0;
+    bool have = false;  // cur holds the rows of group gi
+    for (int64_t li = 0; li < cnt; li++) {
+        const int64_t gi = g0 + li * gs;
+        if (li >= kStRecs && li % kStRecs == 0) {
+            const int64_t c = li / kStRecs;
+            __syncthreads();
+            if (li + kStRecs < cnt) st_load_recs(p, g0, gs, li + kStRecs, cnt, sm, (int)((c + 1) & 1));
+            __syncthreads();
+        }
+        const MsdGroup &g = sm.recs[li % (2 * kStRecs)];
+        if (!stw_ok<COMB>(p, g)) {  // the staged kernel's, or listed by it
+            have = false;
+            continue;
+        }
+        if (!have) {
+            uint32_t o0[2], o1[2];
+            st_load_offs(p, g, o0, o1);
+            st_issue<COMB, PK>(p, g, o0, o1, cur, sm, wsb);
+            __syncthreads();
+        }
+        bool nfit = false;
+        const MsdGroup &gn = sm.recs[(li + 1) % (2 * kStRecs)];
+        uint32_t o0[2] = {0, 0}, o1[2] = {0, 0};
+        if (li + 1 < cnt) {
+            nfit = stw_ok<COMB>(p, gn);
+            if (nfit) st_load_offs(p, gn, o0, o1);
+        }
+        uint32_t mmask = 0, part[kStIt], nex;
+        const bool ok = stw_sort<COMB, PK>(p, g, cur, sm, wsb, mmask, part, o0, o1, nex);
+        // the join lookups read the histogram, which does not alias the list
+        // region st_issue_lists writes; its barrier orders them before st_emit
+        // zeroes the histogram
+        if (nfit)
+            st_issue_lists<COMB, PK>(p, gn, o0, o1, nex, cur, sm);
+        else
+            __syncthreads();
+        if (ok) {
+            st_emit<COMB, true>(p, g, gi, sm, wsb, mmask, part, sm.k64);
+        } else {  // a bin over SMJ_ST_MAXRUN rows: the radix tier's (nothing was written)
+            if (opaque_tid() == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+            for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+        }
+        have = nfit;
+        __syncthreads();
+    }
+}
+
+template <bool COMB, int PKM = 0>
+__global__ __launch_bounds__(kStThreads, 4) void msd_final_wstage_kernel(const MsdFinalParams p) {
+    __shared__ StwSmem sm;
+    if (msd_plan_failed(p.plan) || uni32(p.plan->nwst) == 0u) return;
+    if (PKM == 2) {
+        if (uni32(p.plan->packB)) stw_body<COMB, true>(p, sm);
+        else stw_body<COMB, false>(p, sm);
+        return;
+    }
+    stw_body<COMB, PKM == 1>(p, sm);
 }
 
 // Packed pass-B rows: the single-key and oversized groups (msd_group's
@@ -5269,6 +5476,16 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
         } else {
             if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, 2>), dim3(sg), dim3(kStThreads), pad, s, p);
             else hipLaunchKernelGGL((msd_final_stage_kernel<false, 0>), dim3(sg), dim3(kStThreads), pad, s, p);
+        }
+        // the groups of a key span over kStRange the staged kernel left (none: returns at entry)
+        MsdFinalParams pw = p;
+        if (g_wide_maxrun >= 0) pw.dbg |= (min(g_wide_maxrun, 254) + 1) << 16;
+        if (p.combined) {
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<true, 2>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            else hipLaunchKernelGGL((msd_final_wstage_kernel<true, 0>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+        } else {
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<false, 2>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            else hipLaunchKernelGGL((msd_final_wstage_kernel<false, 0>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
         }
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         q.pk_mode = p.shadow[0] ? 2 : -1;  // packed rows possible: the tiers unpack / read the shadow on the device

@@ -65,6 +65,10 @@ SIGNATURES = {
     "smj_dev_partition_regions": (_I, [_P, _L, _I, _I, _I, _L, _I, _P, _I, _P, _P, _P, _P]),
     "smj_dev_gen_uniform": (_I, [_P, _L, _L, _U, _U, _P]),
     "smj_dev_gen_zipf": (_I, [_P, _L, _L, _U, _L, _D, _D, _P]),
+    "smj_dev_gen_wide": (_I, [_P, _L, _L, _U, _U, _L, _P]),
+    "smj_trim": (_I, []),
+    "smj_scratch_bytes": (_L, []),
+    "smj_set_scratch_limit": (None, [_L]),
     "smj_zipf_zeta": (_D, [_L, _D]),
     "smj_dev_digest": (_I, [_P, _L, _I, _L, _P, _P]),
     "smj_dev_dist_sample": (_I, [_P, _L, _I, _I, _P, _L, _I, _I, _I, _P, _P]),
@@ -123,6 +127,21 @@ def load(build_if_missing=True):
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+def source_sha():
+    """sha256 (16 hex digits) of the library's sources (csrc/, include/): the
+    key under which a profile summary (profiles/pmc_traffic*.json) is valid
+    for the library built from this tree."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*")) + glob.glob(os.path.join(REPO_DIR, "include", "*.h")))
+    for f in files:
+        h.update(os.path.relpath(f, REPO_DIR).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def check(rc, where):

@@ -295,6 +295,23 @@ def msd_packb():
     return int(lib.smj_debug_msd_packb())
 
 
+def msd_wstage():
+    """Groups of the last MSD pipeline call sorted by the wide-span staged
+    kernel (msd_final_wstage_kernel: key spans over 4096 values)."""
+    lib = _lib.load()
+    if not hasattr(lib, "smj_debug_msd_wstage"):
+        return 0
+    lib.smj_debug_msd_wstage.restype = ctypes.c_int64
+    return int(lib.smj_debug_msd_wstage())
+
+
+def debug_wide_maxrun(rows=-1):
+    """Diagnostic: the wide-span staged kernel hands a group to the radix tier
+    when one of its bins holds more than `rows` rows (-1: the built-in limit;
+    0: every group)."""
+    _lib.load().smj_debug_wide_maxrun(int(rows))
+
+
 def msd_bigdev():
     """Oversized multi-key groups of the last MSD pipeline call sorted on the
     device (msd_big_stage_kernel); the other oversized ones took the host-driven
@@ -564,6 +581,19 @@ def gen_zipf(rows, row0=0, seed=3, domain=100_000_000, theta=0.9, device="cuda",
     return out
 
 
+def gen_wide(rows, row0=0, seed=1, plant_seed=1, plant_rows=0, device="cuda", out=None, stream=None):
+    """C3-wide synthetic table (SURVEY 8(d) stress input): full-range signed
+    int64 keys; with plant_rows > 0 a random third of the rows take the key of
+    a random row of the plant_seed table of plant_rows rows (R), so they join.
+    payload = global row index (smj_dev_gen_wide)."""
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty((rows, 2), dtype=torch.int64, device=device)
+    _lib.check(lib.smj_dev_gen_wide(_ptr(out), int(row0), int(rows), int(seed), int(plant_seed), int(plant_rows),
+                                    _stream(stream)), "smj_dev_gen_wide")
+    return out
+
+
 MASK64 = (1 << 64) - 1
 
 
@@ -634,6 +664,22 @@ def digest(table, pos0=0, stream=None):
     to the digest of the whole table (smj.h smj_dev_digest)."""
     d = digest_async(table, pos0, stream=stream)
     return int(d.item()) & MASK64
+
+
+def trim():
+    """smj_trim: return every device buffer the library holds (synchronises)."""
+    _lib.check(_lib.load().smj_trim(), "smj_trim")
+
+
+def scratch_bytes():
+    """Device bytes the library holds now (smj_scratch_bytes)."""
+    return int(_lib.load().smj_scratch_bytes())
+
+
+def set_scratch_limit(nbytes=-1):
+    """smj_set_scratch_limit: a call ending over `nbytes` of library scratch
+    trims before it returns (-1: keep scratch for the next call)."""
+    _lib.load().smj_set_scratch_limit(int(nbytes))
 
 
 def prof_enable(on=True):

@@ -202,7 +202,7 @@ def check_join(gR, gS, gJ):
     assert off == gJ.shape[0]
 
 
-def check_window(R, S, gR, gS, gJ, lo, hi):
+def check_window(R, S, gR, gS, gJ, lo, hi, sel=SEL):
     """Input rows with lo <= key <= hi (input order) through the C oracle ==
     the output slices holding those keys."""
     def window_in(T):
@@ -216,16 +216,16 @@ def check_window(R, S, gR, gS, gJ, lo, hi):
         return host(G[a:b])
 
     Rw, Sw = window_in(R), window_in(S)
-    Rs, Ss, J = ref_pipeline(Rw, Sw, 0, 0, (0, SEL), (0, SEL))
+    Rs, Ss, J = ref_pipeline(Rw, Sw, 0, 0, (0, sel), (0, sel))
     np.testing.assert_array_equal(window_out(gR), Rs)
     np.testing.assert_array_equal(window_out(gS), Ss)
     np.testing.assert_array_equal(window_out(gJ), J)
     return len(Rs) + len(Ss), len(J)
 
 
-def run_full(R, S):
+def run_full(R, S, sel=SEL):
     from smj import ops
-    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, SEL), (0, SEL))
+    gR, gS, gJ = ops.sort_merge_join(R, S, 0, 0, (0, sel), (0, sel))
     torch.cuda.synchronize()
     return gR, gS, gJ
 
@@ -248,6 +248,38 @@ def test_c5_full_size_one_gpu(gpu, oracle_built):
     check_window(R, S, gR, gS, gJ, int(gS[mid, 0]), int(gS[mid + 500_000, 0]))
 
 
+C3W_SEL = -(1 << 63)  # WHERE col0 > INT64_MIN: ~every row passes
+
+
+def test_c3_wide_full_size(gpu, oracle_built):
+    """SURVEY 8(d)'s C3-wide stress input at full size: |R| = |S| = 1e8,
+    full-range signed int64 keys (smj_dev_gen_wide), S planted with R's keys
+    in a random third of its rows.  No group fits the narrow-span tiers
+    (spans of ~2^45 keys per pass-B sub-bucket), so every group takes the
+    wide-key path; packed pass-B rows are off (keys span 2^64)."""
+    from smj import ops
+    n = 100_000_000
+    R = ops.gen_wide(n, seed=1)
+    S = ops.gen_wide(n, seed=2, plant_seed=1, plant_rows=n)
+    gR, gS, gJ = run_full(R, S, C3W_SEL)
+    groups = ops.msd_groups()
+    assert ops.msd_packb() == 0
+    check_sorted_selection(R, gR, C3W_SEL)
+    check_sorted_selection(S, gS, C3W_SEL)
+    check_join(gR, gS, gJ)
+    # ~n (1 - e^(-1/3)) distinct planted R rows (R's keys are distinct w.h.p.)
+    assert 0.27 * n < gJ.shape[0] < 0.30 * n, gJ.shape[0]
+    for q in (n // 7, n // 2):
+        lo = int(gR[q, 0])
+        hi = int(gR[q + 400_000, 0])
+        rows, j = check_window(R, S, gR, gS, gJ, lo, hi, C3W_SEL)
+        assert rows > 600_000 and j > 50_000
+    # the extremes of the key range, where signed order matters
+    check_window(R, S, gR, gS, gJ, -(1 << 63) + 1, int(gR[200_000, 0]), C3W_SEL)
+    check_window(R, S, gR, gS, gJ, int(gR[n - 200_000, 0]), (1 << 63) - 1, C3W_SEL)
+    print("c3-wide groups (dense, radix-tier, wide-tier, in-LDS LSD):", groups)
+
+
 def test_c4_full_size_one_gpu(gpu, oracle_built):
     """BASELINE C4's tables (1e9 x 1e9, keys iid uniform in [1, 3e9], seeds
     1 / 2, WHERE col0 > 5000) on ONE MI355X through the partitioned mode."""
@@ -263,6 +295,14 @@ def test_c4_full_size_one_gpu(gpu, oracle_built):
     lo = int(gR[n // 3, 0])
     rows, j = check_window(R, S, gR, gS, gJ, lo, lo + 1_500_000)
     assert rows > 500_000 and j > 0
+    # the library's scratch (part regions, two per-part sets: ~100 GB here) goes
+    # back to the device without smj_finalize, with the results still alive
+    # 
+    ops.trim()
+    assert ops.scratch_bytes() == 0
+    torch.cuda.empty_cache()
+    big = torch.empty(100 * 2 ** 30, dtype=torch.uint8, device=R.device)
+    del big
 
 
 @pytest.mark.parametrize("workload,stages", [("c3", 1), ("c5", 2), ("c4", 3)])

@@ -34,6 +34,11 @@ def table(rng, n, cols, kind, key_col, payload0):
         t = np.full((n, cols), 7, dtype=np.int64)
     elif kind == "wide":
         t = rng.integers(I64.min, I64.max, size=(n, cols), dtype=np.int64, endpoint=True)
+    elif kind == "widepool":  # full-range keys drawn from a fixed pool: repeats in and across tables
+        pool = np.random.default_rng(99).integers(I64.min, I64.max, size=50_000, dtype=np.int64, endpoint=True)
+        t = pool[rng.integers(0, pool.size, size=(n, cols))]
+    elif kind == "wide31":  # keys spanning < 2^31 (packed pass-B rows) with groups spanning > 4096 keys
+        t = rng.integers(-(1 << 31) + 1, (1 << 31) - 1, size=(n, cols), dtype=np.int64)
     elif kind == "extremes":
         vals = np.array([I64.min, -1, 0, 1, I64.max], dtype=np.int64)
         t = vals[rng.integers(0, 5, size=(n, cols))]
@@ -135,7 +140,14 @@ def test_packed_pass_b_rows(gpu, oracle_built, monkeypatch, mode, nr, ns, kind, 
     else:
         R = table(rng, nr, 2, kind, k1, 0)
         S = table(rng, ns, 2, kind, k2, pay0)
-    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, None)
+    # "spread": the wide-span staged kernel hands every group over, so that the
+    # radix tier runs on the unpacked copy (test_wide_span_groups_match_oracle
+    # covers the wide-span kernel itself on packed words)
+    ops.debug_wide_maxrun(0 if kind == "spread" else -1)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, None)
+    finally:
+        ops.debug_wide_maxrun(-1)
     assert ops.msd_packb() == expect, (ops.msd_packb(), ops.msd_groups())
     Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, None)
     np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
@@ -703,3 +715,46 @@ def test_heavy_keys_edge_cases(gpu, oracle_built, kc):
         np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
     assert ops.msd_stats()[0] > 0  # single-key groups streamed
+
+
+WSTAGE_CASES = [
+    # nr, ns, key1, key2, kind, select1, select2, maxrun override (-1: none), packed pass-B rows expected
+    (300_000, 300_000, 0, 0, "wide", None, None, -1, 0),
+    (400_000, 350_000, 0, 0, "widepool", None, None, -1, 0),                # ~8 occurrences per key
+    (250_000, 300_000, 1, 1, "widepool", (0, 0), (0, -(1 << 62)), -1, 0),   # key in column 1, WHEREs
+    (30_000, 400_000, 0, 0, "widepool", None, (0, 0), -1, 0),               # skewed: combined layout
+    (500_000, 500_000, 0, 0, "wide31", None, None, -1, 1),                  # packed words, wide groups
+    (300_000, 300_000, 0, 0, "widepool", None, None, 0, 0),                 # every group handed over
+    (200_000, 200_000, 0, 0, "wide31", (1, 150_000), None, 2, 1),           # hand-over on bins > 2 rows
+]
+
+
+@pytest.mark.parametrize("nr,ns,k1,k2,kind,s1,s2,maxrun,packed", WSTAGE_CASES)
+def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, s1, s2, maxrun, packed):
+    """Groups spanning more than 4096 keys (full-range keys: SURVEY 8(d)'s
+    C3-wide) through msd_final_wstage_kernel -- bins by key, rounds by (key,
+    group row), zip join by key within a bin -- and its hand-over to the radix
+    tier (maxrun override), bit for bit against the oracle."""
+    from smj import ops
+    rng = np.random.default_rng(nr + 3 * ns + k1)
+    R = table(rng, nr, 2, kind, k1, 0)
+    S = table(rng, ns, 2, kind, k2, 10 ** 8)
+    if kind in ("wide", "wide31"):  # plant R's keys in a third of S's rows
+        pick = rng.random(ns) < 1 / 3
+        S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
+    ops.debug_wide_maxrun(maxrun)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, s2)
+        torch.cuda.synchronize()
+        wst, tiers = ops.msd_wstage(), ops.msd_groups()
+    finally:
+        ops.debug_wide_maxrun(-1)
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, s2)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+    assert len(J) > 0
+    assert ops.msd_packb() == packed
+    assert wst > 0.9 * tiers[0], (wst, tiers)
+    if maxrun == 0:
+        assert tiers[1] == wst, tiers  # every wide group went on to the radix tier

@@ -235,6 +235,21 @@ def test_gen_uniform_matches_oracle(gpu, oracle_built):
     np.testing.assert_array_equal(host(got), oracle.gen_uniform(1_000_003, 12345, 2, 3_000_000))
 
 
+def test_gen_wide_matches_oracle(gpu, oracle_built):
+    """C3-wide generator: device == oracle restatement, full-range
+    keys, and a third of S's rows planted with R's keys."""
+    from smj import ops
+    n = 1_000_003
+    R = host(ops.gen_wide(n, row0=7, seed=1))
+    S = host(ops.gen_wide(n, row0=7, seed=2, plant_seed=1, plant_rows=n + 7))
+    np.testing.assert_array_equal(R, oracle.gen_wide(n, 7, 1))
+    np.testing.assert_array_equal(S, oracle.gen_wide(n, 7, 2, 1, n + 7))
+    assert R[:, 0].min() < -(1 << 62) and R[:, 0].max() > (1 << 62)
+    Rall = oracle.gen_wide(n + 7, 0, 1)
+    frac = np.isin(S[:, 0], Rall[:, 0]).mean()
+    assert 0.32 < frac < 0.345, frac
+
+
 def test_gen_zipf_shape(gpu):
     from smj import ops
     z = host(ops.gen_zipf(2_000_000, seed=3, domain=100_000_000, theta=0.9))

@@ -21,6 +21,8 @@ while [ -e "$OUT" ]; do OUT=$ROOT/gpurun_out/${TAG}_$i; i=$((i + 1)); done
 mkdir -p "$OUT"
 cd "$ROOT"
 export TMPDIR=/tmp
+# the library's source hash on the box: PMC summaries are keyed by it (tools/pmc_traffic.py)
+python3 -c "import sys; sys.path.insert(0, 'pim-sort-merge-join_amd'); from smj._lib import source_sha; print(source_sha())" > "$OUT/source_sha.txt" 2>/dev/null || true
 BA=${BENCH_ARGS:-}
 NOCPU="--cpu-sample 0 --cpu-mt 0"
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
@@ -62,6 +64,11 @@ for s in $STEPS; do
     largeh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so test_run largeh 900 $PYT tests/test_gpu_large.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
+    c3w)   run c3w 400 python bench.py --workload c3w $NOCPU $BA && summ "$OUT/c3w.out" c3w ;;
+    c3wv)  run c3wv 600 python bench.py --workload c3w $BA && summ "$OUT/c3wv.out" c3w ;;
+    c3w7)  run c3w7 300 python bench.py --workload c3w --rows 10000000 $NOCPU $BA && summ "$OUT/c3w7.out" c3w_1e7 ;;
+    c4v)   run c4v 900 python bench.py --workload c4 --steps 5 --warmup 2 --cpu-sample 0 $BA && summ "$OUT/c4v.out" c4 ;;
+    c5v)   run c5v 900 python bench.py --workload c5 --steps 5 --warmup 2 --cpu-sample 0 $BA && summ "$OUT/c5v.out" c5 ;;
     c4)    run c4 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4.out" c4 ;;
     c5)    run c5 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c5.out" c5 ;;
     c4old) SMJ_PART1C=0 run c4old 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU $BA && summ "$OUT/c4old.out" c4old ;;

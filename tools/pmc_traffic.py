@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--runs", type=int, default=5,
                     help="bench.py steps the PMC runs executed: warmup + steps + profiling steps (1 + 2 + 2)")
     ap.add_argument("-o", "--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--source-sha", default=None,
+                    help="smj._lib.source_sha() of the tree the PMC runs used (default: <fetch_dir>/../source_sha.txt "
+                         "written by tools/gpu_run.sh on the box, else this tree's)")
     a = ap.parse_args()
     base = os.path.splitext(a.out)[0]
     fcsv, wcsv = base + "_fetch_summary.csv", base + "_write_summary.csv"
@@ -108,7 +111,18 @@ def main():
         w = write.get(t, 0.0) / max(nw.get(t, 0), 1)
         kernels[t] = {"launches": nf.get(t, 0), "fetch_kib_raw": round(f, 1),
                       "write_kib": round(w, 1), "hbm_bytes_per_launch": round((2 * f + w) * 1024)}
-    out = {"rows_per_table": a.rows, "workload": a.workload, "runs": a.runs, "source": [fcsv, wcsv],
+    sha = a.source_sha
+    side = os.path.join(os.path.dirname(os.path.normpath(a.fetch_dir)), "source_sha.txt")
+    if sha is None and os.path.exists(side):
+        sha = open(side).read().strip()
+    if sha is None:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "pim-sort-merge-join_amd"))
+        from smj._lib import source_sha
+        sha = source_sha()
+    out = {"rows_per_table": a.rows, "workload": a.workload, "runs": a.runs, "source_sha": sha,
+           "source": [fcsv, wcsv],
            "raw_runs": [a.fetch_dir, a.write_dir],
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB per scope launch (gfx950: FETCH_SIZE "
                          "counts half of a wide coalesced read; MI355X_MICROARCH.md, HBM)",
