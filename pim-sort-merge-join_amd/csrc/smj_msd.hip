@@ -942,7 +942,8 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
     const int a = blockIdx.x, t = threadIdx.x;
     if (t == 0) s_skew = p.plan->skew >= kHeavySkew ? 1u : 0u;
     __syncthreads();
-    if (t + 1 < kSplA && p.spl[t] == p.spl[t + 1]) s_skew = 1;  // benign race: all write 1
+    for (int i = t; i + 1 < kSplA; i += kHeavyThreads)  // (every splitter pair: SMJ_BITS_A=9 has 511 splitters)
+        if (p.spl[i] == p.spl[i + 1]) s_skew = 1;  // benign race: all write 1
     __syncthreads();
     const int64_t *spl = p.spl;
     const bool own = a >= 1 && a < kSplA && spl[a] == spl[a - 1] && (a == 1 || spl[a - 2] != spl[a - 1]);

@@ -612,10 +612,9 @@ PACK = os.environ.get("SMJ_DIST_PACK", "1") != "0"
 PACK_MAX_ROWS = 160_000_000  # smj_dev_sort_merge_join_begin_pk's limit per table; larger stages are unpacked first
 
 
-def _key_base(est, t):
-    """The middle of table t's sampled keys over every rank (the gathered
-    sample buffers of choose_splitters), 0 without samples."""
-    import numpy as np
+def _key_range(est, t):
+    """(min, max) of table t's sampled keys over every rank (the gathered
+    sample buffers of choose_splitters), None without samples."""
     a, H, nt = est["all"], est["H"], est["nt"]
     lo, hi = None, None
     for r in range(a.shape[0]):
@@ -625,7 +624,27 @@ def _key_base(est, t):
             k = a[r, o: o + c[t]]
             lo = int(k.min()) if lo is None else min(lo, int(k.min()))
             hi = int(k.max()) if hi is None else max(hi, int(k.max()))
-    return 0 if lo is None else (lo + hi) // 2
+    return None if lo is None else (lo, hi)
+
+
+def _key_base(est, t):
+    """The middle of table t's sampled keys over every rank, 0 without samples."""
+    r = _key_range(est, t)
+    return 0 if r is None else (r[0] + r[1]) // 2
+
+
+# A packed key is (int32)(key - base): with the base in the middle of the
+# sampled keys, a sample spanning 2^31 or more already shows keys that cannot
+# fit, and every call would pay a packed partition that is thrown away plus an
+# unpacked re-partition (ADVICE r5).  Such tables are sent plain from the start,
+# and a table whose packing failed on any rank is remembered (by tensor, shape
+# and key column) so that the next calls on it do not try again.
+PACK_SPAN = 1 << 31
+_NOPACK = set()
+
+
+def _pack_id(T, k):
+    return (T.data_ptr(), tuple(T.shape), int(k)) if T.is_cuda else None
 
 
 def _unpacked(ops, t, key, pack):
@@ -749,7 +768,13 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
         a = est["all"]
         big = max(int(a[:, 1 + 2 + x].sum()) for x in range(2)) * smax / world * 1.25
         can_pack = big <= PACK_MAX_ROWS
-    packs = [(_key_base(est, x), 0) if can_pack and T.shape[1] == 2 else None for x, T in enumerate((R, S))]
+    packs = []
+    for x, (T, k) in enumerate(((R, k1), (S, k2))):
+        kr = _key_range(est, x)
+        ok = (can_pack and T.shape[1] == 2 and _pack_id(T, k) not in _NOPACK
+              and (kr is None or kr[1] - kr[0] < PACK_SPAN))
+        packs.append(((kr[0] + kr[1]) // 2 if kr else 0, 0) if ok else None)
+    pack_fallbacks = 0
     tr("bounds, regions, key bases")
     part = [_partition(ops, R, bounds, cnt[0], own[0], k1, sc1, sv1, packs[0])]
     gR = _HostGather(cnt[0], world, group)
@@ -785,6 +810,10 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
             T, k, sc, sv = tabs[t]
             buf, reg = _repartition(ops, T, bounds, k, sc, sv), None
             packs[t] = None
+            nonlocal pack_fallbacks
+            pack_fallbacks += 1
+            if any(allc[r][nb] & 4 for r in range(world)) and _pack_id(T, k) is not None:
+                _NOPACK.add(_pack_id(T, k))
         elif reg is not None and allc[rank][nb] & 1:  # a region overflowed: the counting partition
             T, k, sc, sv = tabs[t]
             buf, reg = _repartition(ops, T, bounds, k, sc, sv), None
@@ -879,7 +908,8 @@ def _sort_merge_join(R, S, sc1, sv1, sc2, sv2, k1, k2, group, ops, samples, stat
                  for d in range(world)]
         mean = sum(loads) / world
         stats.update(rows_in=rows_in, loads=loads, load_max_over_mean=(max(loads) / mean) if mean else 1.0,
-                     cuts=cuts, buckets=nb, stages=K)
+                     cuts=cuts, buckets=nb, stages=K, exchange_packed=[p is not None for p in packs],
+                     pack_fallbacks=pack_fallbacks)
     tr.end()
     if into:
         return J[:at]

@@ -6,6 +6,7 @@ orchestration: splitter choice, stable bucket scatter semantics, the
 all_to_all exchange in source-rank order, the per-rank radix base, and that
 concatenating rank outputs in rank order reproduces cpu_app.c's result.
 """
+import json
 import os
 import socket
 
@@ -133,6 +134,8 @@ def _worker(rank, world, port, R, S, cfg, outdir):
     np.save(os.path.join(outdir, f"rank{rank}.npy"), out.cpu().numpy())
     if rank == 0:
         np.save(os.path.join(outdir, "load.npy"), np.array([stats["load_max_over_mean"]]))
+        with open(os.path.join(outdir, "stats.json"), "w") as f:
+            json.dump({k: stats.get(k) for k in ("exchange_packed", "pack_fallbacks", "stages")}, f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -150,6 +153,9 @@ def make_tables(kind, n):
         R, S = oracle.gen_uniform(n, 0, 1, 3 * n), oracle.gen_uniform(n, 0, 2, 3 * n)
         R[:, 1] = rng.integers(-(1 << 62), 1 << 62, n)
         S[:, 1] = rng.integers(-(1 << 62), 1 << 62, n)
+        return R, S
+    if kind == "widekeys":  # full-range keys (C3-wide): the sample's span rules packing out up front
+        R, S = oracle.gen_wide(n, 0, 1), oracle.gen_wide(n, 0, 2, 1, n)
         return R, S
     if kind == "skew":  # one key carries most rows, negative keys too
         R = rng.integers(-1000, 1000, size=(n, 2)).astype(np.int64)
@@ -242,7 +248,13 @@ def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
     # messages over ~2 GiB, profiles/r04/r04e): hundreds of pieces per stage
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "max_msg": 65536}),
     # payloads over int32: packing falls back to plain rows on every rank
-    ("widepay", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True}),
+    ("widepay", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "expect_pack": (
+        [False, False], 2)}),
+    # full-range keys: not packed to begin with (no thrown-away packed partition)
+    ("widekeys", {"select": (0, -(1 << 63), 0, -(1 << 63)), "keys": (0, 0), "samples": 4096, "gpu": True,
+                  "expect_pack": ([False, False], 0)}),
+    ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "expect_pack": (
+        [True, True], 0)}),
     # the packed exchange turned off
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "pack": "0"}),
 ])
@@ -257,6 +269,9 @@ def test_distributed_rccl_loopback_one_gpu(tmp_path, oracle_built, pkg_built, mo
     if cfg.get("pack"):
         monkeypatch.setenv("SMJ_DIST_PACK", cfg["pack"])
     _run_and_check(tmp_path, 1, kind, dict(cfg, backend="nccl", loopback=True), 1_000_000)
+    if cfg.get("expect_pack"):
+        st = json.loads((tmp_path / "stats.json").read_text())
+        assert (st["exchange_packed"], st["pack_fallbacks"]) == tuple(cfg["expect_pack"]), st
 
 
 def test_heavy_key_is_split_by_occurrence(tmp_path, oracle_built):

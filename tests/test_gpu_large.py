@@ -350,6 +350,10 @@ def test_repeated_partitioned_calls_agree(gpu):
             ops.prof_enable(False)
             ops.prof_report()
         d = (gR.shape[0], gS.shape[0], gJ.shape[0], ops.digest(gR), ops.digest(gS), ops.digest(gJ))
+        if n not in ref:  # the first call of each size against the property checks, not only itself
+            check_sorted_selection(R, gR, SEL)
+            check_sorted_selection(S, gS, SEL)
+            check_join(gR, gS, gJ)
         assert ref.setdefault(n, d) == d, (n, prof, ref[n], d)
         del R, S, gR, gS, gJ
         torch.cuda.empty_cache()
