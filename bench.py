@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--workload", default="c3", choices=["c3", "c3w", "c4", "c5"],
                    help="c3 (default, the metric's config); c3w: C3-wide (full-range keys); "
                         "c4 / c5: BASELINE's 1e9-row tables on one GPU")
+    p.add_argument("--key-range", type=int, default=0,
+                   help="c3 / c4: keys iid uniform in [1, K] instead of [1, 3n] (a probe of other key densities)")
     p.add_argument("--cpu-sample", type=int, default=196608,
                    help="rows per table for the single-core cpu_app.c baseline (0 = skip)")
     p.add_argument("--cpu-mt", type=int, default=1,
@@ -228,7 +230,7 @@ def main():
         NR = NS = 1_000_000_000
     else:
         NR, NS = 100_000_000, 1_000_000_000
-    key_range = {"c5": 100_000_000, "c3w": None}.get(a.workload, 3 * NR)  # C5: the Zipf domain; c3w: 2^64
+    key_range = {"c5": 100_000_000, "c3w": None}.get(a.workload, a.key_range or 3 * NR)  # C5: the Zipf domain; c3w: 2^64
 
     def shard(N):  # this rank's contiguous slice of a table of N global rows
         if not strong:

@@ -1035,6 +1035,10 @@ __global__ __launch_bounds__(kHeavyThreads) void msd_heavy_kernel(const MsdHeavy
 #ifndef SMJ_PACK_HEAVY
 #define SMJ_PACK_HEAVY 0  // 1: packed pass-B rows with heavy keys too (C5 +1.7 ms, r05zzp; the single-key tier reads words)
 #endif
+constexpr uint32_t kWideSkew = 256;  // repeated sampled keys that keep sparse buckets narrow (msd_bases)
+#ifndef SMJ_WIDE_FILL
+#define SMJ_WIDE_FILL 65  // percent (0: never)
+#endif
 constexpr int kBasesWaves = kOffsA / 64;
 __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams p) {
     __shared__ uint32_t s_wsum[kBasesWaves];
@@ -1131,7 +1135,22 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             // exact span of every group
             const uint64_t w = s32 ? ((1ull << 32) + s32 - 1u) / s32 + 1u
                                    : (uint64_t)((((unsigned __int128)1 << 64) + scale - 1u) / scale) + 1u;
-            const uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
+            uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
+            // narrow groups (<= kStageRange keys: the staged kernel) of `span`
+            // sub-buckets hold ~span Lm / D rows per table; well under a full
+            // group, full groups spanning more keys for the wide-span staged
+            // kernel cost less (round 6, r06g: C3's tables with keys over
+            // [1, 1e9] made groups of two sub-buckets, msd_final 3.3 ms against
+            // 1.6 at [1, 3e8] and 2.1 on wide groups).  SMJ_WIDE_FILL = the
+            // narrow fill (percent of kFill) below which a bucket goes wide.
+            // Not when the pass-A sample repeats many keys (plan->skew over
+            // kWideSkew of its ~8192): few distinct keys with long equal-key
+            // runs fill the narrow groups whatever the interval, and the wide
+            // kernel hands bins over 32 rows on.  (Joining tables repeat a few:
+            // an S key sampled together with its R partner.)
+            if (w <= (uint64_t)kStageRange && Lm > 0 && p.plan->skew < kWideSkew &&
+                span * Lm * 100u < (uint64_t)SMJ_WIDE_FILL * kFill * D)
+                span = ((uint64_t)1 << 48) / w;
             maxspan = span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
         }
     }
@@ -2133,7 +2152,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
         const uint64_t w = b0.scale == 0 ? 1ull
                            : b0.s32      ? ((1ull << 32) + b0.s32 - 1u) / b0.s32 + 1u
                                          : (uint64_t)((((unsigned __int128)1 << 64) + b0.scale - 1u) / b0.scale) + 1u;
-        comb = comb && w <= (uint64_t)kStageRange;
+        comb = comb && w * (uint64_t)b0.maxspan <= (uint64_t)kStageRange;  // (msd_bases: not a wide bucket)
         for (int x = 0; x < p.ntab; x++)
             comb = comb && (p.bk[x][a].L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x] <= (uint32_t)kStList;
     }
@@ -4093,7 +4112,12 @@ __device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
         if (ok) {
             st_emit<COMB, true>(p, g, gi, sm, wsb, mmask, part, sm.k64);
         } else {  // a bin over SMJ_ST_MAXRUN rows: the radix tier's (nothing was written)
-            if (opaque_tid() == 0) p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            if (opaque_tid() == 0) {
+                if (g.nR > (uint32_t)kGroupCap || (p.ntab > 1 && g.nS > (uint32_t)kGroupCap))
+                    atomicOr(&p.plan->err, 4u);  // over the radix tier's LDS (combined groups are never wide)
+                else
+                    p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
+            }
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
             for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
         }

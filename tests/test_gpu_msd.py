@@ -39,6 +39,8 @@ def table(rng, n, cols, kind, key_col, payload0):
         t = pool[rng.integers(0, pool.size, size=(n, cols))]
     elif kind == "wide31":  # keys spanning < 2^31 (packed pass-B rows) with groups spanning > 4096 keys
         t = rng.integers(-(1 << 31) + 1, (1 << 31) - 1, size=(n, cols), dtype=np.int64)
+    elif kind == "sparse":  # keys over [1, 1e9]: pass-B sub-buckets of ~1000-4000 keys -- wide groups (msd_bases)
+        t = rng.integers(1, 10 ** 9, size=(n, cols), dtype=np.int64, endpoint=True)
     elif kind == "extremes":
         vals = np.array([I64.min, -1, 0, 1, I64.max], dtype=np.int64)
         t = vals[rng.integers(0, 5, size=(n, cols))]
@@ -726,6 +728,7 @@ WSTAGE_CASES = [
     (500_000, 500_000, 0, 0, "wide31", None, None, -1, 1),                  # packed words, wide groups
     (300_000, 300_000, 0, 0, "widepool", None, None, 0, 0),                 # every group handed over
     (200_000, 200_000, 0, 0, "wide31", (1, 150_000), None, 2, 1),           # hand-over on bins > 2 rows
+    (300_000, 300_000, 0, 0, "sparse", None, None, -1, 1),                  # narrow sub-buckets, too few rows
 ]
 
 
@@ -739,7 +742,7 @@ def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, 
     rng = np.random.default_rng(nr + 3 * ns + k1)
     R = table(rng, nr, 2, kind, k1, 0)
     S = table(rng, ns, 2, kind, k2, 10 ** 8)
-    if kind in ("wide", "wide31"):  # plant R's keys in a third of S's rows
+    if kind in ("wide", "wide31", "sparse"):  # plant R's keys in a third of S's rows
         pick = rng.random(ns) < 1 / 3
         S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
     ops.debug_wide_maxrun(maxrun)

@@ -64,6 +64,9 @@ for s in $STEPS; do
     largeh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so test_run largeh 900 $PYT tests/test_gpu_large.py ;;
     c3)    run c3 400 python bench.py $BA && summ "$OUT/c3.out" c3 ;;
     quick) run quick 300 python bench.py $NOCPU $BA && summ "$OUT/quick.out" c3 ;;
+    krange) for k in 300000000 1000000000 2147483648 4000000000 8000000000 30000000000 1000000000000; do
+              run kr$k 300 python bench.py --key-range $k $NOCPU && summ "$OUT/kr$k.out" c3_keyrange_$k
+            done ;;
     c3w)   run c3w 400 python bench.py --workload c3w $NOCPU $BA && summ "$OUT/c3w.out" c3w ;;
     c3wv)  run c3wv 600 python bench.py --workload c3w $BA && summ "$OUT/c3wv.out" c3w ;;
     c3w7)  run c3w7 300 python bench.py --workload c3w --rows 10000000 $NOCPU $BA && summ "$OUT/c3w7.out" c3w_1e7 ;;
