@@ -3321,10 +3321,10 @@ __device__ unsigned long long g_st_sub[8];
         st_t = t_;                                                  \
     }
 
-template <bool COMB, bool PK>
+template <bool COMB, bool PK, class SM>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                                const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
-                                               StSmem &sm);
+                                               SM &sm);
 
 // run lists from the offsB values (union region), then the row gathers of
 // group g into registers (group row v = tid + k * kStThreads).  Row v's range
@@ -3332,26 +3332,26 @@ __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const Ms
 // non-empty range starting in (64b, v] (bitmap word + at[]; the list also
 // holds the group's empty ranges, so a popcount of the bitmap would not
 // index it).  S's ranges start at group row nR + their table row.
-template <bool COMB, bool PK>
+template <bool COMB, bool PK, class SM>
 __device__ __forceinline__ void st_issue(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
-                                         const uint32_t (&o1)[2], i64x2 (&rows)[kStIt], StSmem &sm, int &wsb) {
+                                         const uint32_t (&o1)[2], i64x2 (&rows)[kStIt], SM &sm, int &wsb) {
     const uint32_t tid = opaque_tid();
     for (uint32_t i = tid; i < kStRows / 32; i += kStThreads) sm.L.starts[i] = 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
     uint32_t tot;
     const uint32_t ex = block_excl_scan_nb<kStWaves>(len[0] | (len[1] << 16), sm.wsum[wsb], &tot);  // + barrier
     wsb ^= 1;
-    st_issue_lists<COMB, PK>(p, g, o0, o1, ex, rows, sm);
+    st_issue_lists<COMB, PK, SM>(p, g, o0, o1, ex, rows, sm);
 }
 
 // st_issue after the run-length scan: ex = this thread's exclusive prefix of
 // (len R | len S << 16), the start bitmap zeroed and ordered by a barrier.
 // PK: tempB holds packed words (MsdPlan::packB); a row is rebuilt from its
 // word and the group's base (the group spans <= kStRange keys)
-template <bool COMB, bool PK>
+template <bool COMB, bool PK, class SM>
 __device__ __forceinline__ void st_issue_lists(const MsdFinalParams &p, const MsdGroup &g, const uint32_t (&o0)[2],
                                                const uint32_t (&o1)[2], uint32_t ex, i64x2 (&rows)[kStIt],
-                                               StSmem &sm) {
+                                               SM &sm) {
     const uint32_t tid = opaque_tid(), lane = tid & 63;
     unsigned long long st_t = (SMJ_STAMPS && (p.dbg & 1)) ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t len[2] = {o1[0] - o0[0], o1[1] - o0[1]};
@@ -3749,8 +3749,9 @@ __device__ __forceinline__ void st_emit(const MsdFinalParams &p, const MsdGroup 
 // no loop -- a dynamic-count load loop here would make hipcc's waitcnt pass
 // give up counting, and every group's prefetched rows would then be consumed
 // behind a vmcnt(0) that also drains the previous group's stores
+template <class SM>
 __device__ __forceinline__ void st_load_recs(const MsdFinalParams &p, int64_t g0, int64_t gs, int64_t t0,
-                                             int64_t cnt, StSmem &sm, int h) {
+                                             int64_t cnt, SM &sm, int h) {
     constexpr int WORDS = sizeof(MsdGroup) / 8;
     static_assert(kStRecs * WORDS <= kStThreads, "at most one record word per thread");
     int64_t *dst = reinterpret_cast<int64_t *>(&sm.recs[h * kStRecs]);
@@ -3895,18 +3896,56 @@ __global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_stage_kerne
 // order each bin by (key, group row) -- the narrow kernel's equal-residual
 // rounds with a key compare -- and the zip join by key within each bin
 // (cpu_app.c:204-266: occurrence i of a key in R pairs with occurrence i in
-// S).  The full keys cost 16 KiB of LDS: two workgroups per CU.  A bin over
-// SMJ_ST_MAXRUN rows (keys clustered inside the group's interval) hands the
-// group to the radix tier before anything is written.
-struct StwSmem : StSmem {
-    int64_t k64[kStRows];  // keys, group-row order
+// S).  Staging the keys costs LDS: layouts below.  A bin over SMJ_ST_MAXRUN
+// rows (keys clustered inside the group's interval) hands the group to the
+// radix tier before anything is written.
+// LDS layouts of the wide-span kernels: PayT = the staged other column,
+// KT = the staged key (int64; uint32 = key - group base with packed pass-B
+// rows, whose keys lie within 2^32 of every group base), HB = bins per table.
+// <int32, uint32, 4096> (packed rows) and <int32, int64, 2048> (rows whose
+// other column fits int32, MsdPlan::nopack == 0) take 50.7 KiB: three
+// workgroups per CU, as the narrow kernel; <int64, int64, 4096> (any rows)
+// 66.6 KiB: two.
+template <class PayT, class KT, int HB>
+struct StwSmemT {
+    PayT pay[kStRows];              // other column, group-row order
+    KT kk[kStRows];                 // keys, group-row order
+    uint32_t key[kStRows];          // sort words bin << kStIdx | group row, sorted
+    uint32_t hist[2][HB / 2];       // per table, packed u16 bins
+    union {
+        struct {
+            uint2 list[2][kStList];
+            uint16_t at[kStRows];
+            uint32_t starts[kStRows / 32];
+            uint16_t btab[kStRows / 64];
+        } L;
+        uint32_t match[kGroupCap];
+    };
+    MsdGroup recs[2 * kStRecs];
+    uint32_t wsum[2][kStWaves];
+    uint32_t wlen[kStWaves];
+    uint32_t wmax[2][kStWaves];
+    static constexpr int kBins = HB;
+    using PayType = PayT;
 };
+using StwSmemP = StwSmemT<int32_t, uint32_t, kStRange>;      // packed pass-B rows
+using StwSmemR = StwSmemT<int32_t, int64_t, kStRange / 2>;   // 16-B rows, other column in int32
+using StwSmem64 = StwSmemT<int64_t, int64_t, kStRange>;      // 16-B rows
+
+template <class SM>
+__device__ __forceinline__ int64_t stw_key(const SM &sm, const MsdGroup &g, uint32_t v) {
+    if constexpr (sizeof(sm.kk[0]) == 4) return g.base + (int64_t)sm.kk[v];
+    else return (int64_t)sm.kk[v];
+}
 
 // stage + bin sort + in-bin rounds of wide group g, then the zip join lookups
-template <bool COMB, bool PK>
+template <bool COMB, bool PK, class SM>
 __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup &g, const i64x2 (&rows)[kStIt],
-                                         StwSmem &sm, int &wsb, uint32_t &mmask, uint32_t (&part)[kStIt],
+                                         SM &sm, int &wsb, uint32_t &mmask, uint32_t (&part)[kStIt],
                                          const uint32_t (&no0)[2], const uint32_t (&no1)[2], uint32_t &nex) {
+    constexpr int HB = SM::kBins;
+    constexpr int BSH = HB == kStRange ? 0 : HB == kStRange / 2 ? 1 : 2;  // bins from the record's kStRange-bin scale
+    static_assert(HB == (kStRange >> BSH), "bins per table");
     const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
     const StSplit<COMB> L(p, g);
     const uint32_t nR = L.nR, nS = L.nS, sp = L.sp;
@@ -3923,18 +3962,19 @@ __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup
             const int kc = x ? kc1 : kc0;
             // PK: the packed word's key half is exact from the base (packB: every key
             // within 2^32 of every group base)
-            const int64_t key = PK ? g.base + (int64_t)(uint32_t)((uint32_t)rows[k].x - (uint32_t)g.base)
-                                   : st_key(rows[k], kc);
-            sm.pay[v] = PK ? (int64_t)(int32_t)(uint32_t)((uint64_t)rows[k].x >> 32) : kc ? rows[k].x : rows[k].y;
-            sm.k64[v] = key;
-            const uint32_t bin = min((uint32_t)__umul64hi((uint64_t)key - (uint64_t)g.base, bscale),
-                                     (uint32_t)kStRange - 1u);
+            const uint64_t r = PK ? (uint64_t)((uint32_t)rows[k].x - (uint32_t)g.base)
+                                  : (uint64_t)st_key(rows[k], kc) - (uint64_t)g.base;
+            const int64_t pay = PK ? (int64_t)(int32_t)(uint32_t)((uint64_t)rows[k].x >> 32) : kc ? rows[k].x : rows[k].y;
+            sm.pay[v] = (typename SM::PayType)pay;
+            if constexpr (sizeof(sm.kk[0]) == 4) sm.kk[v] = (uint32_t)r;
+            else sm.kk[v] = (int64_t)((uint64_t)g.base + r);
+            const uint32_t bin = min((uint32_t)(__umul64hi(r, bscale) >> BSH), (uint32_t)HB - 1u);
             const uint32_t sh = 16u * (bin & 1u);
             w[k] = (bin << 16) | ((atomicAdd(&sm.hist[x ? 1 : 0][bin >> 1], 1u << sh) >> sh) & 0xffffu);
         }
     }
     __syncthreads();
-    constexpr int W = kStRange / 2 / kStThreads;
+    constexpr int W = HB / 2 / kStThreads;
     uint32_t tot = 0, mrun = 0;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
@@ -3995,7 +4035,8 @@ __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup
     // rows of one bin were placed in atomic order: odd-even rounds (as many as
     // the longest bin) order each bin by (key, group row) -- group rows ascend
     // in input order within a table, so this is the stable order.  A pair
-    // across the R / S boundary never swaps.
+    // across the R / S boundary never swaps.  (kk: the key, or its offset from
+    // the group base -- the same order.)
     for (uint32_t rd = 0; rd < fl; rd++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -4003,7 +4044,7 @@ __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup
             if (L.valid_pos(q) && L.valid_pos(q + 1) && (q < sp) == (q + 1 < sp)) {
                 const uint32_t a = sm.key[q], b = sm.key[q + 1];
                 if ((a >> kStIdx) == (b >> kStIdx)) {
-                    const int64_t ka = sm.k64[a & kStIdxMask], kb = sm.k64[b & kStIdxMask];
+                    const auto ka = sm.kk[a & kStIdxMask], kb = sm.kk[b & kStIdxMask];
                     if (ka > kb || (ka == kb && a > b)) {
                         sm.key[q] = b;
                         sm.key[q + 1] = a;
@@ -4031,18 +4072,17 @@ __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup
                 const uint32_t wi = sm.key[i], bin = wi >> kStIdx, sh = 16u * (bin & 1u);
                 const uint32_t hS = sm.hist[1][bin >> 1];
                 const uint32_t sS = (hS >> sh) & 0xffffu;
-                const uint32_t eS = (bin & 1u) ? ((bin + 1u < (uint32_t)kStRange) ? (sm.hist[1][(bin + 1) >> 1] & 0xffffu)
-                                                                                 : nS)
+                const uint32_t eS = (bin & 1u) ? ((bin + 1u < (uint32_t)HB) ? (sm.hist[1][(bin + 1) >> 1] & 0xffffu) : nS)
                                                : (hS >> 16);
                 if (sS == eS) continue;  // no S row in the bin
-                const int64_t kk = sm.k64[wi & kStIdxMask];
+                const auto kk = sm.kk[wi & kStIdxMask];
                 const uint32_t sR = (sm.hist[0][bin >> 1] >> sh) & 0xffffu;
                 uint32_t f = i;
-                while (f > sR && sm.k64[sm.key[f - 1] & kStIdxMask] == kk) f--;
+                while (f > sR && sm.kk[sm.key[f - 1] & kStIdxMask] == kk) f--;
                 const uint32_t occ = i - f;
                 uint32_t j = sS;
-                while (j < eS && sm.k64[kS[j] & kStIdxMask] < kk) j++;
-                if (j + occ < eS && sm.k64[kS[j + occ] & kStIdxMask] == kk) {
+                while (j < eS && sm.kk[kS[j] & kStIdxMask] < kk) j++;
+                if (j + occ < eS && sm.kk[kS[j + occ] & kStIdxMask] == kk) {
                     part[q] = j + occ;
                     mmask |= 1u << q;
                 }
@@ -4052,12 +4092,71 @@ __device__ __forceinline__ bool stw_sort(const MsdFinalParams &p, const MsdGroup
     return true;
 }
 
+// sorted rows out (coalesced), join rows out (word-coalesced); the histogram
+// is zeroed for the next group here (st_emit's shape, keys from kk)
+template <bool COMB, class SM>
+__device__ __forceinline__ void stw_emit(const MsdFinalParams &p, const MsdGroup &g, int64_t gi, SM &sm, int &wsb,
+                                         uint32_t mmask, const uint32_t (&part)[kStIt]) {
+    const int tid = opaque_tid();
+    const StSplit<COMB> L(p, g);
+    {
+        uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
+        for (int i = tid; i < SM::kBins / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+    }
+    i64x2 *dR = reinterpret_cast<i64x2 *>(p.tab[0].out) + g.outR;
+    i64x2 *dS = reinterpret_cast<i64x2 *>(p.tab[1].out) + g.outS - L.sp;  // S row q - sp
+    const int kc0 = p.tab[0].key, kc1 = p.tab[1].key;
+#pragma unroll
+    for (int k = 0; k < kStIt; k++) {
+        const uint32_t q = tid + k * kStThreads;
+        if (L.valid(k, q)) {
+            const bool x = L.is_s(k, q);
+            const uint32_t v = sm.key[q] & kStIdxMask;
+            const int64_t key = stw_key(sm, g, v), pay = (int64_t)sm.pay[v];
+            const int kc = x ? kc1 : kc0;
+            i64x2 r;
+            r.x = kc ? pay : key;
+            r.y = kc ? key : pay;
+            __builtin_nontemporal_store(r, (x ? dS : dR) + q);
+        }
+    }
+    if (!p.join) return;
+    const uint32_t *kS = sm.key + L.sp;
+    uint32_t total;
+    uint32_t o = block_excl_scan_nb<kStWaves>((uint32_t)__popc(mmask), sm.wsum[wsb], &total);
+    wsb ^= 1;
+    if (tid == 0) p.counts[gi] = total;
+    if (total == 0) return;
+    constexpr int JI = COMB ? kStIt : kStIt / 2;
+#pragma unroll
+    for (int q = 0; q < JI; q++)
+        if ((mmask >> q) & 1u) sm.match[o++] = (((uint32_t)tid * JI + q) << kStIdx) | part[q];
+    __syncthreads();
+    int64_t *dst = p.slots + (int64_t)g.outR * 3;
+    constexpr int EMIT_IT = (3 * kGroupCap + kStThreads - 1) / kStThreads;
+#pragma unroll
+    for (int it = 0; it < EMIT_IT; it++) {
+        const uint32_t wd = tid + it * kStThreads;
+        if (wd < total * 3u) {
+            const uint32_t row = wd / 3u, c = wd - row * 3u;
+            const uint32_t m = sm.match[row];
+            int64_t val;
+            if (c < 2) {
+                const uint32_t v = sm.key[m >> kStIdx] & kStIdxMask;
+                val = (int)c == kc0 ? stw_key(sm, g, v) : (int64_t)sm.pay[v];
+            } else {
+                val = (int64_t)sm.pay[kS[m & kStIdxMask] & kStIdxMask];
+            }
+            __builtin_nontemporal_store(val, dst + wd);
+        }
+    }
+}
+
 // persistent over the dense groups with the staged kernel's XCD-aware
 // schedule, taking only the wide groups (stw_ok) the staged kernel skipped
-constexpr int kStwGrid = 512;  // two workgroups per CU (LDS)
 int g_wide_maxrun = -1;
-template <bool COMB, bool PK>
-__device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
+template <bool COMB, bool PK, class SM>
+__device__ __forceinline__ void stw_body(const MsdFinalParams &p, SM &sm) {
     const int64_t ng = p.plan->ngroups;
     const int64_t gs = gridDim.x / kXcdSlots;
     const int64_t xr = (ng + kXcdSlots - 1) / kXcdSlots;
@@ -4066,7 +4165,7 @@ __device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
     const int64_t cnt = x1 > g0 ? (x1 - g0 + gs - 1) / gs : 0;
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
-        for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = opaque_tid(); i < SM::kBins / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
     }
     if (0 < cnt) st_load_recs(p, g0, gs, 0, cnt, sm, 0);
     if (kStRecs < cnt) st_load_recs(p, g0, gs, kStRecs, cnt, sm, 1);
@@ -4103,14 +4202,14 @@ __device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
         uint32_t mmask = 0, part[kStIt], nex;
         const bool ok = stw_sort<COMB, PK>(p, g, cur, sm, wsb, mmask, part, o0, o1, nex);
         // the join lookups read the histogram, which does not alias the list
-        // region st_issue_lists writes; its barrier orders them before st_emit
-        // zeroes the histogram
+        // region st_issue_lists writes; its barrier orders them before the
+        // emit zeroes the histogram
         if (nfit)
             st_issue_lists<COMB, PK>(p, gn, o0, o1, nex, cur, sm);
         else
             __syncthreads();
         if (ok) {
-            st_emit<COMB, true>(p, g, gi, sm, wsb, mmask, part, sm.k64);
+            stw_emit<COMB>(p, g, gi, sm, wsb, mmask, part);
         } else {  // a bin over SMJ_ST_MAXRUN rows: the radix tier's (nothing was written)
             if (opaque_tid() == 0) {
                 if (g.nR > (uint32_t)kGroupCap || (p.ntab > 1 && g.nS > (uint32_t)kGroupCap))
@@ -4119,23 +4218,42 @@ __device__ __forceinline__ void stw_body(const MsdFinalParams &p, StwSmem &sm) {
                     p.radix_list[atomicAdd(&p.plan->nradix, 1u)] = (uint32_t)gi;
             }
             uint4 *h4 = reinterpret_cast<uint4 *>(&sm.hist[0][0]);
-            for (int i = opaque_tid(); i < kStRange / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
+            for (int i = opaque_tid(); i < SM::kBins / 4; i += kStThreads) h4[i] = make_uint4(0, 0, 0, 0);
         }
         have = nfit;
         __syncthreads();
     }
 }
 
-template <bool COMB, int PKM = 0>
-__global__ __launch_bounds__(kStThreads, 4) void msd_final_wstage_kernel(const MsdFinalParams p) {
-    __shared__ StwSmem sm;
+// the layout a call's wide groups take (block-uniform, from the plan): 0 =
+// packed rows, 1 = 16-B rows whose other column fits int32 (part_a checked it:
+// a call that may pack, p.shadow[0]), 2 = any 16-B rows
+__device__ __forceinline__ int stw_layout(const MsdFinalParams &p) {
+    if (uni32(p.plan->packB)) return 0;
+    return p.shadow[0] && uni32(p.plan->nopack) == 0u ? 1 : 2;
+}
+
+// layouts 0 and 1: three workgroups per CU
+constexpr int kStwGrid = SMJ_ST_GRID;
+template <bool COMB>
+__global__ __launch_bounds__(kStThreads, SMJ_ST_MINW) void msd_final_wstage_kernel(const MsdFinalParams p) {
+    __shared__ union {
+        StwSmemP pk;
+        StwSmemR rw;
+    } sm;
     if (msd_plan_failed(p.plan) || uni32(p.plan->nwst) == 0u) return;
-    if (PKM == 2) {
-        if (uni32(p.plan->packB)) stw_body<COMB, true>(p, sm);
-        else stw_body<COMB, false>(p, sm);
-        return;
-    }
-    stw_body<COMB, PKM == 1>(p, sm);
+    const int lay = stw_layout(p);
+    if (lay == 0) stw_body<COMB, true>(p, sm.pk);
+    else if (lay == 1) stw_body<COMB, false>(p, sm.rw);
+}
+
+// layout 2: two workgroups per CU
+constexpr int kStw64Grid = 512;
+template <bool COMB>
+__global__ __launch_bounds__(kStThreads, 4) void msd_final_wstage64_kernel(const MsdFinalParams p) {
+    __shared__ StwSmem64 sm;
+    if (msd_plan_failed(p.plan) || uni32(p.plan->nwst) == 0u || stw_layout(p) != 2) return;
+    stw_body<COMB, false>(p, sm);
 }
 
 // Packed pass-B rows: the single-key and oversized groups (msd_group's
@@ -5502,15 +5620,16 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
             if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, 2>), dim3(sg), dim3(kStThreads), pad, s, p);
             else hipLaunchKernelGGL((msd_final_stage_kernel<false, 0>), dim3(sg), dim3(kStThreads), pad, s, p);
         }
-        // the groups of a key span over kStRange the staged kernel left (none: returns at entry)
+        // the groups of a key span over kStRange the staged kernel left (none: returns at entry);
+        // the layout is picked on the device (stw_layout): the other kernel returns at entry
         MsdFinalParams pw = p;
         if (g_wide_maxrun >= 0) pw.dbg |= (min(g_wide_maxrun, 254) + 1) << 16;
         if (p.combined) {
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<true, 2>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
-            else hipLaunchKernelGGL((msd_final_wstage_kernel<true, 0>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<true>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            hipLaunchKernelGGL((msd_final_wstage64_kernel<true>), dim3(kStw64Grid), dim3(kStThreads), 0, s, pw);
         } else {
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<false, 2>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
-            else hipLaunchKernelGGL((msd_final_wstage_kernel<false, 0>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<false>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
+            hipLaunchKernelGGL((msd_final_wstage64_kernel<false>), dim3(kStw64Grid), dim3(kStThreads), 0, s, pw);
         }
         MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
         q.pk_mode = p.shadow[0] ? 2 : -1;  // packed rows possible: the tiers unpack / read the shadow on the device

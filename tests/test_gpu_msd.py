@@ -720,20 +720,23 @@ def test_heavy_keys_edge_cases(gpu, oracle_built, kc):
 
 
 WSTAGE_CASES = [
-    # nr, ns, key1, key2, kind, select1, select2, maxrun override (-1: none), packed pass-B rows expected
-    (300_000, 300_000, 0, 0, "wide", None, None, -1, 0),
-    (400_000, 350_000, 0, 0, "widepool", None, None, -1, 0),                # ~8 occurrences per key
-    (250_000, 300_000, 1, 1, "widepool", (0, 0), (0, -(1 << 62)), -1, 0),   # key in column 1, WHEREs
-    (30_000, 400_000, 0, 0, "widepool", None, (0, 0), -1, 0),               # skewed: combined layout
-    (500_000, 500_000, 0, 0, "wide31", None, None, -1, 1),                  # packed words, wide groups
-    (300_000, 300_000, 0, 0, "widepool", None, None, 0, 0),                 # every group handed over
-    (200_000, 200_000, 0, 0, "wide31", (1, 150_000), None, 2, 1),           # hand-over on bins > 2 rows
-    (300_000, 300_000, 0, 0, "sparse", None, None, -1, 1),                  # narrow sub-buckets, too few rows
+    # nr, ns, key1, key2, kind, select1, select2, maxrun override (-1: none), packed pass-B rows expected,
+    # S's first payload (over int32: the 16-B-row layout with 64-bit payloads, two workgroups per CU)
+    (300_000, 300_000, 0, 0, "wide", None, None, -1, 0, 10 ** 8),
+    (400_000, 350_000, 0, 0, "widepool", None, None, -1, 0, 10 ** 8),                # ~8 occurrences per key
+    (250_000, 300_000, 1, 1, "widepool", (0, 0), (0, -(1 << 62)), -1, 0, 10 ** 8),   # key in column 1, WHEREs
+    (30_000, 400_000, 0, 0, "widepool", None, (0, 0), -1, 0, 10 ** 8),               # skewed: combined layout
+    (500_000, 500_000, 0, 0, "wide31", None, None, -1, 1, 10 ** 8),                  # packed words, wide groups
+    (300_000, 300_000, 0, 0, "widepool", None, None, 0, 0, 10 ** 8),                 # every group handed over
+    (200_000, 200_000, 0, 0, "wide31", (1, 150_000), None, 2, 1, 10 ** 8),           # hand-over on bins > 2 rows
+    (300_000, 300_000, 0, 0, "sparse", None, None, -1, 1, 10 ** 8),                  # narrow sub-buckets, few rows
+    (300_000, 250_000, 0, 0, "wide", None, None, -1, 0, 1 << 40),                    # 64-bit payloads
+    (200_000, 300_000, 1, 1, "widepool", None, None, -1, 0, -(1 << 50)),             # the same, key in column 1
 ]
 
 
-@pytest.mark.parametrize("nr,ns,k1,k2,kind,s1,s2,maxrun,packed", WSTAGE_CASES)
-def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, s1, s2, maxrun, packed):
+@pytest.mark.parametrize("nr,ns,k1,k2,kind,s1,s2,maxrun,packed,pay0", WSTAGE_CASES)
+def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, s1, s2, maxrun, packed, pay0):
     """Groups spanning more than 4096 keys (full-range keys: SURVEY 8(d)'s
     C3-wide) through msd_final_wstage_kernel -- bins by key, rounds by (key,
     group row), zip join by key within a bin -- and its hand-over to the radix
@@ -741,7 +744,7 @@ def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, 
     from smj import ops
     rng = np.random.default_rng(nr + 3 * ns + k1)
     R = table(rng, nr, 2, kind, k1, 0)
-    S = table(rng, ns, 2, kind, k2, 10 ** 8)
+    S = table(rng, ns, 2, kind, k2, pay0)
     if kind in ("wide", "wide31", "sparse"):  # plant R's keys in a third of S's rows
         pick = rng.random(ns) < 1 / 3
         S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
