@@ -299,6 +299,17 @@ for s in $STEPS; do
              run pmc_write_$w 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$w" -o run -- \
                python3 "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 $NOCPU
            done ;;
+    pmc:*) # pmc:WORKLOAD -- FETCH_SIZE and WRITE_SIZE passes (separate runs) of bench.py --workload WORKLOAD
+           w=${s#pmc:}; st="--steps 2 --warmup 1"; [ "$w" = c4 ] || [ "$w" = c5 ] && st="--steps 1 --warmup 1"
+           run pmc_fetch_$w 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$w" -o run -- \
+               python3 "$ROOT/bench.py" --workload $w $st $NOCPU --verify 0 && \
+           run pmc_write_$w 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$w" -o run -- \
+               python3 "$ROOT/bench.py" --workload $w $st $NOCPU --verify 0 ;;
+    kstat:*) # kstat:WORKLOAD -- rocprofv3 kernel stats of bench.py --workload WORKLOAD
+           w=${s#kstat:}
+           run kstat_$w 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstat_$w" -o $w -- \
+               python3 "$ROOT/bench.py" --workload $w --steps 10 --warmup 2 $NOCPU --verify 0
+           rm -f "$OUT/kstat_$w/${w}_kernel_trace.csv" ;;
     pmcsq) run pmc_sq 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS \
                --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmcsq2) run pmc_sq2 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES \

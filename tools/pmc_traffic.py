@@ -28,6 +28,7 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_final_stage_kernel", "msd_final", True),
     (r"msd_final_kernel<", "msd_final", False),
     (r"msd_final_wide_kernel", "msd_final", False),
+    (r"msd_final_wstage(64)?_kernel", "msd_final", False),
     (r"msd_part_a_kernel", "msd_part_a", True),
     (r"msd_part_b(_pipe)?_kernel", "msd_part_b", True),
     (r"msd_bases_kernel", "msd_runs", True),
@@ -40,6 +41,7 @@ TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_compact_kernel", "msd_compact", True),
     (r"gen_uniform_kernel", "gen_uniform", True),
     (r"gen_zipf_kernel", "gen_zipf", True),
+    (r"gen_wide_kernel", "gen_wide", True),
     (r"msd_part1c?_kernel", "partition_1pass", True),
     (r"msd_p1c_desc_kernel", "partition_1pass", False),
     (r"msd_big_stage_kernel", "msd_big_dev", True),
