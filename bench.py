@@ -178,6 +178,9 @@ def verify_distributed(J, rank, world, dev, full_tables, wire=None):
         ok = not bad and sum(counts) == total and (sum(got) & MASK64) == whole
         flag.fill_(1 if ok else 0)
         info = {"ok": ok, "against": "single-GPU smj_dev_sort_merge_join on the whole job's tables (rank 0)",
+                "kind": "self-consistency: the distributed path against the same library's single-GPU call (they "
+                        "share the sampler, heavy-key and packed pass-B kernels); that call is checked against the "
+                        "CPU port by the N = 1 line (cpu_baseline_mt) and against the oracle by the GPU tests",
                 "joined_rows": sum(counts), "reference_joined_rows": total, "digest": "%016x" % (sum(got) & MASK64),
                 "reference_digest": "%016x" % whole, "mismatched_ranks": bad,
                 "seconds": None}
@@ -467,6 +470,7 @@ def main():
             verified = ok
             verification = {"ok": ok, "against": "oracle/cpu_mt.cpp on the full workload (sorted R, sorted S, "
                                                  "joined rows: row counts + order-sensitive digests)",
+                            "kind": "independent: the CPU port of cpu_app.c's select + stable sort + zip join",
                             "rows": list(res), "cpu_rows": list(rows),
                             "digests": ["%016x" % x for x in dg], "cpu_digests": ["%016x" % x for x in dc]}
             log(f"verification: {verification}")

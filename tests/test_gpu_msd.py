@@ -764,3 +764,40 @@ def test_wide_span_groups_match_oracle(gpu, oracle_built, nr, ns, k1, k2, kind, 
     assert wst > 0.9 * tiers[0], (wst, tiers)
     if maxrun == 0:
         assert tiers[1] == wst, tiers  # every wide group went on to the radix tier
+
+
+WIDE_RANDOM_KINDS = ["wide", "widepool", "wide31", "sparse"]
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_two_column_wide_spans(gpu, oracle_built, seed):
+    """Seeded random 2-column tables whose groups span more than 4096 keys
+    (the wide-span staged kernel in all three LDS layouts, its hand-over, the
+    sparse-bucket switch): sizes 0 to 6e5, skewed pairs, the key in either
+    column, payloads inside or outside int32, a WHERE or none, R's keys planted
+    in a third of S's rows -- bit-exact against the oracle."""
+    from smj import ops
+    rng = np.random.default_rng(3000 + seed)
+    kind = WIDE_RANDOM_KINDS[seed % len(WIDE_RANDOM_KINDS)]
+    nr, ns = (int(rng.integers(0, 600_000)) if rng.random() < 0.9 else int(rng.integers(0, 50)) for _ in range(2))
+    k1, k2 = int(rng.integers(0, 2)), int(rng.integers(0, 2))
+    pay0 = [0, 10 ** 9, -(1 << 45)][int(rng.integers(0, 3))]
+    R = table(rng, nr, 2, kind, k1, 0)
+    S = table(rng, ns, 2, kind, k2, pay0)
+    if nr and ns:
+        pick = rng.random(ns) < 1 / 3
+        S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
+
+    def where(t, key):
+        if rng.random() < 0.5 or len(t) == 0:
+            return None
+        col = int(rng.integers(0, 2))
+        return (col, int(np.sort(t[:, col])[int(rng.integers(0, len(t)))]))
+
+    s1, s2 = where(R, k1), where(S, k2)
+    gR, gS, gJ = ops.sort_merge_join(dev(R).reshape(nr, 2), dev(S).reshape(ns, 2), k1, k2, s1, s2)
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, s2)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    if nr and ns:
+        np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))

@@ -171,6 +171,16 @@ for s in $STEPS; do
              run c5a1_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a1_$r.out" c5_packa
              SMJ_PACKA=0 run c5a0_$r 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5a0_$r.out" c5_rowsa
            done ;;
+    ab:*)  # ab:VARIANT -- same-box A/B of lib/variants/VARIANT against lib/variants/headv: C3 x3, C3-wide x2
+           V=$ROOT/pim-sort-merge-join_amd/lib/variants; vn=${s#ab:}
+           for r in 1 2 3; do
+             SMJ_LIB=$V/$vn/libsmj_hip.so run c3${vn}_$r 300 python bench.py $NOCPU && summ "$OUT/c3${vn}_$r.out" c3_$vn
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3h_$r 300 python bench.py $NOCPU && summ "$OUT/c3h_$r.out" c3_head
+           done
+           for r in 1 2; do
+             SMJ_LIB=$V/$vn/libsmj_hip.so run c3w${vn}_$r 300 python bench.py --workload c3w $NOCPU && summ "$OUT/c3w${vn}_$r.out" c3w_$vn
+             SMJ_LIB=$V/headv/libsmj_hip.so run c3wh_$r 300 python bench.py --workload c3w $NOCPU && summ "$OUT/c3wh_$r.out" c3w_head
+           done ;;
     abhv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # working tree vs the HEAD build (headv), C3, three rounds
            for r in 1 2 3; do
              run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new
