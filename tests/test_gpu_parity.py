@@ -56,6 +56,8 @@ SORT_CASES = [
     # wider than 8 columns: the index-sort path
     (50_000, 9, "dups", 8, (3, 0)), (70_000, 12, "uniform", 4, None), (20_000, 33, "extremes", 31, (0, 0)),
     (0, 16, "uniform", 0, None),
+    # full-range keys through the wide-span staged kernel (one table), a WHERE on the other column
+    (500_000, 2, "wide", 0, None), (300_000, 2, "wide", 1, (0, 100_000)),
 ]
 
 
