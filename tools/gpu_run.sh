@@ -325,6 +325,7 @@ for s in $STEPS; do
     pmcsq2) run pmc_sq2 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES \
                --output-format csv -d "$OUT/pmc_sq2" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmclist) run pmclist 60 rocprofv3 -L ;;
+    shapes) run shapes 600 python tools/shape_probe.py ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     finv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # phases (stamps build) + ablation (ablate build) on HEAD
