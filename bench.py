@@ -404,7 +404,7 @@ def main():
     sort_passes = None
     if pmc:
         sort_passes = {}
-        for name in ("msd_part_a", "msd_part_b", "msd_final"):
+        for name in ("msd_part_a", "msd_part_b", "msd_final", "msd_final_tiers"):
             k, d = pmc.get("kernels", {}).get(name), prof.get(name)
             if k and d and d["launches"]:
                 fetched = 2.0 * k["fetch_kib_raw"] * 1024

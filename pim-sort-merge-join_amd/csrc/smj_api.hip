@@ -1279,19 +1279,44 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
         g_msd_wstage = ms->h_plan->nwst;
     }
     bool redo = false;
+    // 2-column tables: the groups the staged kernel did not sort (wide groups
+    // with 64-bit payloads, the radix / 64-bit tiers' hand-overs) -- launched
+    // only when the plan shows some; the speculative compact was then a no-op
+    // (msd_compact_kernel) and runs again below
+    const bool two = fp.tab[0].cols == 2 && (ntab == 1 || fp.tab[1].cols == 2);
+    const bool tiers = two && (ms->h_plan->nwst || ms->h_plan->nradix);
+    size_t pt = (size_t)-1;
+    if (tiers) {
+        {
+            ProfScope ps("msd_final_tiers", 0, s);
+            HIP_TRY(launch_msd_final_tiers(fp, s));
+        }
+        pt = prof_last();
+    }
+    ms->n_cwork = 0;  // (msd_fallback lists the oversized groups' join chunks, if any)
     MsdFinalParams ff = fp;  // packed pass-B rows: the single-key tier reads the words (pk_mode 3), the
                              // others read the shadow, which the unpack kernel fills for the oversized groups
     ff.pk_mode = ms->h_plan->packB ? 3 : -1;
     if (ms->h_plan->packB && ms->h_plan->nbig) HIP_TRY(launch_msd_unpack_groups(fp, s));
     SMJ_TRY(msd_fallback(ms, in, ntab, join, ff, out_j, s, &redo));
+    redo = redo || (tiers && join);
     if (redo) {
         SMJ_TRY(compact(1));
         pc = prof_last();
     }
-    if (redo || ms->h_plan->nbig) {  // joined (after the redo), the device big-group count
+    if (redo || ms->h_plan->nbig || tiers) {  // joined (after the redo), the device big-group count, the tiers' counts
         HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (t_slot < 0) g_msd_bigdev = ms->h_plan->nbigdev;
+        if (ms->h_plan->err) {  // a tier handed a group over its capacity (a bug: err bit 2)
+            fprintf(stderr, "smj: pipeline group plan inconsistent after the final tiers (err 0x%x)\n", ms->h_plan->err);
+            return SMJ_ERR_HIP;
+        }
+        if (t_slot < 0) {
+            g_msd_bigdev = ms->h_plan->nbigdev;
+            g_msd_groups[1] = ms->h_plan->nradix;
+            g_msd_groups[2] = ms->h_plan->nwide;
+            g_msd_wstage = ms->h_plan->nwst;
+        }
     }
     const MsdPlan &pl = *ms->h_plan;
     double pa_bytes = 0.0;
@@ -1306,6 +1331,11 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
     const double Jb = join ? 8.0 * tc * (double)pl.joined : 0.0;
     double fb = Jb;
     for (int x = 0; x < ntab; x++) fb += 2.0 * 8.0 * in[x].cols * pl.m[x];
+    if (pt != (size_t)-1 && pl.ngroups) {  // the tiers' share of the rows, by their groups (wide groups: all of C3-wide's)
+        const double share = std::min(1.0, (double)(pl.nwst + pl.nradix) / (double)pl.ngroups);
+        prof_set_bytes(pt, fb * share);
+        fb -= fb * share;
+    }
     prof_set_bytes(pf, fb);
     prof_set_bytes(pc, 2.0 * Jb);
     if (join) h_rows[2] = pl.joined;

@@ -594,6 +594,7 @@ hipError_t launch_msd_runs_apply(const MsdRunsArgs &a, hipStream_t s);
 hipError_t launch_msd_part_b(const MsdPartBParams &p, int cols, int64_t max_tiles, hipStream_t s, bool pb_pack = false);
 hipError_t launch_msd_group(const MsdGroupParams &p, hipStream_t s);
 hipError_t launch_msd_final(const MsdFinalParams &p, hipStream_t s);
+hipError_t launch_msd_final_tiers(const MsdFinalParams &p, hipStream_t s);  // 2-column: wide-span kernels, radix, 64-bit tiers
 int msd_packb_mode();
 // the single-key / oversized groups' rows unpacked into MsdFinalParams::shadow (packed calls)
 hipError_t launch_msd_unpack_groups(const MsdFinalParams &p, hipStream_t s);  // packed pass-B rows (MsdPlan::packB): 0 off, 1 on unskewed tables, 2 forced (SMJ_PACKB)

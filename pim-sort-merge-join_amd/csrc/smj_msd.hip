@@ -3805,7 +3805,7 @@ __device__ __forceinline__ void st_body(const MsdFinalParams &p, StSmem &sm) {
             continue;
         }
         if (!st_ok<COMB>(p, g)) {
-            if (stw_ok<COMB>(p, g)) {  // a wide group: msd_final_wstage_kernel's (launched next)
+            if (stw_ok<COMB>(p, g)) {  // a wide group: the wide-span kernels' (msd_back launches them)
                 nwst++;
                 have = false;
                 continue;
@@ -5233,7 +5233,9 @@ __global__ __launch_bounds__(256) void msd_compact_kernel(const int64_t *__restr
     constexpr int U = 8;
     const int lane = threadIdx.x & 63;
     if (msd_plan_failed(plan)) return;
-    if (!after_fallback && plan->nsingle + plan->nbig > 0) return;
+    // (speculative call: a no-op while some groups' counts are still to come --
+    // the host-driven tiers' groups, and the final tiers launched by msd_back)
+    if (!after_fallback && plan->nsingle + plan->nbig + plan->nradix + plan->nwst > 0) return;
     const int64_t ng = plan->ngroups, step = (int64_t)gridDim.x * 4;
     int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= ng) return;
@@ -5620,28 +5622,42 @@ hipError_t launch_msd_final(const MsdFinalParams &p_in, hipStream_t s) {
             if (p.shadow[0]) hipLaunchKernelGGL((msd_final_stage_kernel<false, 2>), dim3(sg), dim3(kStThreads), pad, s, p);
             else hipLaunchKernelGGL((msd_final_stage_kernel<false, 0>), dim3(sg), dim3(kStThreads), pad, s, p);
         }
-        // the groups of a key span over kStRange the staged kernel left (none: returns at entry);
-        // the layout is picked on the device (stw_layout): the other kernel returns at entry
-        MsdFinalParams pw = p;
-        if (g_wide_maxrun >= 0) pw.dbg |= (min(g_wide_maxrun, 254) + 1) << 16;
-        if (p.combined) {
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<true>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
-            hipLaunchKernelGGL((msd_final_wstage64_kernel<true>), dim3(kStw64Grid), dim3(kStThreads), 0, s, pw);
-        } else {
-            if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<false>), dim3(kStwGrid), dim3(kStThreads), 0, s, pw);
-            hipLaunchKernelGGL((msd_final_wstage64_kernel<false>), dim3(kStw64Grid), dim3(kStThreads), 0, s, pw);
-        }
-        MsdFinalParams q = p;  // the radix tier over the groups the staged kernel handed over
-        q.pk_mode = p.shadow[0] ? 2 : -1;  // packed rows possible: the tiers unpack / read the shadow on the device
-        hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
-        q.radix_list = nullptr;
-        hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
+        // (the wide-span kernels and the radix / 64-bit tiers: launch_msd_final_tiers,
+        // from msd_back once the plan shows groups for them)
     } else {
         MsdFinalParams q = p;
         q.radix_list = nullptr;  // contiguous mode
         hipLaunchKernelGGL((msd_final_kernel<0, 0>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
         hipLaunchKernelGGL((msd_final_wide_kernel<0, 0>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
     }
+    return hipGetLastError();
+}
+
+// 2-column tables: the groups the staged kernel did not sort -- the wide
+// groups (msd_final_wstage_kernel, or msd_final_wstage64_kernel with 64-bit
+// payloads: the other returns at entry), then the radix tier over the
+// handed-over groups and the 64-bit tier over what it passes on.  The host
+// launches these only when the plan shows such groups (msd_back): in C3 /
+// C4 / C5 the staged kernel sorts every group, and launches that return at
+// entry still take CU slots behind a concurrent part's kernels (C4's trace,
+// profiles/r06/r06o).  (Sorting the wide groups inside the staged kernel's
+// own walk, in views of its LDS, made its narrow path slower: C4 msd_final
+// 14.64-14.71 -> 15.39-15.50 ms, profiles/r06/r06p.)
+hipError_t launch_msd_final_tiers(const MsdFinalParams &p_in, hipStream_t s) {
+    MsdFinalParams p = p_in;
+    if (g_wide_maxrun >= 0) p.dbg |= (min(g_wide_maxrun, 254) + 1) << 16;
+    if (p.combined) {
+        if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<true>), dim3(kStwGrid), dim3(kStThreads), 0, s, p);
+        hipLaunchKernelGGL((msd_final_wstage64_kernel<true>), dim3(kStw64Grid), dim3(kStThreads), 0, s, p);
+    } else {
+        if (p.shadow[0]) hipLaunchKernelGGL((msd_final_wstage_kernel<false>), dim3(kStwGrid), dim3(kStThreads), 0, s, p);
+        hipLaunchKernelGGL((msd_final_wstage64_kernel<false>), dim3(kStw64Grid), dim3(kStThreads), 0, s, p);
+    }
+    MsdFinalParams q = p;
+    q.pk_mode = p.shadow[0] ? 2 : -1;  // packed rows possible: the tiers unpack / read the shadow on the device
+    hipLaunchKernelGGL((msd_final_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kFinThreads), 0, s, q);
+    q.radix_list = nullptr;
+    hipLaunchKernelGGL((msd_final_wide_kernel<2, 2>), dim3(kMsdFinalGrid), dim3(kMsdThreads), 0, s, q);
     return hipGetLastError();
 }
 

@@ -181,6 +181,14 @@ for s in $STEPS; do
              SMJ_LIB=$V/$vn/libsmj_hip.so run c3w${vn}_$r 300 python bench.py --workload c3w $NOCPU && summ "$OUT/c3w${vn}_$r.out" c3w_$vn
              SMJ_LIB=$V/headv/libsmj_hip.so run c3wh_$r 300 python bench.py --workload c3w $NOCPU && summ "$OUT/c3wh_$r.out" c3w_head
            done ;;
+    ab4:*) # ab4:VARIANT -- same-box A/B on C4 (two rounds) and C5 (one)
+           V=$ROOT/pim-sort-merge-join_amd/lib/variants; vn=${s#ab4:}
+           for r in 1 2; do
+             SMJ_LIB=$V/$vn/libsmj_hip.so run c4${vn}_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4${vn}_$r.out" c4_$vn
+             SMJ_LIB=$V/headv/libsmj_hip.so run c4h_$r 600 python bench.py --workload c4 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c4h_$r.out" c4_head
+           done
+           SMJ_LIB=$V/$vn/libsmj_hip.so run c5${vn} 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5${vn}.out" c5_$vn
+           SMJ_LIB=$V/headv/libsmj_hip.so run c5h 600 python bench.py --workload c5 --steps 5 --warmup 2 $NOCPU && summ "$OUT/c5h.out" c5_head ;;
     abhv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # working tree vs the HEAD build (headv), C3, three rounds
            for r in 1 2 3; do
              run c3n_$r 300 python bench.py $NOCPU && summ "$OUT/c3n_$r.out" c3_new

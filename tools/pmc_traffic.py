@@ -26,9 +26,12 @@ from collections import defaultdict
 
 TAGS = [  # (regex on the demangled kernel name, bench.py scope tag, primary?)
     (r"msd_final_stage_kernel", "msd_final", True),
-    (r"msd_final_kernel<", "msd_final", False),
+    (r"msd_final_wstage64_kernel", "msd_final_tiers", True),   # (round 6: launched by msd_back when needed)
+    (r"msd_final_wstage_kernel", "msd_final_tiers", False),
+    (r"msd_final_kernel<2, 2>", "msd_final_tiers", False),
+    (r"msd_final_wide_kernel<2, 2>", "msd_final_tiers", False),
+    (r"msd_final_kernel<", "msd_final", False),        # (tables of other widths: in msd_final)
     (r"msd_final_wide_kernel", "msd_final", False),
-    (r"msd_final_wstage(64)?_kernel", "msd_final", False),
     (r"msd_part_a_kernel", "msd_part_a", True),
     (r"msd_part_b(_pipe)?_kernel", "msd_part_b", True),
     (r"msd_bases_kernel", "msd_runs", True),
