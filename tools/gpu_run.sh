@@ -336,6 +336,7 @@ for s in $STEPS; do
     shapes) run shapes 600 python tools/shape_probe.py ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
+    finabv) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/ablate/libsmj_hip.so run finabv 300 python tools/final_ablate.py ;;
     finv)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # phases (stamps build) + ablation (ablate build) on HEAD
            SMJ_LIB=$V/stamps/libsmj_hip.so run phasesv 300 python tools/msd_phases.py && \
            SMJ_LIB=$V/ablate/libsmj_hip.so run finabv 300 python tools/final_ablate.py ;;
