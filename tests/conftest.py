@@ -76,3 +76,21 @@ def gpu(pkg_built):
     from smj import _lib
     lib = _lib.load(build_if_missing=False)
     return lib
+
+
+@pytest.fixture(autouse=True)
+def _gpu_memlog(request):
+    """SMJ_TEST_MEMLOG=1: after each test, the device memory the library, torch
+    and everything else hold (finding what keeps memory between tests)."""
+    yield
+    if os.environ.get("SMJ_TEST_MEMLOG") != "1":
+        return
+    import torch
+    if not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    from smj import ops
+    free, total = torch.cuda.mem_get_info()
+    lib = ops.scratch_bytes()
+    tor = torch.cuda.memory_reserved()
+    print(f"\n[memlog] {request.node.name}: lib {lib / 2**30:.1f} GiB, torch reserved {tor / 2**30:.1f}, "
+          f"free {free / 2**30:.1f}, other {(total - free - lib - tor) / 2**30:.1f}", flush=True)
