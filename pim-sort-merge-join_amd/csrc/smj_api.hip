@@ -526,6 +526,7 @@ struct MsdScratch {
     int64_t *p1h = nullptr;             // pinned twin
     int64_t *heavy = nullptr;           // [kBucketsA][kHeavyMax] heavy keys per bucket (msd_heavy_kernel)
     uint32_t *nheavy = nullptr;         // [kBucketsA] their count
+    MsdSeg *seg = nullptr;              // [kBucketsA] segmented pass-B digits (msd_bases_kernel)
     uint32_t *p1c = nullptr;            // chunked partition: device [2][kP1cWords]: rows per (chunk, part), flags
     uint32_t *h_p1c = nullptr;          // pinned twin
     void *p1desc[2] = {nullptr, nullptr};  // its parts' part_a tile descriptors per table
@@ -539,6 +540,7 @@ int64_t g_msd_groups[4] = {0, 0, 0, 0};  // last pipeline: dense groups, radix-t
 int64_t g_msd_bigdev = 0;                // last pipeline: oversized multi-key groups sorted on the device
 int64_t g_msd_packb = 0;                 // last pipeline: pass-B rows packed (MsdPlan::packB)
 int64_t g_msd_wstage = 0;                // last pipeline: groups the wide-span staged kernel took (MsdPlan::nwst)
+int64_t g_msd_segb = 0;                  // last pipeline: buckets with a segmented pass-B digit (MsdPlan::nsegb)
 struct PbLast {  // last pipeline call's part_b launches (smj_debug_part_b_time)
     MsdPartBParams p;
     int cols;
@@ -567,7 +569,7 @@ int msd_scratch(MsdScratch **out) {
     MsdScratch &m = g_msd[key];
     if (m.dev < 0) {
         HIP_TRY(dev_alloc(&m.spl, sizeof(int64_t) * (kSplA + 1)));
-        HIP_TRY(dev_alloc(&m.samp, sizeof(int64_t) * (2 * kSampleMax + 64)));
+        HIP_TRY(dev_alloc(&m.samp, sizeof(int64_t) * kSampScratch));
         HIP_TRY(dev_alloc(&m.groups, sizeof(MsdGroup) * kSlots));
         HIP_TRY(dev_alloc(&m.gpart, sizeof(uint32_t) * 2 * kBucketsA * kGroupSlices * kRadB));
         HIP_TRY(dev_alloc(&m.ngrp, sizeof(uint32_t) * kOffsA));
@@ -586,6 +588,7 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(dev_alloc(&m.p1c, sizeof(uint32_t) * 2 * kP1cWords));
         HIP_TRY(dev_alloc(&m.heavy, sizeof(int64_t) * kBucketsA * kHeavyMax));
         HIP_TRY(dev_alloc(&m.nheavy, sizeof(uint32_t) * kBucketsA));
+        HIP_TRY(dev_alloc(&m.seg, sizeof(MsdSeg) * kBucketsA));
         HIP_TRY(hipHostMalloc(&m.h_p1c, sizeof(uint32_t) * 2 * kP1cWords, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
@@ -607,7 +610,7 @@ void msd_free_one(MsdScratch &m) {  // also a set whose creation failed half-way
     for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                     (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                     (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
-                    (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy})
+                    (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy, (void *)m.seg})
         dev_free(p);
     hipHostFree(m.p1h);
     hipHostFree(m.h_p1c);
@@ -807,6 +810,25 @@ int msd_fallback(MsdScratch *ms, const MsdIn *in, int ntab, int join, const MsdF
                 if (hist[d][b])
                     fprintf(stderr, "smj big groups span%s4096 rows 2^%d: %lld groups, %lld rows\n", d ? ">" : "<=", b,
                             (long long)hist[d][b], (long long)rows[d][b]);
+        int shown = 0;  // and the first few: bucket, sub-buckets, rows, key interval
+        for (const Listed &e : bigs) {
+            const MsdGroup &g = *e.g;
+            if (shown++ >= 12) break;
+            fprintf(stderr, "smj big group a=%u b=[%u,%u) nR=%u nS=%u base=%lld span=%u\n", g.a, g.b0, g.b1, g.nR, g.nS,
+                    (long long)g.base, g.span);
+            if (shown <= 3) {  // its bucket's digit
+                MsdBucket bk;
+                MsdSeg sg;
+                hipMemcpy(&bk, (const MsdBucket *)ms->t[0].bk + g.a, sizeof bk, hipMemcpyDeviceToHost);
+                hipMemcpy(&sg, ms->seg + g.a, sizeof sg, hipMemcpyDeviceToHost);
+                fprintf(stderr, "  bucket lo=%lld L=%u one_key=%#x scale=%llu s32=%u maxspan=%u\n", (long long)bk.lo, bk.L,
+                        bk.one_key, (unsigned long long)bk.scale, bk.s32, bk.maxspan);
+                if (bk.one_key & kBucketSeg)
+                    for (uint32_t k = 0; k < sg.nseg; k++)
+                        fprintf(stderr, "  seg %u st=%lld s32=%u db=%u dn=%u sh=%u ms=%u (hi %lld)\n", k, (long long)sg.st[k],
+                                sg.s32[k], seg_db(sg.pk[k]), seg_dn(sg.pk[k]), seg_sh(sg.pk[k]), sg.ms[k], (long long)sg.hi);
+            }
+        }
     }
     if (!host_bigs.empty()) {
         // all remaining oversized multi-key groups at once: gather (in key
@@ -1145,6 +1167,9 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         bp.spl = ms->spl;
         bp.plan = ms->plan;
         bp.pack_ok = pack_mode;
+        bp.samp = ms->samp;
+        // the segmented digit (clustered keys; SMJ_SEG=0: the linear one everywhere)
+        bp.seg = getenv("SMJ_SEG") && atoi(getenv("SMJ_SEG")) == 0 ? nullptr : ms->seg;
         HIP_TRY(launch_msd_bases(bp, s));
         HIP_TRY(launch_msd_runs_apply(ra, s));
     }
@@ -1154,6 +1179,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
                          (const uint2 *)ms->t[x].tinfo, (const MsdBucket *)ms->t[x].bk, ms->plan,
                          (uint16_t *)ms->t[x].offsB, in[x].key, x};
         p.heavy = ms->heavy;
+        p.seg = ms->seg;
         {
             ProfScope ps("msd_part_b", 0, s);
             HIP_TRY(launch_msd_part_b(p, in[x].cols, maxB[x], s, pack_ok));
@@ -1182,6 +1208,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         gp.big_list = ms->big_list;
         gp.spin_limit = g_spin_limit;
         gp.heavy = ms->heavy;
+        gp.seg = ms->seg;
         ProfScope ps("msd_group", 0, s);
         HIP_TRY(launch_msd_group(gp, s));
     }
@@ -1277,6 +1304,7 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
         g_msd_groups[3] = ms->h_plan->nlsd;
         g_msd_packb = ms->h_plan->packB;
         g_msd_wstage = ms->h_plan->nwst;
+        g_msd_segb = ms->h_plan->nsegb;
     }
     bool redo = false;
     // 2-column tables: the groups the staged kernel did not sort (wide groups
@@ -2112,6 +2140,9 @@ extern "C" int64_t smj_debug_msd_packb(void) { return g_msd_packb; }
 // Diagnostic only: groups of the last pipeline call that the wide-span staged
 // kernel took (msd_final_wstage_kernel: key spans over kStageRange)
 extern "C" int64_t smj_debug_msd_wstage(void) { return g_msd_wstage; }
+// Diagnostic only: pass-A buckets of the last pipeline call given a segmented
+// pass-B digit (MsdSeg: keys in dense intervals with wide gaps between)
+extern "C" int64_t smj_debug_msd_segmented(void) { return g_msd_segb; }
 // Diagnostic only: the wide-span staged kernel hands a group to the radix tier
 // when a bin holds more than `rows` rows (-1: the built-in SMJ_ST_MAXRUN; 0:
 // every group -- the tests' way to the hand-over path)

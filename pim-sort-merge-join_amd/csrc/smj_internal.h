@@ -281,7 +281,8 @@ struct MsdSampleParams {
     MsdTable tab[2];
     int ntab;
     int64_t *spl;        // out: kSplA splitters
-    int64_t *samp;       // scratch: 2 kSampleMax samples + per-block valid counts
+    int64_t *samp;       // scratch: 2 kSampleMax samples + per-block valid counts; then (select kernel, out)
+                         // the valid samples in key order at samp + kSortedOff
     struct MsdPlan *plan;  // out (select kernel): plan->skew, sampled keys with an equal partner (nullptr: not counted)
 };
 struct MsdPartAParams {
@@ -306,6 +307,36 @@ struct MsdPartA2 {       // one part_a launch over up to two tables
     MsdPartAParams t[2];
     unsigned tiles0;     // blocks [0, tiles0) take table 0's tiles, the rest table 1's
 };
+// samp + kSortedOff: the select kernel's samples in key order (msd_bases_kernel's segmented digit)
+constexpr int kSortedOff = 2 * kSampleMax + 64;
+constexpr int kSampScratch = kSortedOff + 2 * kSampleMax;  // int64 words of MsdScratch::samp
+// A segmented pass-B digit (MsdBucket::one_key bit 1, kBucketSeg): a bucket
+// whose sampled keys sit in up to kSegMax dense intervals separated by wide
+// empty gaps (clustered keys: an interval straddling two clusters 2^40 apart
+// put both clusters' rows into one or two linear sub-buckets).  Interval k,
+// [st[k], en[k]], gets dn[k] linear sub-buckets from db[k] on and the one
+// after them holds the keys past en[k] up to st[k + 1] (the gap; keys in the
+// gap are rare but legal):
+//   k = the last interval with st[k] <= key (k = 0 below st[1]),
+//   r = (key - st[k]) >> sh[k],
+//   digit = db[k] + (r >= 2^32 ? dn[k] : min(dn[k], mulhi32(r, s32[k]))),
+//   s32[k] = 2^32 dn[k] / (((en[k] - st[k]) >> sh[k]) + 1)   (keys <= en[k]: < dn[k]),
+// sh[k] the shift that brings the interval under 2^32 (a 32-bit multiply in
+// part_b).  st[0] = the bucket's lo, so every key of the bucket has an interval.
+constexpr int kSegMax = 8;
+constexpr uint32_t kBucketSeg = 2u;  // MsdBucket::one_key bit: the bucket's digit is MsdSeg's
+struct MsdSeg {
+    int64_t st[kSegMax];   // interval starts, ascending (st[0] = lo; unused entries repeat the last)
+    uint32_t s32[kSegMax]; // interval scales
+    uint32_t pk[kSegMax];  // db | dn << 11 | sh << 22
+    int64_t hi;            // the bucket's last key
+    uint32_t ms[kSegMax];  // sub-buckets a final group of the interval may span (MsdBucket::maxspan)
+    uint32_t nseg, pad[21];
+};
+__host__ __device__ inline uint32_t seg_db(uint32_t pk) { return pk & 0x7ffu; }
+__host__ __device__ inline uint32_t seg_dn(uint32_t pk) { return (pk >> 11) & 0x7ffu; }
+__host__ __device__ inline uint32_t seg_sh(uint32_t pk) { return pk >> 22; }
+static_assert(sizeof(MsdSeg) == 256 && offsetof(MsdSeg, hi) == 128, "part_b loads st, s32, pk: 16 words");
 struct MsdBucket {       // per pass-A bucket and table
     int64_t lo;          // pass-B digit (common to R and S): with r = key - lo,
     uint64_t scale;      //   scale == 0: r (interval < kRadB keys: one key per sub-bucket)
@@ -317,6 +348,8 @@ struct MsdBucket {       // per pass-A bucket and table
     uint32_t nruns;      // run-list entries
     uint32_t tile_base;  // first pass-B tile
     uint32_t one_key;    // bit 0: the bucket's interval is a single key value (a heavy key's bucket);
+                         // bit 1 (kBucketSeg): the pass-B digit is the segmented one (MsdSeg; scale,
+                         // s32 and maxspan unused);
                          // bits 8..15: m, the bucket's heavy keys (msd_heavy_kernel): the pass-B digit
                          // is then d = lin(r) + 2 c + e over D - 2 m linear sub-buckets, c = heavy keys
                          // below the key, e = the key is one -- every heavy key a sub-bucket of its own
@@ -382,6 +415,7 @@ struct MsdPlan {         // device-side pipeline state (zeroed per call)
     uint32_t packB;      // msd_bases: pass-B rows are packed in this call
     uint32_t nwst;       // groups of a key span over kStageRange left by the staged kernel to
                          // msd_final_wstage_kernel (full-range keys: SURVEY 8(d)'s C3-wide)
+    uint32_t nsegb;      // msd_bases: buckets given a segmented pass-B digit (MsdSeg)
 };
 // A kernel launched after msd_group_kernel reads the plan's error word first:
 // a set bit means the dense group array may hold slots this call never wrote.
@@ -403,6 +437,8 @@ struct MsdBasesParams {
     MsdPlan *plan;
     int pack_ok;               // msd_packb_mode() with 2-column tables: MsdPlan::packB may be set (2: despite skew)
     const uint32_t *nheavy;    // [kBucketsA] heavy keys per bucket (msd_heavy_kernel), nullptr = none
+    const int64_t *samp;       // MsdSampleParams::samp: the valid-sample counts and the sorted samples
+    MsdSeg *seg;               // out: [kBucketsA] segmented digits; nullptr = none (SMJ_SEG=0)
 };
 struct MsdPartBParams {
     const int64_t *srcA;
@@ -415,6 +451,7 @@ struct MsdPartBParams {
     int key_col, x;
     int dbg;             // SMJ_DEBUG_MSD: phase stamps (tools/msd_phases.py)
     const int64_t *heavy;  // [kBucketsA][kHeavyMax] heavy keys (MsdBucket::one_key bits 8..15: how many)
+    const MsdSeg *seg;     // [kBucketsA] segmented digits (MsdBucket::one_key & kBucketSeg)
 };
 struct MsdGroup {        // one final group: sub-buckets [b0, b1) of bucket a
     uint16_t a, flags, b0, b1;
@@ -440,6 +477,7 @@ struct MsdGroupParams {
     int combined;           // as MsdBasesParams::combined
     uint32_t spin_limit;    // polls of the look-back before it gives up (kMsdSpinLimit; 0 in the forced-timeout test)
     const int64_t *heavy;   // as MsdPartBParams::heavy
+    const MsdSeg *seg;      // as MsdPartBParams::seg
 };
 struct MsdTab {          // a table as the final kernels see it
     const int64_t *tempB;

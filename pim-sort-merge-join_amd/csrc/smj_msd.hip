@@ -365,6 +365,7 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
         // over a range >> the sample: ~0 of them; Zipf: thousands)
         const uint64_t rep = __ballot(e > 1u && key != INT64_MAX && rank < M);
         if (tid == 0 && rep && p.plan) atomicAdd(&p.plan->skew, (uint32_t)__popcll(rep));
+        if (rank < M) p.samp[kSortedOff + rank] = key;  // key order (msd_bases_kernel's segmented digit)
         if (M > 0 && rank < M)
             for (int q = 0; q < kSplA; q++)
                 if (min(M - 1, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))) == rank) p.spl[q] = key;
@@ -1040,10 +1041,252 @@ constexpr uint32_t kWideSkew = 256;  // repeated sampled keys that keep sparse b
 #define SMJ_WIDE_FILL 65  // percent (0: never)
 #endif
 constexpr int kBasesWaves = kOffsA / 64;
+constexpr uint64_t kFill = (uint64_t)kGroupCap * 15 / 16, kOne = (uint64_t)kGroupCap * 13 / 16;
+
+// sub-buckets a final group may span, for sub-buckets of <= w keys each: a
+// group's span stays within the staged kernel's counting range when one
+// sub-bucket fits it, else below 2^48 (the radix tiers' sort word); the group
+// kernel computes the exact span of every group.  Narrow groups (<=
+// kStageRange keys) of `span` sub-buckets hold ~span Lm / D rows per table;
+// well under a full group, full groups spanning more keys for the wide-span
+// staged kernel cost less (round 6, r06g: C3's tables with keys over [1, 1e9]
+// made groups of two sub-buckets, msd_final 3.3 ms against 1.6 at [1, 3e8]
+// and 2.1 on wide groups).  SMJ_WIDE_FILL = the narrow fill (percent of
+// kFill) below which a bucket goes wide.  Not when the pass-A sample repeats
+// many keys (plan->skew over kWideSkew of its ~8192): few distinct keys with
+// long equal-key runs fill the narrow groups whatever the interval, and the
+// wide kernel hands bins over 32 rows on.  (Joining tables repeat a few: an
+// S key sampled together with its R partner.)
+__device__ uint32_t bases_maxspan(uint64_t w, uint64_t Lm, uint64_t D, uint32_t skew) {
+    uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
+    if (w <= (uint64_t)kStageRange && Lm > 0 && skew < kWideSkew &&
+        span * Lm * 100u < (uint64_t)SMJ_WIDE_FILL * kFill * D)
+        span = ((uint64_t)1 << 48) / w;
+    return span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
+}
+// keys per sub-bucket of a 64-bit scale, + 1: ceil(2^64 / scale) + 1
+__device__ uint64_t sub_width(uint64_t scale) {
+    return (uint64_t)((((unsigned __int128)1 << 64) + scale - 1u) / scale) + 1u;
+}
+
+// The segmented pass-B digit of bucket a (MsdSeg), from its sampled keys in
+// key order (msd_sample_select_kernel: positions (at(a - 1), at(a)] hold the
+// bucket's ~32).  The gaps between consecutive samples -- and from lo to the
+// first, from the last to hi -- are the candidates: with delta the mean gap
+// less the kSegMax largest (the spacing inside the dense parts), a gap over 32
+// delta, over 1/16 of the interval and over 4 kRadB keys separates two dense
+// intervals, and the bucket is segmented when such gaps make up half its
+// interval (uniform keys: the largest of ~33 gaps is ~3.5 delta, so a uniform
+// bucket never is).  A dense interval runs from its first to its last sample
+// widened by kSegMargin = 6 spacings on each side (rows past the extreme
+// samples: ~1 spacing's worth on average, e^-6 of one beyond 6), so the gap
+// sub-buckets stay near empty; a gap at the bottom (the bucket's lo lies in a
+// gap: the previous cluster's unsampled tail sits just above lo) makes a
+// first interval [lo, lo + 6 spacings of the previous bucket's last samples].
+// Up to kSegMax intervals (the largest gaps; a bucket spanning more clusters
+// keeps some of them in one interval).
+// Sub-buckets go to the intervals by their width in spacings (expected rows,
+// margins included: a count of ~8 samples was too noisy -- r06y, sub-buckets
+// of 1000 rows), so rows per sub-bucket stay even; the spacing is the
+// interval's own over 8 or more samples, else the bucket's (delta).
+constexpr uint64_t kSegMargin = 6;  // spacings past an interval's extreme samples
+__device__ bool seg_plan(const int64_t *ss, uint32_t M, int a, int64_t lo, int64_t hi, uint64_t D, uint64_t Lm,
+                         uint32_t skew, MsdSeg &sg) {
+    if (M < (uint32_t)(8 * kBucketsA) || M > (uint32_t)kSampleN) return false;
+    auto at = [&](int q) { return min(M - 1u, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))); };
+    const uint32_t p0 = a == 0 ? 0u : at(a - 1) + 1u, p1 = a >= kSplA ? M - 1u : at(a);
+    if (p1 < p0 || p1 - p0 > 1024u) return false;
+    const uint64_t range = (uint64_t)hi - (uint64_t)lo;
+    {  // a light first pass: the largest gap alone.  No gap can be a cut when it
+       // is under 32 x the least delta0 below can be (the top TG gaps at most TG
+       // x the largest): uniform buckets end here (C3: bases 37 -> ~18 us)
+        uint32_t n1 = 0;
+        int64_t pv = lo;
+        uint64_t G = 0;
+        for (uint32_t i = p0; i <= p1; i++) {
+            const int64_t k = ss[i];
+            const bool in = k >= lo && k <= hi;
+            G = in ? max(G, (uint64_t)k - (uint64_t)pv) : G;
+            pv = in ? k : pv;
+            n1 += in ? 1u : 0u;
+        }
+        G = max(G, (uint64_t)hi - (uint64_t)pv);
+        if (n1 < 16) return false;
+        const uint64_t topb = G > range / kSegMax ? range : (uint64_t)kSegMax * G;
+        if (G / 32u <= (range - topb) / (n1 + 1u - kSegMax)) return false;
+    }
+    // the kSegMax largest gaps: size, ordinal of the sample after it (0: from
+    // lo; n: to hi), and its ends
+    constexpr int TG = kSegMax;
+    uint64_t tg[TG];
+    uint32_t to[TG];
+    int64_t tl[TG], tr[TG];
+#pragma unroll
+    for (int j = 0; j < TG; j++) tg[j] = 0, to[j] = 0, tl[j] = tr[j] = 0;
+    auto insert = [&](uint64_t g, uint32_t o, int64_t l, int64_t r) {
+#pragma unroll
+        for (int j = 0; j < TG; j++)
+            if (g > tg[j]) {
+                const uint64_t g2 = tg[j];
+                const uint32_t o2 = to[j];
+                const int64_t l2 = tl[j], r2 = tr[j];
+                tg[j] = g, to[j] = o, tl[j] = l, tr[j] = r;
+                g = g2, o = o2, l = l2, r = r2;
+            }
+    };
+    uint32_t n = 0;
+    int64_t prev = lo, first = lo;
+    for (uint32_t i = p0; i <= p1; i++) {
+        const int64_t k = ss[i];
+        if (k < lo || k > hi) continue;
+        if (n == 0) first = k;
+        insert((uint64_t)k - (uint64_t)prev, n, prev, k);
+        prev = k;
+        n++;
+    }
+    if (n < 16) return false;
+    insert((uint64_t)hi - (uint64_t)prev, n, prev, hi);
+    uint64_t top = 0;
+#pragma unroll
+    for (int j = 0; j < TG; j++) top += tg[j];
+    // (a low estimate: the largest in-cluster gaps are left out too)
+    const uint64_t delta0 = max<uint64_t>(1u, (range - min(range, top)) / (n + 1u - TG));
+    const uint64_t thr = max(max(32u * delta0, range / 16u), (uint64_t)(4 * kRadB));
+    // accepted cuts, largest first, while the intervals fit kSegMax
+    bool bottom = false, topcut = false;
+    uint32_t ni = 0, nint = 0;  // accepted internal cuts (bit j: tg[j])
+    uint64_t total = 0;
+    uint32_t ncut = 0;
+#pragma unroll
+    for (int j = 0; j < TG; j++) {
+        if (tg[j] <= thr) continue;
+        const bool b = to[j] == 0u, t = to[j] == n;
+        const uint32_t K = 1u + nint + (bottom ? 1u : 0u) + (b ? 1u : 0u) + (!b && !t ? 1u : 0u);
+        if (K > (uint32_t)kSegMax) continue;
+        if (b) bottom = true;
+        else if (t) topcut = true;
+        else ni |= 1u << j, nint++;
+        total += tg[j];
+        ncut++;
+    }
+    if (total < range / 2u || ncut == 0) return false;
+    // the spacing inside the dense parts: the mean of the other gaps
+    const uint64_t delta = max<uint64_t>(1u, (range - total) / (n + 1u - ncut));
+    // the internal cuts in key order
+    uint32_t co[kSegMax - 1];
+    int64_t cl[kSegMax - 1], cr[kSegMax - 1];
+    uint64_t cg[kSegMax - 1];
+    uint64_t gbot = 0, gtop = 0;
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < TG; j++) {
+        if ((ni >> j) & 1u) {
+            const uint32_t q = c < kSegMax - 1 ? c : kSegMax - 2;
+            co[q] = to[j], cl[q] = tl[j], cr[q] = tr[j], cg[q] = tg[j];
+            c++;
+        }
+        if (to[j] == 0u && bottom && tg[j] > thr) gbot = tg[j];
+        if (to[j] == n && topcut && tg[j] > thr) gtop = tg[j];
+    }
+    for (uint32_t x = 0; x < nint; x++)
+        for (uint32_t y = x + 1; y < nint; y++)
+            if (co[y] < co[x]) {
+                uint32_t to2 = co[x]; co[x] = co[y]; co[y] = to2;
+                int64_t t2 = cl[x]; cl[x] = cl[y]; cl[y] = t2;
+                t2 = cr[x]; cr[x] = cr[y]; cr[y] = t2;
+                const uint64_t g2 = cg[x]; cg[x] = cg[y]; cg[y] = g2;
+            }
+    // the intervals: [st, en] and their weights
+    int64_t st[kSegMax], en[kSegMax];
+    double wt[kSegMax];  // width in spacings
+    uint32_t K = 0;
+    if (bottom) {  // the previous bucket's tail: its last samples' spacing
+        // (the middle two of its last four gaps: one of them may cross a gap)
+        uint64_t dp = delta;
+        if (p0 >= 5u) {
+            uint64_t g4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) g4[i] = (uint64_t)ss[p0 - 1 - i] - (uint64_t)ss[p0 - 2 - i];
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 3; y++)
+                    if (g4[y] > g4[y + 1]) {
+                        const uint64_t t2 = g4[y];
+                        g4[y] = g4[y + 1], g4[y + 1] = t2;
+                    }
+            dp = max<uint64_t>(1u, g4[1] / 2u + g4[2] / 2u);
+        }
+        st[0] = lo;
+        en[0] = (int64_t)((uint64_t)lo + min(kSegMargin * dp, gbot / 4u));
+        wt[0] = (double)((uint64_t)en[0] - (uint64_t)lo + 1u) / (double)dp;
+        K = 1;
+    }
+    for (uint32_t j = 0; j <= nint; j++) {
+        const uint32_t o0 = j == 0 ? 0u : co[j - 1], o1 = j == nint ? n : co[j];
+        const int64_t f = j == 0 ? first : cr[j - 1], e = j == nint ? prev : cl[j];
+        const uint32_t cnt = o1 - o0;
+        const uint64_t dk = cnt >= 8u ? max<uint64_t>(1u, ((uint64_t)e - (uint64_t)f) / (cnt - 1u)) : delta;
+        const uint64_t gb = j == 0 ? gbot : cg[j - 1], ga = j == nint ? gtop : cg[j];
+        st[K] = (j == 0 && !bottom) ? lo : (int64_t)((uint64_t)f - min(kSegMargin * dk, gb / 4u));
+        en[K] = (j == nint && !topcut) ? hi : (int64_t)((uint64_t)e + min(kSegMargin * dk, ga / 4u));
+        wt[K] = (double)((uint64_t)en[K] - (uint64_t)st[K] + 1u) / (double)dk;
+        K++;
+    }
+    double W = 0;
+    for (uint32_t k = 0; k < K; k++) W += wt[k];
+    const uint64_t dense = D - K;  // the rest: one gap sub-bucket per interval
+    uint32_t db = 0;
+    for (uint32_t k = 0; k < kSegMax; k++) {
+        if (k >= K) {
+            // unused: copies of the last interval (part_b's search may land on them)
+            sg.st[k] = sg.st[K - 1], sg.s32[k] = sg.s32[K - 1], sg.pk[k] = sg.pk[K - 1], sg.ms[k] = sg.ms[K - 1];
+            continue;
+        }
+        uint64_t dn = max<uint64_t>(1u, (uint64_t)((double)(dense - K) * wt[k] / W));
+        // the interval's residuals r = key - st < R (R > dn), shifted under 2^32
+        const uint64_t R1 = max((uint64_t)en[k] - (uint64_t)st[k], dn);  // R - 1
+        const uint32_t sh = R1 >> 32 ? 64u - (uint32_t)__clzll((long long)(R1 >> 32)) : 0u;  // bits of R1 >> 32
+        const uint64_t Rs = (R1 >> sh) + 1u;  // <= 2^32
+        dn = min(dn, Rs - 1u);
+        const uint32_t s32 = (uint32_t)((dn << 32) / Rs);
+        sg.st[k] = st[k];
+        sg.s32[k] = s32;
+        sg.pk[k] = db | (uint32_t)dn << 11 | sh << 22;
+        // keys per sub-bucket <= (ceil(2^32 / s32) + 1) << sh
+        sg.ms[k] = bases_maxspan((((1ull << 32) + s32 - 1u) / s32 + 1u) << sh, (uint64_t)((double)Lm * wt[k] / W), dn, skew);
+        db += (uint32_t)dn + 1u;
+    }
+    sg.hi = hi;
+    sg.nseg = K;
+    for (int k = 0; k < 21; k++) sg.pad[k] = 0;
+    return true;
+}
+
 __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams p) {
     __shared__ uint32_t s_wsum[kBasesWaves];
     __shared__ int64_t s_mm[2 * kBasesWaves];
+    __shared__ int64_t s_ss[kSampleN];  // the samples in key order (seg_plan), staged once
+    __shared__ uint32_t s_M;
     const int a = threadIdx.x, lane = a & 63, wave = a >> 6;
+    if (p.seg) {
+        if (wave == 0) {
+            uint32_t m = lane < kSampleGatherBlocks ? (uint32_t)p.samp[kSampleN + lane] : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
+            if (lane == 0) s_M = m;
+        }
+        // every load issued before the first store: one memory latency, not
+        // one per 4 KiB (a load-store loop: bases 18 -> 41 us, r06z4)
+        constexpr int SI = kSampleN / 2 / kOffsA;
+        static_assert(kSampleN / 2 % kOffsA == 0, "whole int4 rows per thread");
+        const int4 *src = reinterpret_cast<const int4 *>(p.samp + kSortedOff);
+        int4 v[SI];
+#pragma unroll
+        for (int i = 0; i < SI; i++) v[i] = src[a + i * kOffsA];
+#pragma unroll
+        for (int i = 0; i < SI; i++) reinterpret_cast<int4 *>(s_ss)[a + i * kOffsA] = v[i];
+    }
     // global min / max of the selected keys over both tables
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (int x = 0; x < p.ntab; x++)  // per (segment, wave) partials of msd_runs_seg_kernel
@@ -1087,7 +1330,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
     int64_t lo = 0;
     uint64_t scale = 0;
     uint32_t maxspan = kRadB, s32 = 0, heavy = 0;
-    bool one_key = false;
+    bool one_key = false, seg = false;
     if (a < kBucketsA) {
         // bucket a = (spl[a-1], spl[a]] (open ends: the global min / max),
         // less a repeated splitter value, which is bucket i + 1 of its first
@@ -1108,7 +1351,6 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             // k >= 2 gets lone sub-buckets of ~kOne rows, 6 standard deviations
             // (uniform keys) below the cap: a multi-key sub-bucket over the cap
             // would leave the LDS path for the (slow) LSD fallback
-            constexpr uint64_t kFill = (uint64_t)kGroupCap * 15 / 16, kOne = (uint64_t)kGroupCap * 13 / 16;
             // (combined packing: groups of ~2 kFill rows of both tables)
             const uint64_t Lm = p.combined ? ((uint64_t)Lt[0] + Lt[1] + 1u) / 2u : (uint64_t)max(Lt[0], Lt[1]);
             uint64_t D = kRadB;
@@ -1129,29 +1371,19 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             // (one multiply in part_b instead of a 64 x 64 high product)
             if (range < 0xffffffffull) s32 = (uint32_t)(((uint64_t)D << 32) / (range + 1u));
             // keys per sub-bucket <= ceil(2^K / scale) + 1 =: w (K = 64, or 32
-            // with s32; ~(range + 1) / D + 2).  Group spans stay within the final
-            // kernel's counting range when one sub-bucket fits it, else below
-            // 2^48 (the radix tiers' sort word); the group kernel computes the
-            // exact span of every group
-            const uint64_t w = s32 ? ((1ull << 32) + s32 - 1u) / s32 + 1u
-                                   : (uint64_t)((((unsigned __int128)1 << 64) + scale - 1u) / scale) + 1u;
-            uint64_t span = w <= (uint64_t)kStageRange ? (uint64_t)kStageRange / w : ((uint64_t)1 << 48) / w;
-            // narrow groups (<= kStageRange keys: the staged kernel) of `span`
-            // sub-buckets hold ~span Lm / D rows per table; well under a full
-            // group, full groups spanning more keys for the wide-span staged
-            // kernel cost less (round 6, r06g: C3's tables with keys over
-            // [1, 1e9] made groups of two sub-buckets, msd_final 3.3 ms against
-            // 1.6 at [1, 3e8] and 2.1 on wide groups).  SMJ_WIDE_FILL = the
-            // narrow fill (percent of kFill) below which a bucket goes wide.
-            // Not when the pass-A sample repeats many keys (plan->skew over
-            // kWideSkew of its ~8192): few distinct keys with long equal-key
-            // runs fill the narrow groups whatever the interval, and the wide
-            // kernel hands bins over 32 rows on.  (Joining tables repeat a few:
-            // an S key sampled together with its R partner.)
-            if (w <= (uint64_t)kStageRange && Lm > 0 && p.plan->skew < kWideSkew &&
-                span * Lm * 100u < (uint64_t)SMJ_WIDE_FILL * kFill * D)
-                span = ((uint64_t)1 << 48) / w;
-            maxspan = span >= (uint64_t)kRadB ? (uint32_t)kRadB : span ? (uint32_t)span : 1u;
+            // with s32; ~(range + 1) / D + 2)
+            const uint64_t w = s32 ? ((1ull << 32) + s32 - 1u) / s32 + 1u : sub_width(scale);
+            maxspan = bases_maxspan(w, Lm, D, p.plan->skew);
+            // keys in dense intervals with wide gaps between (clustered keys)
+            if (p.seg && !p.full_radix && heavy == 0u && p.plan->skew < kWideSkew) {
+                MsdSeg sg;
+                if (seg_plan(s_ss, s_M, a, lo, hi, D, Lm, p.plan->skew, sg)) {
+                    seg = true;
+                    p.seg[a] = sg;
+                    scale = 1, s32 = 0, maxspan = kRadB;  // (unused: nonzero, so not single-key sub-buckets)
+                    atomicAdd(&p.plan->nsegb, 1u);
+                }
+            }
         }
     }
     for (int x = 0; x < p.ntab; x++) {
@@ -1171,7 +1403,7 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             b.list_base = lb;
             b.nruns = C;
             b.tile_base = tb;
-            b.one_key = (one_key ? 1u : 0u) | (heavy << 8);
+            b.one_key = (one_key ? 1u : 0u) | (seg ? kBucketSeg : 0u) | (heavy << 8);
             b.s32 = s32;
             p.bk[x][a] = b;
         }
@@ -1334,6 +1566,21 @@ __device__ __forceinline__ uint32_t pb_digit_heavy(uint32_t lin, const int64_t *
     return lin + 2u * c + (eq ? 1u : 0u);
 }
 
+// the segmented digit (MsdSeg's first 16 words in LDS: st[0..7], s32 at 8, pk
+// at 12 (u32 pairs)): the last interval starting at or below the key
+// (st[0] = lo <= every key of the bucket), then its linear sub-bucket or, past
+// the interval, its gap sub-bucket
+__device__ __forceinline__ uint32_t pb_digit_seg(const int64_t *sg, int64_t key) {
+    uint32_t k = 0;  // (the unused entries repeat the last interval: any of them gives its digit)
+#pragma unroll
+    for (uint32_t j = 1; j < (uint32_t)kSegMax; j++) k += key >= sg[j] ? 1u : 0u;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(sg + kSegMax);
+    const uint32_t s32 = w[k], pk = w[kSegMax + k];
+    const uint64_t r = ((uint64_t)key - (uint64_t)sg[k]) >> seg_sh(pk);
+    const uint32_t m = (r >> 32) ? seg_dn(pk) : min(__umulhi((uint32_t)r, s32), seg_dn(pk));
+    return seg_db(pk) + m;
+}
+
 // Diagnostic phase stamps of part_b (SMJ_DEBUG_MSD=1; off in production):
 // [k] cycles of phase k summed over tiles (thread 0's view), [7] tiles.
 // Ablation bits for smj_debug_part_b_time (timing only, output invalid):
@@ -1431,6 +1678,8 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
         for (int i = tid; i < QB / 16; i += NT) reinterpret_cast<uint4 *>(s_q)[i] = make_uint4(0, 0, 0, 0);
         if (msd_heavy_count(b.one_key) && tid < kHeavyMax)  // read after two barriers; padded (heavy_rank)
             s_hv[tid] = (uint32_t)tid < msd_heavy_count(b.one_key) ? p.heavy[(int64_t)ti.x * kHeavyMax + tid] : INT64_MAX;
+        if ((b.one_key & kBucketSeg) && tid < 16)  // a segmented digit instead (no heavy keys then)
+            s_hv[tid] = reinterpret_cast<const int64_t *>(p.seg + ti.x)[tid];
         if (p.dbg & 32) goto lookups_done;
         if (tid < J) reinterpret_cast<uint64_t *>(s_list)[tid] = le;
         for (int j = tid + NT; j < J; j += NT)  // > NT runs: rare
@@ -1486,6 +1735,11 @@ __global__ __launch_bounds__(pb_threads(COLS), COLS == 2 ? 8 : COLS == 1 ? 2 : 4
             for (int it = 0; it < ITEMS; it++)
                 if ((vmask >> it) & 1u)
                     dig[it] = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
+        }
+        if (__builtin_expect((b.one_key & kBucketSeg) != 0u, 0)) {  // clustered keys: the segmented digit
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++)
+                if ((vmask >> it) & 1u) dig[it] = pb_digit_seg(s_hv, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
         }
         // Atomic path: per quad of waves one u16 count per sub-bucket, ranks in
         // atomic order.  Stability is restored per row below among the rows
@@ -1790,6 +2044,19 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                 reinterpret_cast<uint2 *>(s_hv)[hm + lane] = make_uint2(lo, hi);
             }
         }
+        const bool sgb = (b.one_key & kBucketSeg) != 0u;  // block-uniform: a segmented digit (clustered keys)
+        if (__builtin_expect(sgb, 0)) {  // its 16 words, eight per wave of the first two (scalar loads, as above)
+            const uint32_t w8 = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 8u;
+            if (w8 < 16u) {
+                SMJ_CONST(int64_t) *hq = (SMJ_CONST(int64_t) *)uni64((uint64_t)(reinterpret_cast<const int64_t *>(p.seg + ti.x) + w8));
+                const int64_t h0 = hq[0], h1 = hq[1], h2 = hq[2], h3 = hq[3], h4 = hq[4], h5 = hq[5], h6 = hq[6],
+                              h7 = hq[7];
+                const int l8 = lane & 7;
+                const int64_t v = l8 == 0 ? h0 : l8 == 1 ? h1 : l8 == 2 ? h2 : l8 == 3 ? h3 : l8 == 4 ? h4
+                                                                                           : l8 == 5 ? h5 : l8 == 6 ? h6 : h7;
+                if (lane < 8) s_hv[w8 + lane] = v;
+            }
+        }
         __syncthreads();
 
         uint32_t dig[ITEMS];  // sub-bucket | atomic rank << 16, then the staging position
@@ -1810,6 +2077,14 @@ __global__ __launch_bounds__(pb_threads(COLS), 8) void msd_part_b_pipe_kernel(co
                     const uint32_t hd = pb_digit_heavy(dig[it], s_hv, hm, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
                     dig[it] = ((vmask >> it) & 1u) ? hd : dig[it];
                 }
+                asm volatile("" ::: "memory");
+            }
+        }
+        if (__builtin_expect(sgb, 0)) {  // the segmented digit, one item at a time (two spilled)
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                const uint32_t sd = pb_digit_seg(s_hv, pick<COLS>(rows[it], p.key_col)) & (RADIX - 1);
+                dig[it] = ((vmask >> it) & 1u) ? sd : dig[it];
                 asm volatile("" ::: "memory");
             }
         }
@@ -2048,6 +2323,23 @@ constexpr int kGroupThreads = 1024;
 constexpr uint32_t kGrpReady = 0x80000000u;  // ngrp[a]: bucket a's group count is published
 constexpr int kGroupLevels = 11;  // 2^11 = kRadB: binary-lifting levels over the group starts
 static_assert((1 << kGroupLevels) == kRadB, "one level per bit of a group index");
+// the segmented digit's interval of sub-bucket b (the last with db <= b)
+__device__ __forceinline__ uint32_t seg_of(const MsdSeg &sg, uint32_t b) {
+    uint32_t k = 0;
+    for (uint32_t j = 1; j < sg.nseg; j++) k = seg_db(sg.pk[j]) <= b ? j : k;
+    return k;
+}
+// the smallest key of sub-bucket b of a segmented digit (b = one past the
+// last: hi + 1): interval k's linear sub-bucket j = b - db[k] <= dn[k] starts
+// at st[k] + (ceil(j 2^32 / s32[k]) << sh[k]) (j = dn[k]: the gap sub-bucket,
+// the first key past en[k])
+__device__ __int128 seg_lower(const MsdSeg &sg, uint32_t b) {
+    const uint32_t k = seg_of(sg, b), pk = sg.pk[k], j = b - seg_db(pk);
+    if (j > seg_dn(pk)) return (__int128)sg.hi + 1;
+    const uint64_t q = (((uint64_t)j << 32) + sg.s32[k] - 1u) / sg.s32[k];
+    return (__int128)sg.st[k] + (__int128)((unsigned __int128)q << seg_sh(pk));
+}
+
 __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroupParams p) {
     constexpr int NW = kGroupThreads / 64, SB = kRadB / kGroupThreads;
     __shared__ uint32_t s_P[2][kRadB + 1];          // row prefix over sub-buckets, per table (P[kRadB] = total)
@@ -2061,6 +2353,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     __shared__ int s_ng, s_a;
     __shared__ int64_t s_hk[kHeavyMax];             // the bucket's heavy keys (ascending)
     __shared__ uint16_t s_hs[kHeavyMax], s_hl[kHeavyMax];  // heavy key j's sub-bucket, and its linear sub-bucket
+    __shared__ MsdSeg s_sg;                         // the bucket's segmented digit (kBucketSeg)
     // The bucket is a ticket, not blockIdx.x: dispatch order (and which XCD
     // gets a workgroup when) is undefined, so a workgroup waiting on a lower
     // blockIdx could wait on one that is not resident yet -- and with other
@@ -2115,6 +2408,8 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
     }
     __syncthreads();
     const bool single_sub = p.bk[0][a].scale == 0;  // every sub-bucket holds one key value
+    const bool sgb = (p.bk[0][a].one_key & kBucketSeg) != 0u;  // a segmented digit (MsdSeg)
+    if (sgb && t < 64) reinterpret_cast<uint32_t *>(&s_sg)[t] = reinterpret_cast<const uint32_t *>(p.seg + a)[t];
     // heavy keys (msd_heavy_kernel): heavy key j alone in sub-bucket
     // s_hs[j] = lin(h_j) + 2 j + 1 -- a group of its own, flagged single-key
     // (streamed in stable order); the others' linear sub-bucket of a digit d
@@ -2153,6 +2448,7 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
                            : b0.s32      ? ((1ull << 32) + b0.s32 - 1u) / b0.s32 + 1u
                                          : (uint64_t)((((unsigned __int128)1 << 64) + b0.scale - 1u) / b0.scale) + 1u;
         comb = comb && w * (uint64_t)b0.maxspan <= (uint64_t)kStageRange;  // (msd_bases: not a wide bucket)
+        comb = comb && !sgb;  // (its gap sub-buckets span wide)
         for (int x = 0; x < p.ntab; x++)
             comb = comb && (p.bk[x][a].L + (uint32_t)p.tile[x] - 1) / (uint32_t)p.tile[x] <= (uint32_t)kStList;
     }
@@ -2195,6 +2491,10 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
                 const uint32_t c = heavy_below((uint32_t)i, is);
                 if (is) lim = i + 1;
                 else if (c < hm) lim = min(lim, (int)s_hs[c]);
+            }
+            if (sgb) {  // a group stays inside one interval's linear sub-buckets; a gap sub-bucket is its own
+                const uint32_t k = seg_of(s_sg, (uint32_t)i), d0 = seg_db(s_sg.pk[k]), dn = seg_dn(s_sg.pk[k]);
+                lim = (uint32_t)i >= d0 + dn ? i + 1 : min(lim, min(i + (int)s_sg.ms[k], (int)(d0 + dn)));
             }
             f = next_nz(max(lim, i + 1));
         }
@@ -2317,7 +2617,10 @@ __global__ __launch_bounds__(kGroupThreads) void msd_group_kernel(const MsdGroup
             l1 = (is ? (uint32_t)s_hl[c] : b1 - 1u - 2u * c) + 1u;
         }
         unsigned __int128 r0 = l0, r1 = l1;
-        if (s32) {
+        if (sgb) {  // the segmented digit: offsets from lo
+            r0 = seg_lower(s_sg, b0) - (__int128)p.bk[0][a].lo;
+            r1 = seg_lower(s_sg, b1) - (__int128)p.bk[0][a].lo;
+        } else if (s32) {
             r0 = (((uint64_t)l0 << 32) + s32 - 1u) / s32;
             r1 = (((uint64_t)l1 << 32) + s32 - 1u) / s32;
         } else if (sc) {

@@ -305,6 +305,17 @@ def msd_wstage():
     return int(lib.smj_debug_msd_wstage())
 
 
+def msd_segmented():
+    """Pass-A buckets of the last MSD pipeline call given a segmented pass-B
+    digit (MsdSeg in smj_internal.h: keys in dense intervals with wide gaps
+    between, e.g. clustered keys)."""
+    lib = _lib.load()
+    if not hasattr(lib, "smj_debug_msd_segmented"):
+        return 0
+    lib.smj_debug_msd_segmented.restype = ctypes.c_int64
+    return int(lib.smj_debug_msd_segmented())
+
+
 def debug_wide_maxrun(rows=-1):
     """Diagnostic: the wide-span staged kernel hands a group to the radix tier
     when one of its bins holds more than `rows` rows (-1: the built-in limit;

@@ -801,3 +801,77 @@ def test_random_two_column_wide_spans(gpu, oracle_built, seed):
     np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
     if nr and ns:
         np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
+def clustered(rng, n, cols, kind, key_col, payload0):
+    """Clustered keys (the segmented pass-B digit, MsdSeg): dense runs of keys
+    far apart, so that pass-A buckets straddle the gaps."""
+    u = rng.integers(1, 3 * max(n, 1), size=n, dtype=np.int64, endpoint=True)
+    if kind == "clust64":      # 64 clusters 2^40 apart (tools/shape_probe.py)
+        k = (u % 64) * (1 << 40) + u // 64
+    elif kind == "clust1k":    # 1024 clusters 2^33 apart: several in one pass-A bucket
+        k = (u % 1024) * (1 << 33) + u // 1024
+    elif kind == "clustout":   # 64 clusters and 0.2 % of the rows anywhere (keys in the gaps)
+        k = (u % 64) * (1 << 40) + u // 64
+        out = rng.random(n) < 0.002
+        k[out] = rng.integers(I64.min, I64.max, size=int(out.sum()), dtype=np.int64, endpoint=True)
+    elif kind == "clustext":   # 64 clusters over the whole signed range, the extremes themselves included
+        k = ((u % 64) - 32) * (1 << 57) + u // 64
+        k[rng.random(n) < 0.001] = I64.min
+        k[rng.random(n) < 0.001] = I64.max
+    elif kind == "clust3":     # 3 unequal clusters (90 / 9 / 1 %) 2^50 apart
+        r = rng.random(n)
+        k = np.where(r < 0.9, 0, np.where(r < 0.99, 1 << 50, 1 << 51)) + u
+    elif kind == "clustdup":   # clusters of 200 distinct keys each (long equal-key runs)
+        k = (u % 64) * (1 << 40) + (u // 64) % 200
+    else:
+        raise ValueError(kind)
+    t = rng.integers(-1000, 1000, size=(n, cols), dtype=np.int64)
+    t[:, key_col] = k
+    if cols > 1:
+        t[:, (key_col + 1) % cols] = payload0 + np.arange(n)
+    return t
+
+
+SEG_CASES = [
+    # nr, ns, cols, key1, key2, kind, select1, segmented buckets expected (None: either)
+    (1_000_000, 1_000_000, 2, 0, 0, "clust64", None, True),
+    (600_000, 800_000, 2, 1, 1, "clust1k", None, True),
+    (700_000, 700_000, 2, 0, 0, "clustout", None, True),
+    (500_000, 500_000, 2, 0, 0, "clustext", None, True),
+    (800_000, 600_000, 2, 0, 0, "clust3", None, True),
+    (400_000, 400_000, 2, 0, 0, "clustdup", None, False),
+    (300_000, 350_000, 3, 2, 0, "clust64", None, True),
+    (300_000, 350_000, 3, 2, 0, "clust64", (1, 0), None),     # a WHERE keeping ~1/2000 of R
+    (400_000, 300_000, 1, 0, 0, "clust1k", None, True),
+    (60_000, 2_000_000, 2, 0, 0, "clust64", None, None),     # R keys ~11 times in S: skew gates the digit off
+]
+
+
+@pytest.mark.parametrize("nr,ns,cols,k1,k2,kind,s1,seg", SEG_CASES)
+def test_clustered_keys_segmented_digit(gpu, oracle_built, monkeypatch, nr, ns, cols, k1, k2, kind, s1, seg):
+    """Clustered keys through the segmented pass-B digit (msd_bases_kernel's
+    seg_plan, part_b's pb_digit_seg, the group kernel's seg_lower): bit for
+    bit against the oracle, the same output with the digit switched off
+    (SMJ_SEG=0), and the digit in use where the sample shows the gaps."""
+    from smj import ops
+    rng = np.random.default_rng(nr + 7 * ns + cols)
+    R = clustered(rng, nr, cols, kind, k1, 0)
+    S = clustered(rng, ns, cols, kind, k2, 10 ** 9)
+    pick = rng.random(ns) < 1 / 3  # R's keys in a third of S's rows
+    S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, None)
+    torch.cuda.synchronize()
+    nseg = ops.msd_segmented()
+    Rs, Ss, J = ref_pipeline(R, S, k1, k2, s1, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, cols))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, cols))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 2 * cols - 1))
+    assert len(J) > 0
+    if seg is not None:
+        assert (nseg > 0) == seg, nseg
+    monkeypatch.setenv("SMJ_SEG", "0")
+    gR2, gS2, gJ2 = ops.sort_merge_join(dev(R), dev(S), k1, k2, s1, None)
+    torch.cuda.synchronize()
+    assert ops.msd_segmented() == 0
+    assert torch.equal(gR2, gR) and torch.equal(gS2, gS) and torch.equal(gJ2, gJ)

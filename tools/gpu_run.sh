@@ -334,6 +334,9 @@ for s in $STEPS; do
                --output-format csv -d "$OUT/pmc_sq2" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 $NOCPU $BA ;;
     pmclist) run pmclist 60 rocprofv3 -L ;;
     shapes) run shapes 600 python tools/shape_probe.py ;;
+    shapesh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so run shapesh 600 python tools/shape_probe.py ;;
+    seg)   test_run seg 600 $PYT tests/test_gpu_msd.py -k clustered ;;
+    segp)  run segp 600 python tools/seg_probe.py ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     finabv) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/ablate/libsmj_hip.so run finabv 300 python tools/final_ablate.py ;;
