@@ -527,6 +527,7 @@ struct MsdScratch {
     int64_t *heavy = nullptr;           // [kBucketsA][kHeavyMax] heavy keys per bucket (msd_heavy_kernel)
     uint32_t *nheavy = nullptr;         // [kBucketsA] their count
     MsdSeg *seg = nullptr;              // [kBucketsA] segmented pass-B digits (msd_bases_kernel)
+    MsdSegFind *segf = nullptr;         // [kBucketsA] their intervals (msd_runs_seg_kernel)
     uint32_t *p1c = nullptr;            // chunked partition: device [2][kP1cWords]: rows per (chunk, part), flags
     uint32_t *h_p1c = nullptr;          // pinned twin
     void *p1desc[2] = {nullptr, nullptr};  // its parts' part_a tile descriptors per table
@@ -589,6 +590,7 @@ int msd_scratch(MsdScratch **out) {
         HIP_TRY(dev_alloc(&m.heavy, sizeof(int64_t) * kBucketsA * kHeavyMax));
         HIP_TRY(dev_alloc(&m.nheavy, sizeof(uint32_t) * kBucketsA));
         HIP_TRY(dev_alloc(&m.seg, sizeof(MsdSeg) * kBucketsA));
+        HIP_TRY(dev_alloc(&m.segf, sizeof(MsdSegFind) * kBucketsA));
         HIP_TRY(hipHostMalloc(&m.h_p1c, sizeof(uint32_t) * 2 * kP1cWords, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_plan, sizeof(MsdPlan), hipHostMallocDefault));
         HIP_TRY(hipHostMalloc(&m.h_samp, sizeof(int64_t) * (2 * kSampleMax + 64), hipHostMallocDefault));
@@ -610,7 +612,7 @@ void msd_free_one(MsdScratch &m) {  // also a set whose creation failed half-way
     for (void *p : {(void *)m.spl, (void *)m.samp, (void *)m.groups, (void *)m.gpart, (void *)m.cpart, (void *)m.ngrp, (void *)m.counts, (void *)m.offs, (void *)m.single_list,
                     (void *)m.big_list, (void *)m.wide_list, (void *)m.radix_list, (void *)m.plan, m.slots, m.work, m.jb, m.cwork, (void *)m.d_tmp,
                     (void *)m.lspl, m.giant, m.gmap, m.gh, m.pst[0], m.pst[1], m.p1st, (void *)m.p1d, m.pick,
-                    (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy, (void *)m.seg})
+                    (void *)m.p1c, m.p1desc[0], m.p1desc[1], (void *)m.heavy, (void *)m.nheavy, (void *)m.seg, (void *)m.segf})
         dev_free(p);
     hipHostFree(m.p1h);
     hipHostFree(m.h_p1c);
@@ -1054,6 +1056,7 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
             HIP_TRY(launch_msd_sample(sp, s));
         }
     }
+
     size_t pa[2] = {(size_t)-1, (size_t)-1};
     std::vector<hipEvent_t> chunk_ev;  // staged input: one event per landed chunk
     struct EvRelease {
@@ -1120,6 +1123,14 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
             ra.tinfo[x] = (uint2 *)ms->t[x].tinfo;
         }
         ra.ntab = ntab;
+        // the segmented digit's sample scan (clustered keys; SMJ_SEG=0: the linear digit everywhere)
+        const bool seg_on = !(getenv("SMJ_SEG") && atoi(getenv("SMJ_SEG")) == 0);
+        if (seg_on) {
+            ra.seg_samp = ms->samp;
+            ra.seg_spl = ms->spl;
+            ra.seg_plan = ms->plan;
+            ra.segf = ms->segf;
+        }
         HIP_TRY(launch_msd_runs_seg(ra, s));
         uint32_t *sa[4], *ta[4];
         for (int x = 0; x < ntab; x++) {
@@ -1167,9 +1178,8 @@ int msd_front(const MsdIn *in, int ntab, int join, int key2, hipStream_t s, cons
         bp.spl = ms->spl;
         bp.plan = ms->plan;
         bp.pack_ok = pack_mode;
-        bp.samp = ms->samp;
-        // the segmented digit (clustered keys; SMJ_SEG=0: the linear one everywhere)
-        bp.seg = getenv("SMJ_SEG") && atoi(getenv("SMJ_SEG")) == 0 ? nullptr : ms->seg;
+        bp.segf = seg_on ? ms->segf : nullptr;
+        bp.seg = ms->seg;
         HIP_TRY(launch_msd_bases(bp, s));
         HIP_TRY(launch_msd_runs_apply(ra, s));
     }

@@ -309,7 +309,8 @@ struct MsdPartA2 {       // one part_a launch over up to two tables
 };
 // samp + kSortedOff: the select kernel's samples in key order (msd_bases_kernel's segmented digit)
 constexpr int kSortedOff = 2 * kSampleMax + 64;
-constexpr int kSampScratch = kSortedOff + 2 * kSampleMax;  // int64 words of MsdScratch::samp
+constexpr int kSampScratch = kSortedOff + 2 * kSampleMax + 64;  // int64 words of MsdScratch::samp (+ the
+                                                                 // over-read of seg_plan's fixed-count loads)
 // A segmented pass-B digit (MsdBucket::one_key bit 1, kBucketSeg): a bucket
 // whose sampled keys sit in up to kSegMax dense intervals separated by wide
 // empty gaps (clustered keys: an interval straddling two clusters 2^40 apart
@@ -332,6 +333,14 @@ struct MsdSeg {
     int64_t hi;            // the bucket's last key
     uint32_t ms[kSegMax];  // sub-buckets a final group of the interval may span (MsdBucket::maxspan)
     uint32_t nseg, pad[21];
+};
+// seg_find's intervals of a bucket (extra workgroups of msd_runs_seg_kernel)
+// for msd_bases_kernel, which sizes their sub-buckets
+struct MsdSegFind {
+    int64_t st[kSegMax], en[kSegMax];
+    float wt[kSegMax];   // expected rows (width in sample spacings)
+    uint32_t K, topcut;  // K = 0: not segmented; topcut: the last interval ends before hi
+    uint32_t pad[6];
 };
 __host__ __device__ inline uint32_t seg_db(uint32_t pk) { return pk & 0x7ffu; }
 __host__ __device__ inline uint32_t seg_dn(uint32_t pk) { return (pk >> 11) & 0x7ffu; }
@@ -437,8 +446,8 @@ struct MsdBasesParams {
     MsdPlan *plan;
     int pack_ok;               // msd_packb_mode() with 2-column tables: MsdPlan::packB may be set (2: despite skew)
     const uint32_t *nheavy;    // [kBucketsA] heavy keys per bucket (msd_heavy_kernel), nullptr = none
-    const int64_t *samp;       // MsdSampleParams::samp: the valid-sample counts and the sorted samples
-    MsdSeg *seg;               // out: [kBucketsA] segmented digits; nullptr = none (SMJ_SEG=0)
+    const MsdSegFind *segf;    // [kBucketsA] intervals (msd_runs_seg_kernel); nullptr = none (SMJ_SEG=0)
+    MsdSeg *seg;               // out: [kBucketsA] segmented digits
 };
 struct MsdPartBParams {
     const int64_t *srcA;
@@ -618,12 +627,20 @@ struct MsdRunsArgs {     // msd_runs_seg / msd_runs_apply over both tables (bloc
     uint32_t *segL[2], *segC[2];
     const int64_t *tmm[2];
     int64_t *segmm[2];
+    // the segmented digit's sample scan (seg_find_all, extra workgroups of msd_runs_seg_kernel; segf =
+    // nullptr: none): samples in key order (MsdSampleParams::samp), splitters, plan->skew.  (Before T:
+    // a host source's macro T = int64_t turns `int T[2]` into a member named int64_t.)
+    const int64_t *seg_samp = nullptr;
+    const int64_t *seg_spl = nullptr;
+    const MsdPlan *seg_plan = nullptr;
+    MsdSegFind *segf = nullptr;
     int T[2], TB[2];
     const MsdBucket *bk[2];
     uint2 *list[2], *tinfo[2];
     int ntab;
 };
 hipError_t launch_msd_runs_seg(const MsdRunsArgs &a, hipStream_t s);
+
 hipError_t launch_msd_seg_scan(uint32_t *const *seg, uint32_t *const *tot, int narr, hipStream_t s);
 hipError_t launch_msd_bases(const MsdBasesParams &p, hipStream_t s);
 hipError_t launch_msd_heavy(const MsdHeavyParams &p, hipStream_t s);

@@ -385,11 +385,12 @@ __global__ __launch_bounds__(1024) void msd_sample_select_kernel(const MsdSample
 template <int COLS>
 __global__ __launch_bounds__(pa_threads(COLS), pa_waves_per_eu(COLS)) void msd_part_a_kernel(
     const MsdPartA2 q) {
+    const unsigned bid = blockIdx.x;
     // one launch may cover both tables (the same column count): blocks past
     // q.tiles0 take table 1's tiles
-    const bool second = blockIdx.x >= q.tiles0;
+    const bool second = bid >= q.tiles0;
     const MsdPartAParams &p = second ? q.t[1] : q.t[0];
-    const unsigned bx = blockIdx.x - (second ? q.tiles0 : 0u);
+    const unsigned bx = bid - (second ? q.tiles0 : 0u);
     constexpr int ITEMS = pa_items(COLS), T = msd_tile_a(COLS), RADIX = kBucketsA;
     constexpr int NT = pa_threads(COLS), NW = NT / 64;
     constexpr int ROWB = T * COLS * 8, CNTB = NW * RADIX * 4;
@@ -1071,135 +1072,91 @@ __device__ uint64_t sub_width(uint64_t scale) {
 
 // The segmented pass-B digit of bucket a (MsdSeg), from its sampled keys in
 // key order (msd_sample_select_kernel: positions (at(a - 1), at(a)] hold the
-// bucket's ~32).  The gaps between consecutive samples -- and from lo to the
-// first, from the last to hi -- are the candidates: with delta the mean gap
-// less the kSegMax largest (the spacing inside the dense parts), a gap over 32
-// delta, over 1/16 of the interval and over 4 kRadB keys separates two dense
-// intervals, and the bucket is segmented when such gaps make up half its
-// interval (uniform keys: the largest of ~33 gaps is ~3.5 delta, so a uniform
-// bucket never is).  A dense interval runs from its first to its last sample
-// widened by kSegMargin = 6 spacings on each side (rows past the extreme
-// samples: ~1 spacing's worth on average, e^-6 of one beyond 6), so the gap
-// sub-buckets stay near empty; a gap at the bottom (the bucket's lo lies in a
-// gap: the previous cluster's unsampled tail sits just above lo) makes a
-// first interval [lo, lo + 6 spacings of the previous bucket's last samples].
-// Up to kSegMax intervals (the largest gaps; a bucket spanning more clusters
-// keeps some of them in one interval).
-// Sub-buckets go to the intervals by their width in spacings (expected rows,
-// margins included: a count of ~8 samples was too noisy -- r06y, sub-buckets
-// of 1000 rows), so rows per sub-bucket stay even; the spacing is the
-// interval's own over 8 or more samples, else the bucket's (delta).
+// bucket's ~32), one wave per bucket, a lane per sample.  The gaps between
+// consecutive samples -- and from lo to the first, from the last to hi --
+// are the candidates:
+//  1. the largest gap G, the sum S and number c of the gaps over range / 16
+//     (a cut is one of them, and cuts must sum to range / 2), and delta0 =
+//     the mean of the other gaps (the spacing inside the dense parts); a
+//     bucket with S < range / 2 or G under 16 delta0 has no gaps (uniform
+//     keys: S ~0.4 range, G ~4 spacings);
+//  2. the cuts: gaps over thr = max(32 delta0, range / 16, 4 kRadB); the
+//     bucket is segmented when they sum to half its interval;
+//  3. the intervals, in key order, between the cuts (the first kSegMax - 1
+//     internal ones; a bucket spanning more clusters keeps the rest inside its
+//     last interval).  An interval runs from its first to its last sample
+//     widened by kSegMargin = 6 of its spacings on each side (rows past the
+//     extreme samples: ~1 spacing's worth on average, e^-6 of one beyond 6),
+//     so the gap sub-buckets stay near empty; a cut at the bottom (lo lies in
+//     a gap: the previous cluster's unsampled tail sits just above lo) makes a
+//     first interval [lo, lo + 6 spacings of the previous bucket's last
+//     samples].  Its weight = its width in spacings (expected rows, margins
+//     included: a count of ~8 samples was too noisy -- r06y, sub-buckets of
+//     1000 rows); the spacing is the interval's own over 8 or more samples,
+//     else the bucket's (delta, the mean of the non-cut gaps).
+// Where it runs: extra workgroups of msd_runs_seg_kernel, under its other
+// workgroups' time (a thread per bucket in the one-workgroup bases kernel
+// cost ~6 us on the critical path, r06z11; a side-stream kernel ~15 us,
+// r06z14; four extra workgroups of part_a ~18 us, r06z17).
 constexpr uint64_t kSegMargin = 6;  // spacings past an interval's extreme samples
-__device__ bool seg_plan(const int64_t *ss, uint32_t M, int a, int64_t lo, int64_t hi, uint64_t D, uint64_t Lm,
-                         uint32_t skew, MsdSeg &sg) {
-    if (M < (uint32_t)(8 * kBucketsA) || M > (uint32_t)kSampleN) return false;
+constexpr int kSegFindBlocks = 16;  // msd_runs_seg_kernel's extra workgroups (4 buckets per wave)
+constexpr unsigned kRunsSegX = (kBucketsA + 63) / 64;  // their blockIdx.x
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, 64);
+    return v;
+}
+__device__ void seg_find(const int64_t *ss, uint32_t M, int a, int64_t lo, int64_t hi, MsdSegFind *out) {
+    const int lane = threadIdx.x & 63;
     auto at = [&](int q) { return min(M - 1u, (uint32_t)(((uint64_t)(q + 1) * M) / (kSplA + 1))); };
     const uint32_t p0 = a == 0 ? 0u : at(a - 1) + 1u, p1 = a >= kSplA ? M - 1u : at(a);
-    if (p1 < p0 || p1 - p0 > 1024u) return false;
+    if (p1 < p0 || p1 - p0 >= 64u) return;  // (~32 per bucket; more: leave it linear)
     const uint64_t range = (uint64_t)hi - (uint64_t)lo;
-    {  // a light first pass: the largest gap alone.  No gap can be a cut when it
-       // is under 32 x the least delta0 below can be (the top TG gaps at most TG
-       // x the largest): uniform buckets end here (C3: bases 37 -> ~18 us)
-        uint32_t n1 = 0;
-        int64_t pv = lo;
-        uint64_t G = 0;
-        for (uint32_t i = p0; i <= p1; i++) {
-            const int64_t k = ss[i];
-            const bool in = k >= lo && k <= hi;
-            G = in ? max(G, (uint64_t)k - (uint64_t)pv) : G;
-            pv = in ? k : pv;
-            n1 += in ? 1u : 0u;
-        }
-        G = max(G, (uint64_t)hi - (uint64_t)pv);
-        if (n1 < 16) return false;
-        const uint64_t topb = G > range / kSegMax ? range : (uint64_t)kSegMax * G;
-        if (G / 32u <= (range - topb) / (n1 + 1u - kSegMax)) return false;
-    }
-    // the kSegMax largest gaps: size, ordinal of the sample after it (0: from
-    // lo; n: to hi), and its ends
-    constexpr int TG = kSegMax;
-    uint64_t tg[TG];
-    uint32_t to[TG];
-    int64_t tl[TG], tr[TG];
-#pragma unroll
-    for (int j = 0; j < TG; j++) tg[j] = 0, to[j] = 0, tl[j] = tr[j] = 0;
-    auto insert = [&](uint64_t g, uint32_t o, int64_t l, int64_t r) {
-#pragma unroll
-        for (int j = 0; j < TG; j++)
-            if (g > tg[j]) {
-                const uint64_t g2 = tg[j];
-                const uint32_t o2 = to[j];
-                const int64_t l2 = tl[j], r2 = tr[j];
-                tg[j] = g, to[j] = o, tl[j] = l, tr[j] = r;
-                g = g2, o = o2, l = l2, r = r2;
-            }
-    };
-    uint32_t n = 0;
-    int64_t prev = lo, first = lo;
-    for (uint32_t i = p0; i <= p1; i++) {
-        const int64_t k = ss[i];
-        if (k < lo || k > hi) continue;
-        if (n == 0) first = k;
-        insert((uint64_t)k - (uint64_t)prev, n, prev, k);
-        prev = k;
-        n++;
-    }
-    if (n < 16) return false;
-    insert((uint64_t)hi - (uint64_t)prev, n, prev, hi);
-    uint64_t top = 0;
-#pragma unroll
-    for (int j = 0; j < TG; j++) top += tg[j];
-    // (a low estimate: the largest in-cluster gaps are left out too)
-    const uint64_t delta0 = max<uint64_t>(1u, (range - min(range, top)) / (n + 1u - TG));
+    // lane j: sample p0 + j; the valid ones (in [lo, hi]) are a run of lanes
+    const bool have = (uint32_t)lane <= p1 - p0;
+    const int64_t k = have ? ss[p0 + lane] : hi;
+    const bool in = have && k >= lo && k <= hi;
+    const uint64_t vm = __ballot(in);
+    const uint32_t n = (uint32_t)__popcll(vm);
+    if (n < 16) return;
+    const int l0 = __ffsll((long long)vm) - 1, l1 = 63 - __clzll((long long)vm);
+    const int64_t up = __shfl_up((long long)k, 1, 64);
+    const uint64_t g = in ? (uint64_t)k - (uint64_t)(lane == l0 ? lo : up) : 0u;  // the gap below sample lane
+    const int64_t first = __shfl((long long)k, l0, 64), last = __shfl((long long)k, l1, 64);
+    const uint64_t gtop0 = (uint64_t)hi - (uint64_t)last;
+    // 1.
+    const uint64_t r16 = range / 16u;
+    const uint64_t G = max(wave_max64(g), gtop0);
+    const uint64_t S = wave_sum64(g > r16 ? g : 0u) + (gtop0 > r16 ? gtop0 : 0u);
+    const uint32_t c = (uint32_t)__popcll(__ballot(g > r16)) + (gtop0 > r16 ? 1u : 0u);
+    if (S < range / 2u || c > n) return;
+    const uint64_t delta0 = max<uint64_t>(1u, (range - S) / (n + 1u - c));
+    if (G / 16u <= delta0) return;
+    // 2.
     const uint64_t thr = max(max(32u * delta0, range / 16u), (uint64_t)(4 * kRadB));
-    // accepted cuts, largest first, while the intervals fit kSegMax
-    bool bottom = false, topcut = false;
-    uint32_t ni = 0, nint = 0;  // accepted internal cuts (bit j: tg[j])
-    uint64_t total = 0;
-    uint32_t ncut = 0;
-#pragma unroll
-    for (int j = 0; j < TG; j++) {
-        if (tg[j] <= thr) continue;
-        const bool b = to[j] == 0u, t = to[j] == n;
-        const uint32_t K = 1u + nint + (bottom ? 1u : 0u) + (b ? 1u : 0u) + (!b && !t ? 1u : 0u);
-        if (K > (uint32_t)kSegMax) continue;
-        if (b) bottom = true;
-        else if (t) topcut = true;
-        else ni |= 1u << j, nint++;
-        total += tg[j];
-        ncut++;
-    }
-    if (total < range / 2u || ncut == 0) return false;
-    // the spacing inside the dense parts: the mean of the other gaps
+    const uint64_t cm = __ballot(g > thr);  // cut below sample lane
+    const bool topcut = gtop0 > thr, bottom = (cm >> l0) & 1ull;
+    const uint64_t total = wave_sum64(g > thr ? g : 0u) + (topcut ? gtop0 : 0u);
+    const uint32_t ncut = (uint32_t)__popcll(cm) + (topcut ? 1u : 0u);
+    if (total < range / 2u || ncut == 0) return;
     const uint64_t delta = max<uint64_t>(1u, (range - total) / (n + 1u - ncut));
-    // the internal cuts in key order
-    uint32_t co[kSegMax - 1];
-    int64_t cl[kSegMax - 1], cr[kSegMax - 1];
-    uint64_t cg[kSegMax - 1];
-    uint64_t gbot = 0, gtop = 0;
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < TG; j++) {
-        if ((ni >> j) & 1u) {
-            const uint32_t q = c < kSegMax - 1 ? c : kSegMax - 2;
-            co[q] = to[j], cl[q] = tl[j], cr[q] = tr[j], cg[q] = tg[j];
-            c++;
-        }
-        if (to[j] == 0u && bottom && tg[j] > thr) gbot = tg[j];
-        if (to[j] == n && topcut && tg[j] > thr) gtop = tg[j];
-    }
-    for (uint32_t x = 0; x < nint; x++)
-        for (uint32_t y = x + 1; y < nint; y++)
-            if (co[y] < co[x]) {
-                uint32_t to2 = co[x]; co[x] = co[y]; co[y] = to2;
-                int64_t t2 = cl[x]; cl[x] = cl[y]; cl[y] = t2;
-                t2 = cr[x]; cr[x] = cr[y]; cr[y] = t2;
-                const uint64_t g2 = cg[x]; cg[x] = cg[y]; cg[y] = g2;
-            }
-    // the intervals: [st, en] and their weights
-    int64_t st[kSegMax], en[kSegMax];
-    double wt[kSegMax];  // width in spacings
+    const uint64_t gbot = bottom ? (uint64_t)__shfl((unsigned long long)g, l0, 64) : 0u;
+    const uint64_t gtop = topcut ? gtop0 : 0u;
+    // 3. (wave-uniform: the intervals are a handful; lane 0 stores them)
     uint32_t K = 0;
+    auto emit = [&](int64_t st, int64_t en, uint64_t dk) {
+        if (lane == 0) {
+            out->st[K] = st;
+            out->en[K] = en;
+            out->wt[K] = (float)((double)((uint64_t)en - (uint64_t)st + 1u) / (double)dk);
+        }
+        K++;
+    };
     if (bottom) {  // the previous bucket's tail: its last samples' spacing
         // (the middle two of its last four gaps: one of them may cross a gap)
         uint64_t dp = delta;
@@ -1217,24 +1174,78 @@ __device__ bool seg_plan(const int64_t *ss, uint32_t M, int a, int64_t lo, int64
                     }
             dp = max<uint64_t>(1u, g4[1] / 2u + g4[2] / 2u);
         }
-        st[0] = lo;
-        en[0] = (int64_t)((uint64_t)lo + min(kSegMargin * dp, gbot / 4u));
-        wt[0] = (double)((uint64_t)en[0] - (uint64_t)lo + 1u) / (double)dp;
-        K = 1;
+        emit(lo, (int64_t)((uint64_t)lo + min(kSegMargin * dp, gbot / 4u)), dp);
     }
-    for (uint32_t j = 0; j <= nint; j++) {
-        const uint32_t o0 = j == 0 ? 0u : co[j - 1], o1 = j == nint ? n : co[j];
-        const int64_t f = j == 0 ? first : cr[j - 1], e = j == nint ? prev : cl[j];
-        const uint32_t cnt = o1 - o0;
+    uint64_t cuts = cm & ~(1ull << l0);  // the internal cuts (lanes whose gap below is one)
+    int fl = l0;                          // the open interval's first lane
+    while (true) {
+        int el = l1;
+        uint64_t ga = gtop;
+        bool open_end = !topcut;
+        const bool cut = cuts != 0 && K + 2u <= (uint32_t)kSegMax;  // (room for this interval and the last)
+        if (cut) {
+            const int cl = __ffsll((long long)cuts) - 1;
+            cuts &= cuts - 1;
+            el = cl - 1;
+            ga = (uint64_t)__shfl((unsigned long long)g, cl, 64);
+            open_end = false;
+        }
+        const int64_t f = __shfl((long long)k, fl, 64), e = __shfl((long long)k, el, 64);
+        const uint32_t cnt = (uint32_t)(el - fl + 1);
+        const uint64_t gb = fl == l0 ? gbot : (uint64_t)__shfl((unsigned long long)g, fl, 64);
         const uint64_t dk = cnt >= 8u ? max<uint64_t>(1u, ((uint64_t)e - (uint64_t)f) / (cnt - 1u)) : delta;
-        const uint64_t gb = j == 0 ? gbot : cg[j - 1], ga = j == nint ? gtop : cg[j];
-        st[K] = (j == 0 && !bottom) ? lo : (int64_t)((uint64_t)f - min(kSegMargin * dk, gb / 4u));
-        en[K] = (j == nint && !topcut) ? hi : (int64_t)((uint64_t)e + min(kSegMargin * dk, ga / 4u));
-        wt[K] = (double)((uint64_t)en[K] - (uint64_t)st[K] + 1u) / (double)dk;
-        K++;
+        const int64_t st = (fl == l0 && !bottom) ? lo : (int64_t)((uint64_t)f - min(kSegMargin * dk, gb / 4u));
+        const int64_t en = open_end ? hi : (int64_t)((uint64_t)e + min(kSegMargin * dk, ga / 4u));
+        emit(st, en, dk);
+        if (!cut) break;
+        fl = el + 1;
     }
-    double W = 0;
-    for (uint32_t k = 0; k < K; k++) W += wt[k];
+    if (lane == 0) {
+        out->topcut = topcut ? 1u : 0u;
+        out->K = K;
+    }
+}
+
+// msd_runs_seg_kernel's extra workgroups (blockIdx.x == kRunsSegX, y <
+// kSegFindBlocks), a wave per bucket: seg_find over every bucket, K = 0 where
+// it finds no gaps.  The end buckets' open ends (the global min / max: that
+// kernel's partials) are taken as the extreme samples; msd_bases_kernel
+// extends the end intervals to them.
+__device__ void seg_find_all(const MsdRunsArgs &q, int blk) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blk * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6), nw = kSegFindBlocks * (int)(blockDim.x >> 6);
+    uint32_t M = lane < kSampleGatherBlocks ? (uint32_t)q.seg_samp[kSampleN + lane] : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) M += __shfl_xor(M, o, 64);
+    const int64_t *ss = q.seg_samp + kSortedOff, *spl = q.seg_spl;
+    const bool ok = q.seg_plan->skew < kWideSkew && M >= (uint32_t)(8 * kBucketsA) && M <= (uint32_t)kSampleN;
+    for (int a = wave; a < kBucketsA; a += nw) {
+        MsdSegFind *out = q.segf + a;
+        if (lane == 0) out->K = 0;
+        if (!ok || (a >= 1 && a < kSplA && spl[a] == spl[a - 1])) continue;  // (a heavy key's bucket / a run of repeats)
+        // bucket a = (spl[a-1], spl[a]] as msd_bases_kernel has it
+        const int64_t lo = a == 0 ? ss[0] : (int64_t)((uint64_t)spl[a - 1] + 1u);
+        int64_t hi = a == kSplA ? ss[M - 1] : spl[a];
+        if (a + 1 < kSplA && spl[a + 1] == spl[a]) hi = (int64_t)((uint64_t)spl[a] - 1u);
+        if (hi > lo && (uint64_t)hi - (uint64_t)lo >= (uint64_t)kRadB) seg_find(ss, M, a, lo, hi, out);
+    }
+}
+
+// msd_bases_kernel: the sub-buckets of seg_find's intervals.  The first
+// interval starts at lo, the last ends at hi unless a gap was cut there (the
+// end buckets: seg_find saw the extreme samples).  Sub-buckets go to the
+// intervals by their weights, one gap sub-bucket after each.
+__device__ void seg_finish(const MsdSegFind &f, int64_t lo, int64_t hi, uint64_t D, uint64_t Lm, uint32_t skew,
+                           MsdSeg &sg) {
+    const uint32_t K = f.K;
+    int64_t st[kSegMax], en[kSegMax];
+    float W = 0.f;
+    for (uint32_t k = 0; k < K; k++) {
+        st[k] = f.st[k], en[k] = f.en[k];
+        W += f.wt[k];
+    }
+    st[0] = lo;
+    if (!f.topcut) en[K - 1] = hi;
     const uint64_t dense = D - K;  // the rest: one gap sub-bucket per interval
     uint32_t db = 0;
     for (uint32_t k = 0; k < kSegMax; k++) {
@@ -1243,7 +1254,8 @@ __device__ bool seg_plan(const int64_t *ss, uint32_t M, int a, int64_t lo, int64
             sg.st[k] = sg.st[K - 1], sg.s32[k] = sg.s32[K - 1], sg.pk[k] = sg.pk[K - 1], sg.ms[k] = sg.ms[K - 1];
             continue;
         }
-        uint64_t dn = max<uint64_t>(1u, (uint64_t)((double)(dense - K) * wt[k] / W));
+        const float w = f.wt[k] / W;
+        uint64_t dn = max<uint64_t>(1u, (uint64_t)((float)(dense - K) * w));
         // the interval's residuals r = key - st < R (R > dn), shifted under 2^32
         const uint64_t R1 = max((uint64_t)en[k] - (uint64_t)st[k], dn);  // R - 1
         const uint32_t sh = R1 >> 32 ? 64u - (uint32_t)__clzll((long long)(R1 >> 32)) : 0u;  // bits of R1 >> 32
@@ -1254,39 +1266,18 @@ __device__ bool seg_plan(const int64_t *ss, uint32_t M, int a, int64_t lo, int64
         sg.s32[k] = s32;
         sg.pk[k] = db | (uint32_t)dn << 11 | sh << 22;
         // keys per sub-bucket <= (ceil(2^32 / s32) + 1) << sh
-        sg.ms[k] = bases_maxspan((((1ull << 32) + s32 - 1u) / s32 + 1u) << sh, (uint64_t)((double)Lm * wt[k] / W), dn, skew);
+        sg.ms[k] = bases_maxspan((((1ull << 32) + s32 - 1u) / s32 + 1u) << sh, (uint64_t)((float)Lm * w), dn, skew);
         db += (uint32_t)dn + 1u;
     }
     sg.hi = hi;
     sg.nseg = K;
     for (int k = 0; k < 21; k++) sg.pad[k] = 0;
-    return true;
 }
 
 __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams p) {
     __shared__ uint32_t s_wsum[kBasesWaves];
     __shared__ int64_t s_mm[2 * kBasesWaves];
-    __shared__ int64_t s_ss[kSampleN];  // the samples in key order (seg_plan), staged once
-    __shared__ uint32_t s_M;
     const int a = threadIdx.x, lane = a & 63, wave = a >> 6;
-    if (p.seg) {
-        if (wave == 0) {
-            uint32_t m = lane < kSampleGatherBlocks ? (uint32_t)p.samp[kSampleN + lane] : 0u;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
-            if (lane == 0) s_M = m;
-        }
-        // every load issued before the first store: one memory latency, not
-        // one per 4 KiB (a load-store loop: bases 18 -> 41 us, r06z4)
-        constexpr int SI = kSampleN / 2 / kOffsA;
-        static_assert(kSampleN / 2 % kOffsA == 0, "whole int4 rows per thread");
-        const int4 *src = reinterpret_cast<const int4 *>(p.samp + kSortedOff);
-        int4 v[SI];
-#pragma unroll
-        for (int i = 0; i < SI; i++) v[i] = src[a + i * kOffsA];
-#pragma unroll
-        for (int i = 0; i < SI; i++) reinterpret_cast<int4 *>(s_ss)[a + i * kOffsA] = v[i];
-    }
     // global min / max of the selected keys over both tables
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (int x = 0; x < p.ntab; x++)  // per (segment, wave) partials of msd_runs_seg_kernel
@@ -1375,9 +1366,10 @@ __global__ __launch_bounds__(kOffsA) void msd_bases_kernel(const MsdBasesParams 
             const uint64_t w = s32 ? ((1ull << 32) + s32 - 1u) / s32 + 1u : sub_width(scale);
             maxspan = bases_maxspan(w, Lm, D, p.plan->skew);
             // keys in dense intervals with wide gaps between (clustered keys)
-            if (p.seg && !p.full_radix && heavy == 0u && p.plan->skew < kWideSkew) {
+            if (p.segf && !p.full_radix && heavy == 0u && p.plan->skew < kWideSkew && p.segf[a].K) {
                 MsdSeg sg;
-                if (seg_plan(s_ss, s_M, a, lo, hi, D, Lm, p.plan->skew, sg)) {
+                seg_finish(p.segf[a], lo, hi, D, Lm, p.plan->skew, sg);
+                {
                     seg = true;
                     p.seg[a] = sg;
                     scale = 1, s32 = 0, maxspan = kRadB;  // (unused: nonzero, so not single-key sub-buckets)
@@ -1469,6 +1461,10 @@ __device__ __forceinline__ void runs_apply_body(const uint32_t *__restrict__ off
 // both tables in one launch (blockIdx.z = table): one ramp and tail instead of two
 __global__ __launch_bounds__(256) void msd_runs_seg_kernel(const MsdRunsArgs a) {
     const int x = blockIdx.z;
+    if (blockIdx.x == kRunsSegX) {  // the segmented digit's sample scan (dispatched early: low y)
+        if (a.segf && x == 0 && blockIdx.y < (unsigned)kSegFindBlocks) seg_find_all(a, (int)blockIdx.y);
+        return;
+    }
     if (x >= a.ntab) return;
     runs_seg_body(x ? a.offs[1] : a.offs[0], x ? a.ntiles[1] : a.ntiles[0], kOffsARow, kBucketsA,
                   x ? a.segL[1] : a.segL[0], x ? a.segC[1] : a.segC[0], x ? a.tmm[1] : a.tmm[0],
@@ -5769,14 +5765,15 @@ hipError_t launch_msd_part_a(const MsdPartAParams &p, int cols, hipStream_t s) {
     return launch_msd_part_a_tiles(p, cols, 0, pa_tiles(p, cols), s);
 }
 
+
 hipError_t launch_msd_part_a_tiles(const MsdPartAParams &p_in, int cols, int64_t t0, int64_t t1, hipStream_t s) {
     if (p_in.n <= 0 || t1 <= t0) return hipSuccess;
     MsdPartA2 q{};
     q.t[0] = p_in;
     q.t[0].tile0 = (int)t0;
     q.tiles0 = (unsigned)(t1 - t0);
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3((unsigned)(t1 - t0)), dim3(pa_threads(C)),
-                                             0, s, q));
+    const unsigned nb = q.tiles0;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(nb), dim3(pa_threads(C)), 0, s, q));
     return hipGetLastError();
 }
 
@@ -5788,8 +5785,8 @@ hipError_t launch_msd_part_a2(const MsdPartAParams &a, const MsdPartAParams &b, 
     q.tiles0 = (unsigned)pa_tiles(a, cols);
     const unsigned tiles1 = (unsigned)pa_tiles(b, cols);
     if (q.tiles0 + tiles1 == 0) return hipSuccess;
-    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(q.tiles0 + tiles1), dim3(pa_threads(C)), 0,
-                                             s, q));
+    const unsigned nb = q.tiles0 + tiles1;
+    SMJ_COLS_SWITCH(cols, hipLaunchKernelGGL((msd_part_a_kernel<C>), dim3(nb), dim3(pa_threads(C)), 0, s, q));
     return hipGetLastError();
 }
 
@@ -5799,7 +5796,8 @@ hipError_t launch_msd_sample_select(const MsdSampleParams &p, hipStream_t s) {
 }
 
 hipError_t launch_msd_runs_seg(const MsdRunsArgs &a, hipStream_t s) {
-    const dim3 grid((kBucketsA + 63) / 64, kMsdSegs, a.ntab);
+    static_assert(kSegFindBlocks <= kMsdSegs, "the scan's workgroups are a column of the grid");
+    const dim3 grid(kRunsSegX + (a.segf ? 1u : 0u), kMsdSegs, a.ntab);
     hipLaunchKernelGGL(msd_runs_seg_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -337,6 +337,12 @@ for s in $STEPS; do
     shapesh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so run shapesh 600 python tools/shape_probe.py ;;
     seg)   test_run seg 600 $PYT tests/test_gpu_msd.py -k clustered ;;
     segp)  run segp 600 python tools/seg_probe.py ;;
+    kbis)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # bases-kernel bisection: kernel stats per variant
+           for v in bis1 headv; do
+             SMJ_LIB=$V/$v/libsmj_hip.so run kstat_$v 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstat_$v" -o c3 -- \
+               python bench.py --workload c3 --steps 5 --warmup 2 $NOCPU || exit 1
+             rm -f "$OUT/kstat_$v/c3_kernel_trace.csv"
+           done ;;
     phases) run phases 300 python tools/msd_phases.py ;;
     finab) run finab 300 python tools/final_ablate.py ;;
     finabv) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/ablate/libsmj_hip.so run finabv 300 python tools/final_ablate.py ;;
