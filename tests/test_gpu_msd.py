@@ -875,3 +875,26 @@ def test_clustered_keys_segmented_digit(gpu, oracle_built, monkeypatch, nr, ns, 
     torch.cuda.synchronize()
     assert ops.msd_segmented() == 0
     assert torch.equal(gR2, gR) and torch.equal(gS2, gS) and torch.equal(gJ2, gJ)
+
+
+@pytest.mark.parametrize("kind,parts", [("clust64", 3), ("clust1k", 2), ("clustout", 4)])
+def test_clustered_keys_partitioned(gpu, oracle_built, kind, parts):
+    """The segmented digit inside the partitioned mode (each key-range part
+    runs the pipeline on its own sample: some parts hold one cluster, some a
+    gap), bit for bit against the oracle."""
+    from smj import ops
+    rng = np.random.default_rng(77 + parts)
+    R = clustered(rng, 800_000, 2, kind, 0, 0)
+    S = clustered(rng, 900_000, 2, kind, 0, 10 ** 9)
+    pick = rng.random(len(S)) < 1 / 3
+    S[pick, 0] = R[rng.integers(0, len(R), size=int(pick.sum())), 0]
+    ops.force_parts(parts)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, None, None)
+        torch.cuda.synchronize()
+    finally:
+        ops.force_parts(0)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
