@@ -3879,8 +3879,36 @@ __device__ __forceinline__ bool st_sort(const MsdFinalParams &p, const MsdGroup 
     fl = fl > 1u ? fl : 0u;  // rounds of the equal-key fix-up (0: no run)
     wsb ^= 1;
     ST_SUB(1);
-    const bool lsd = fl > (uint32_t)SMJ_ST_MAXRUN;  // block-uniform
+    bool lsd = fl > (uint32_t)SMJ_ST_MAXRUN;  // block-uniform
     if (lsd && tid == 0) atomicAdd(&p.plan->nlsd, 1u);
+    // One key value per table (keys of ~1000 rows per table, a group each: a
+    // run that long is the whole table part): the gather order is the stable
+    // order, no LSD -- each row's rank becomes its table row, so the scatter
+    // below places it there, and no rounds follow.  Checked only on the LSD
+    // branch (C3 never takes it).
+    if (lsd) {  // a bin holding all of a table's rows (an empty table: any bin)
+        uint32_t f = 0;
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            const uint32_t nx = x ? nS : nR;
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const uint32_t h = sm.hist[x][tid * W + i];
+                f |= ((h & 0xffffu) == nx || (h >> 16) == nx) ? (1u << x) : 0u;
+            }
+        }
+        const int fr = __syncthreads_or((int)(f & 1u)), fs = __syncthreads_or((int)(f & 2u));
+        if (fr && fs) {
+#pragma unroll
+            for (int k = 0; k < kStIt; k++)
+                if (w[k] != ~0u) {
+                    const uint32_t v = (uint32_t)(tid + k * kStThreads);
+                    w[k] = (w[k] & 0xffff0000u) | (L.is_s(k, v) ? v - sp : v);
+                }
+            lsd = false;
+            fl = 0;
+        }
+    }
 #pragma unroll
     for (int x = 0; x < 2; x++) {  // per-table starts (table rows)
         uint32_t run = x ? (ex >> 16) : (ex & 0xffffu);

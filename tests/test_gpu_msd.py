@@ -305,6 +305,37 @@ def test_long_equal_key_runs_in_lds(gpu, oracle_built, nkeys, n, cols):
     np.testing.assert_array_equal(host(gJ), J)
 
 
+@pytest.mark.parametrize("nkeys,n,heavy,skewed", [(2_000, 2_000_000, "0", False), (2_500, 3_000_000, "0", True),
+                                                  (30_000, 3_000_000, "1", False)])
+def test_single_key_groups_skip_the_lsd(gpu, oracle_built, monkeypatch, nkeys, n, heavy, skewed):
+    """Keys of ~600-1000 rows per table: a final group is one key per table,
+    a run too long for the transposition rounds, and the staged kernel keeps
+    the gather order instead of running its LSD (every row of a table part in
+    one histogram bin).  Heavy-key detection off (SMJ_HEAVY=0) so that no key
+    takes the single-key sub-bucket path; the last case leaves it on with
+    more such keys per bucket than it flags.  Bit-exact against the oracle."""
+    from smj import ops
+    monkeypatch.setenv("SMJ_HEAVY", heavy)
+    rng = np.random.default_rng(nkeys + n)
+
+    def make(rows, pay0):
+        t = np.empty((rows, 2), dtype=np.int64)
+        t[:, 0] = rng.integers(0, nkeys, size=rows) * 7919 - 10 ** 9
+        t[:, 1] = pay0 + np.arange(rows)
+        return t
+
+    R = make(n // 10 if skewed else n, 0)
+    S = make(n, 10 ** 9)
+    gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S))
+    torch.cuda.synchronize()
+    dense, radix, wide, lsd = ops.msd_groups()
+    assert lsd > 0 and radix == 0, (dense, radix, wide, lsd)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs)
+    np.testing.assert_array_equal(host(gS), Ss)
+    np.testing.assert_array_equal(host(gJ), J)
+
+
 @pytest.mark.parametrize("c1,c2,sel", [(2, 2, None), (3, 4, (2, -(1 << 62) + (1 << 58)))])
 def test_many_oversized_groups_batched(gpu, oracle_built, monkeypatch, c1, c2, sel):
     """Hundreds of oversized multi-key groups (the shape Zipf tables produce
