@@ -62,6 +62,12 @@ def main():
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) * 1e3)
         times = sorted(times[2:])
+        if os.environ.get("SHAPE_PROF"):  # per-scope times of one more call
+            ops.prof_enable(True)
+            ops.sort_merge_join(R, S, kc, kc, None, None, R_sorted=bR, S_sorted=bS, out=J)
+            rep = ops.prof_report()
+            ops.prof_enable(False)
+            print("   ", {k: round(v["ms"], 3) for k, v in rep.items() if v["ms"] > 0.05}, flush=True)
         print(f"{name:28s} {times[len(times) // 2]:8.3f} ms  joined {j.shape[0]:>11,d}  groups/radix/wide/lsd "
               f"{ops.msd_groups()}  wstage {ops.msd_wstage()}  single/big {ops.msd_stats()[:2]}  "
               f"packB {ops.msd_packb()}", flush=True)
