@@ -337,6 +337,7 @@ for s in $STEPS; do
     shapesh) SMJ_LIB=$ROOT/pim-sort-merge-join_amd/lib/variants/headv/libsmj_hip.so run shapesh 600 python tools/shape_probe.py ;;
     seg)   test_run seg 600 $PYT tests/test_gpu_msd.py -k clustered ;;
     lsdt)  test_run lsdt 600 $PYT tests/test_gpu_msd.py -k "single_key_groups_skip or long_equal_key or zipf or heavy" ;;
+    sortt) test_run sortt 600 $PYT tests/test_gpu_msd.py -k "sorted_input" ;;
     segp)  run segp 600 python tools/seg_probe.py ;;
     kbis)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # bases-kernel bisection: kernel stats per variant
            for v in bis1 headv; do
