@@ -272,6 +272,7 @@ for s in $STEPS; do
               run loop_s$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_s$r.out" loop_split
               SMJ_DIST_SPLIT=0 run loop_n$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_n$r.out" loop_nosplit
             done ;;
+    loop4s0) SMJ_SEG=0 run loop4s0 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4s0.out" loop_c4_seg0 ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
