@@ -272,6 +272,20 @@ for s in $STEPS; do
               run loop_s$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_s$r.out" loop_split
               SMJ_DIST_SPLIT=0 run loop_n$r 300 python bench.py --loopback $NOCPU $BA && summ "$OUT/loop_n$r.out" loop_nosplit
             done ;;
+    trl4)  run trl4 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trl4" -o l4 -- \
+               python3 "$ROOT/bench.py" --loopback --workload c4 --steps 2 --warmup 1 $NOCPU --verify 0 ;;
+    loop4tr) SMJ_DIST_TRACE=2 run loop4tr 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4tr.out" loop_c4_trace ;;
+    memwait) # until the previous step's process has its device memory back (r06y5: a loopback C4 right
+             # after another large run waited 0.5 s in its exchange allocation)
+             python3 -c "
+import sys, time, torch
+t0 = time.time()
+while True:
+    free, total = torch.cuda.mem_get_info()
+    if total - free < 8 * 2 ** 30 or time.time() - t0 > 180:
+        print('memwait %.1f s, %.1f GiB held' % (time.time() - t0, (total - free) / 2 ** 30)); break
+    time.sleep(0.5)
+" | tee -a "$OUT/steps.log" ;;
     loop4s0) SMJ_SEG=0 run loop4s0 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4s0.out" loop_c4_seg0 ;;
     loop4) run loop4 900 python bench.py --loopback --workload c4 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop4.out" loop_c4 ;;
     loop5) run loop5 900 python bench.py --loopback --workload c5 --steps 3 --warmup 1 $NOCPU $BA && summ "$OUT/loop5.out" loop_c5 ;;
