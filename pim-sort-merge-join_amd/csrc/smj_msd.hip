@@ -1254,8 +1254,13 @@ __device__ void seg_finish(const MsdSegFind &f, int64_t lo, int64_t hi, uint64_t
             sg.st[k] = sg.st[K - 1], sg.s32[k] = sg.s32[K - 1], sg.pk[k] = sg.pk[K - 1], sg.ms[k] = sg.ms[K - 1];
             continue;
         }
+        // (kSegMax sub-buckets held back: a float product rounded up in every
+        // interval must not push the last digit past D - 1)
         const float w = f.wt[k] / W;
-        uint64_t dn = max<uint64_t>(1u, (uint64_t)((float)(dense - K) * w));
+        uint64_t dn = max<uint64_t>(1u, (uint64_t)((float)(dense - K - kSegMax) * w));
+        // and by construction: room for this interval's gap sub-bucket and two
+        // digits for each interval after it
+        dn = max<uint64_t>(1u, min<uint64_t>(dn, D - db - 1u - 2u * (K - 1u - k)));
         // the interval's residuals r = key - st < R (R > dn), shifted under 2^32
         const uint64_t R1 = max((uint64_t)en[k] - (uint64_t)st[k], dn);  // R - 1
         const uint32_t sh = R1 >> 32 ? 64u - (uint32_t)__clzll((long long)(R1 >> 32)) : 0u;  // bits of R1 >> 32
