@@ -288,6 +288,12 @@ def main():
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
+        # the previous step's joined rows are dead before the next step runs:
+        # holding them made every distributed step after the first allocate a
+        # second output buffer (6 GB at C4) inside the timed region -- 0.1-0.5 s
+        # on boxes whose driver was still returning an earlier process's memory
+        # (profiles/r06/r06y5, r06z2)
+        res = None
         res = step()
     torch.cuda.synchronize()
     if world > 1:
