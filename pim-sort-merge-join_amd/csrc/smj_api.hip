@@ -1330,6 +1330,17 @@ int msd_back(MsdCtx &cx, T *out_j, int64_t *h_rows, hipStream_t s) {
             HIP_TRY(launch_msd_final_tiers(fp, s));
         }
         pt = prof_last();
+        // the 64-bit tier lists a group whose keys span over 48 bits as
+        // oversized (final_group: plan->nbig, big_list) for the fallback
+        // below, which must see the plan as the tiers left it (far outliers
+        // next to dense keys: a wide sub-bucket's group handed down the tiers)
+        HIP_TRY(hipMemcpyAsync(ms->h_plan, ms->plan, sizeof(MsdPlan), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (ms->h_plan->err) {
+            fprintf(stderr, "smj: pipeline group plan inconsistent in the final tiers (err 0x%x)\n", ms->h_plan->err);
+            return SMJ_ERR_HIP;
+        }
+        if (t_slot < 0) g_msd_stats[1] = ms->h_plan->nbig;
     }
     ms->n_cwork = 0;  // (msd_fallback lists the oversized groups' join chunks, if any)
     MsdFinalParams ff = fp;  // packed pass-B rows: the single-key tier reads the words (pk_mode 3), the

@@ -4,6 +4,9 @@ CPU oracle, bit for bit: sorted R, sorted S and the joined rows.  The cases
 cover the pipeline's paths: normal LDS-sorted groups, single-key groups
 streamed without a sort (heavy / duplicate keys), and the LSD fallback for
 multi-key groups over the LDS capacity."""
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -906,6 +909,69 @@ def test_clustered_keys_segmented_digit(gpu, oracle_built, monkeypatch, nr, ns, 
     torch.cuda.synchronize()
     assert ops.msd_segmented() == 0
     assert torch.equal(gR2, gR) and torch.equal(gS2, gS) and torch.equal(gJ2, gJ)
+
+
+FAR_CASES = [
+    # outliers (fraction of rows, keys anywhere in int64), INT64_MIN rows in R / S, INT64_MAX rows per table
+    (0.01, 0, 45, 30),
+    (0.001, 0, 45, 0),
+    (0.01, 0, 2, 0),
+    (0.01, 20, 45, 30),
+]
+
+
+@pytest.mark.parametrize("maxrun", [-1, 0])
+@pytest.mark.parametrize("outl,min_r,min_s,nmax", FAR_CASES)
+def test_far_outliers_wide_groups(gpu, oracle_built, outl, min_r, min_s, nmax, maxrun):
+    """2-column tables of dense keys with far outliers and the signed extremes
+    (tools/seg_stress.py's failing shapes, round 6): a sparse bucket's
+    sub-buckets are wider than 2^48 keys, so a group handed down the final
+    tiers (wide staged kernel -> radix tier -> 64-bit tier) can span over 48
+    bits and become oversized there, after msd_back first read the plan;
+    those groups' rows were never written.  maxrun 0 hands every wide group's
+    bins down the tiers."""
+    from smj import ops
+    rng = np.random.default_rng(int(outl * 1e4) + 7 * min_r + min_s + nmax)
+    tabs = []
+    for x, nm in ((0, min_r), (1, min_s)):
+        n = 400_000
+        k = rng.integers(0, 10 ** 6, size=n, dtype=np.int64)
+        m = rng.random(n) < outl
+        k[m] = rng.integers(I64.min, I64.max, size=int(m.sum()), dtype=np.int64, endpoint=True)
+        k[rng.choice(n, nm, replace=False)] = I64.min
+        k[rng.choice(n, nmax, replace=False)] = I64.max
+        t = np.stack([k, x * 10 ** 9 + np.arange(n, dtype=np.int64)], axis=1)
+        tabs.append(t)
+    R, S = tabs
+    ops.debug_wide_maxrun(maxrun)
+    try:
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), 0, 0, None, None)
+        torch.cuda.synchronize()
+    finally:
+        ops.debug_wide_maxrun(-1)
+    Rs, Ss, J = ref_pipeline(R, S, 0, 0, None, None)
+    np.testing.assert_array_equal(host(gR), Rs.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gS), Ss.reshape(-1, 2))
+    np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
+
+
+def test_random_layout_stress(gpu, oracle_built):
+    """tools/seg_stress.py's seeded random tables (cluster count, gap, width,
+    outliers, duplicates, the extremes; 1-3 columns, either key column, WHEREs):
+    the seeds that failed before the round-6 plan re-read, and 40 more."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from seg_stress import case, first_diff
+    from smj import ops
+    bad = []
+    for seed in [11, 25, 29, 38, 86, 146, 399] + list(range(1000, 1040)):
+        _, cols, kc, R, S, sel = case(seed)
+        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, None)
+        torch.cuda.synchronize()
+        Rs, Ss, J = ref_pipeline(R, S, kc, kc, sel, None)
+        d = [first_diff("R", host(gR), Rs.reshape(-1, cols), kc), first_diff("S", host(gS), Ss.reshape(-1, cols), kc),
+             first_diff("J", host(gJ), J.reshape(-1, 2 * cols - 1), kc)]
+        bad += [f"seed {seed}: {x}" for x in d if x]
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("kind,parts", [("clust64", 3), ("clust1k", 2), ("clustout", 4)])

@@ -354,6 +354,15 @@ while True:
     lsdt)  test_run lsdt 600 $PYT tests/test_gpu_msd.py -k "single_key_groups_skip or long_equal_key or zipf or heavy" ;;
     sortt) test_run sortt 600 $PYT tests/test_gpu_msd.py -k "sorted_input" ;;
     segp)  run segp 600 python tools/seg_probe.py ;;
+    segst) test_run segst 600 python -u tools/seg_stress.py 0 400 420 ;;
+    extp)  run extp 300 python -u tools/ext_probe.py ${EXTP_SEEDS:-25 29 38 86} ;;
+    segd)  SD=--seeds=${SEGD_SEEDS:-11,25,29,38,86,146,399}  # failing stress seeds in detail, under each switch
+           run segd_def 300 python -u tools/seg_stress.py $SD
+           SMJ_SEG=0 run segd_noseg 300 python -u tools/seg_stress.py $SD
+           SMJ_ST_COMBINED=0 run segd_comb0 300 python -u tools/seg_stress.py $SD
+           SMJ_ST_COMBINED=1 run segd_comb1 300 python -u tools/seg_stress.py $SD
+           SMJ_PACKB=0 run segd_pk0 300 python -u tools/seg_stress.py $SD
+           SMJ_HEAVY=0 run segd_hv0 300 python -u tools/seg_stress.py $SD ;;
     kbis)  V=$ROOT/pim-sort-merge-join_amd/lib/variants  # bases-kernel bisection: kernel stats per variant
            for v in bis1 headv; do
              SMJ_LIB=$V/$v/libsmj_hip.so run kstat_$v 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstat_$v" -o c3 -- \

@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Randomised parity stress of the segmented pass-B digit (clustered keys):
+seeded tables of random cluster layouts (cluster count, gap, width, outliers,
+duplicates, the signed extremes), sizes, column counts, key columns and
+WHEREs, each checked bit for bit against the oracle.  Prints one line per
+failing seed and a summary.
+
+    python tools/seg_stress.py [first_seed] [seeds] [seconds]
+    python tools/seg_stress.py --seeds=11,25   (those seeds, each failure in detail)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "pim-sort-merge-join_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))  # (oracle/oracle.py, as tests/conftest.py has it)
+
+import torch  # noqa: E402
+
+import oracle  # noqa: E402
+from smj import ops  # noqa: E402
+
+I64 = np.iinfo(np.int64)
+
+
+def table(rng, n, cols, key_col, pay0, layout):
+    nclu, gap_bits, width, outl, dup = layout
+    u = rng.integers(0, width, size=n, dtype=np.int64)
+    c = rng.integers(0, nclu, size=n, dtype=np.int64)
+    k = (c - nclu // 2) * (np.int64(1) << np.int64(gap_bits)) + u
+    if dup:
+        k = k - (k % dup)
+    if outl:
+        m = rng.random(n) < outl
+        k[m] = rng.integers(I64.min, I64.max, size=int(m.sum()), dtype=np.int64, endpoint=True)
+    if rng.random() < 0.2:
+        k[rng.random(n) < 0.001] = I64.max
+        k[rng.random(n) < 0.001] = I64.min
+    t = rng.integers(-1000, 1000, size=(n, cols), dtype=np.int64)
+    t[:, key_col] = k
+    if cols > 1:
+        t[:, (key_col + 1) % cols] = pay0 + np.arange(n)
+    return t
+
+
+def case(seed):
+    rng = np.random.default_rng(10_000 + seed)
+    nclu = int(rng.choice([2, 3, 8, 64, 300, 1024, 5000]))
+    gap_bits = int(rng.integers(20, 58))
+    gap_bits = min(gap_bits, 62 - int(np.ceil(np.log2(nclu))))
+    width = int(rng.choice([10, 1000, 10 ** 5, 10 ** 6, 1 << 20]))
+    layout = (nclu, gap_bits, min(width, 1 << (gap_bits - 1)), float(rng.choice([0, 0, 0.001, 0.01])),
+              int(rng.choice([0, 0, 0, 7, 1000])))
+    cols = int(rng.choice([1, 2, 2, 2, 3]))
+    kc = int(rng.integers(0, cols))
+    nr, ns = (int(rng.integers(20_000, 700_000)) for _ in range(2))
+    R = table(rng, nr, cols, kc, 0, layout)
+    S = table(rng, ns, cols, kc, 10 ** 9, layout)
+    pick = rng.random(ns) < 0.3
+    S[pick, kc] = R[rng.integers(0, nr, size=int(pick.sum())), kc]
+    sel = None
+    if rng.random() < 0.3 and cols > 1:
+        sc = (kc + 1) % cols
+        sel = (sc, int(np.sort(R[:, sc])[int(rng.integers(0, nr))]))
+    return layout, cols, kc, R, S, sel
+
+
+def first_diff(name, g, o, kc):
+    """One line on how the device table g differs from the oracle's o."""
+    if g.shape != o.shape:
+        return f"{name}: rows {g.shape[0]} vs oracle {o.shape[0]}"
+    bad = np.nonzero((g != o).any(axis=1))[0]
+    if not len(bad):
+        return None
+    i = int(bad[0])
+    srt = bool((np.diff(g[:, kc]) >= 0).all()) if name != "J" else None
+    same = np.array_equal(g[np.lexsort(g.T[::-1])], o[np.lexsort(o.T[::-1])])
+    return (f"{name}: {len(bad)} rows differ, first {i}: {g[i].tolist()} vs {o[i].tolist()}"
+            f" (prev {o[max(i - 1, 0)].tolist()}) sorted {srt} same-multiset {same}")
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    seeds = None
+    for a in sys.argv[1:]:
+        if a.startswith("--seeds="):
+            seeds = [int(x) for x in a[8:].split(",")]
+    first = int(args[0]) if len(args) > 0 else 0
+    count = int(args[1]) if len(args) > 1 else 100
+    budget = float(args[2]) if len(args) > 2 else 240.0
+    t0 = time.time()
+    bad = done = seg_runs = 0
+    for seed in seeds if seeds is not None else range(first, first + count):
+        if time.time() - t0 > budget:
+            break
+        layout, cols, kc, R, S, sel = case(seed)
+        nr, ns = len(R), len(S)
+        gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), kc, kc, sel, None)
+        torch.cuda.synchronize()
+        nseg = ops.msd_segmented()
+        info = (ops.msd_packb(), ops.msd_groups(), ops.msd_stats())
+        seg_runs += nseg > 0
+        Rs = oracle.select_sort(R, kc, sel[0] if sel else 0, sel[1] if sel else None)
+        Ss = oracle.select_sort(S, kc, 0, None)
+        J = oracle.join(Rs, Ss, kc, kc)
+        diffs = [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, cols), kc),
+                 first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, cols), kc),
+                 first_diff("J", gJ.cpu().numpy(), J.reshape(-1, 2 * cols - 1), kc)]
+        diffs = [d for d in diffs if d]
+        done += 1
+        if done % 10 == 0:
+            print(f"  {done} seeds, {bad} failures, {time.time() - t0:.0f} s", flush=True)
+        if diffs:
+            bad += 1
+            print(f"FAIL seed {seed}: layout {layout} cols {cols} key {kc} n {nr}/{ns} sel {sel} segmented {nseg}", flush=True)
+            if seeds is not None:
+                print(f"    packb {info[0]} groups {info[1]} stats {info[2]}", flush=True)
+                for d in diffs:
+                    print("    " + d, flush=True)
+    print(f"seg_stress: {done} seeds, {bad} failures, {seg_runs} with segmented buckets, {time.time() - t0:.0f} s", flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
