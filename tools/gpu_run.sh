@@ -355,6 +355,8 @@ while True:
     sortt) test_run sortt 600 $PYT tests/test_gpu_msd.py -k "sorted_input" ;;
     segp)  run segp 600 python tools/seg_probe.py ;;
     segst) test_run segst 600 python -u tools/seg_stress.py 0 400 420 ;;
+    segst2) test_run segst2 600 python -u tools/seg_stress.py 400 1600 420 ;;
+    segmix) test_run segmix 600 python -u tools/seg_stress.py --mixed 0 400 420 ;;
     extp)  run extp 300 python -u tools/ext_probe.py ${EXTP_SEEDS:-25 29 38 86} ;;
     segd)  SD=--seeds=${SEGD_SEEDS:-11,25,29,38,86,146,399}  # failing stress seeds in detail, under each switch
            run segd_def 300 python -u tools/seg_stress.py $SD

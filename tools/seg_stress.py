@@ -7,6 +7,7 @@ failing seed and a summary.
 
     python tools/seg_stress.py [first_seed] [seeds] [seconds]
     python tools/seg_stress.py --seeds=11,25   (those seeds, each failure in detail)
+    python tools/seg_stress.py --mixed 0 200   (case_mixed: two shapes, WHEREs on both, partitioned mode)
 """
 import os
 import sys
@@ -68,6 +69,36 @@ def case(seed):
     return layout, cols, kc, R, S, sel
 
 
+def case_mixed(seed):
+    """Mixed shapes: R and S of their own column counts (1-5) and key
+    columns, a WHERE on either, tiny to 2M-row tables, and the partitioned
+    mode forced on some seeds (parts)."""
+    rng = np.random.default_rng(50_000 + seed)
+    nclu = int(rng.choice([1, 2, 8, 64, 1024]))
+    gap_bits = min(int(rng.integers(10, 58)), 62 - int(np.ceil(np.log2(max(nclu, 2)))))
+    width = int(rng.choice([10, 1000, 10 ** 6, 1 << 30]))
+    layout = (nclu, gap_bits, min(width, 1 << (gap_bits - 1)), float(rng.choice([0, 0, 0.001, 0.01])),
+              int(rng.choice([0, 0, 7])))
+    c1, c2 = (int(rng.choice([1, 2, 2, 3, 5])) for _ in range(2))
+    k1, k2 = int(rng.integers(0, c1)), int(rng.integers(0, c2))
+    nr, ns = (int(rng.choice([0, 1, 100, 5000, 300_000, 2_000_000])) if rng.random() < 0.3
+              else int(rng.integers(20_000, 900_000)) for _ in range(2))
+    R = table(rng, nr, c1, k1, 0, layout)
+    S = table(rng, ns, c2, k2, 10 ** 9, layout)
+    if nr and ns:
+        pick = rng.random(ns) < 0.3
+        S[pick, k2] = R[rng.integers(0, nr, size=int(pick.sum())), k1]
+    sels = []
+    for T, c, k in ((R, c1, k1), (S, c2, k2)):
+        sel = None
+        if rng.random() < 0.3 and c > 1 and len(T):
+            sc = (k + 1) % c
+            sel = (sc, int(np.sort(T[:, sc])[int(rng.integers(0, len(T)))]))
+        sels.append(sel)
+    parts = int(rng.choice([0, 0, 0, 2, 3])) if nr + ns > 100_000 else 0
+    return (layout, parts), (c1, c2), (k1, k2), R, S, tuple(sels)
+
+
 def first_diff(name, g, o, kc):
     """One line on how the device table g differs from the oracle's o."""
     if g.shape != o.shape:
@@ -92,30 +123,40 @@ def main():
     count = int(args[1]) if len(args) > 1 else 100
     budget = float(args[2]) if len(args) > 2 else 240.0
     t0 = time.time()
+    mixed = "--mixed" in sys.argv
     bad = done = seg_runs = 0
     for seed in seeds if seeds is not None else range(first, first + count):
         if time.time() - t0 > budget:
             break
-        layout, cols, kc, R, S, sel = case(seed)
+        if mixed:
+            (layout, parts), (c1, c2), (k1, k2), R, S, (sel, sel2) = case_mixed(seed)
+        else:
+            layout, cols, kc, R, S, sel = case(seed)
+            parts, c1, c2, k1, k2, sel2 = 0, cols, cols, kc, kc, None
         nr, ns = len(R), len(S)
-        gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), kc, kc, sel, None)
-        torch.cuda.synchronize()
+        ops.force_parts(parts)
+        try:
+            gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), k1, k2, sel, sel2)
+            torch.cuda.synchronize()
+        finally:
+            ops.force_parts(0)
         nseg = ops.msd_segmented()
         info = (ops.msd_packb(), ops.msd_groups(), ops.msd_stats())
         seg_runs += nseg > 0
-        Rs = oracle.select_sort(R, kc, sel[0] if sel else 0, sel[1] if sel else None)
-        Ss = oracle.select_sort(S, kc, 0, None)
-        J = oracle.join(Rs, Ss, kc, kc)
-        diffs = [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, cols), kc),
-                 first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, cols), kc),
-                 first_diff("J", gJ.cpu().numpy(), J.reshape(-1, 2 * cols - 1), kc)]
+        Rs = oracle.select_sort(R.reshape(-1, c1), k1, sel[0] if sel else 0, sel[1] if sel else None)
+        Ss = oracle.select_sort(S.reshape(-1, c2), k2, sel2[0] if sel2 else 0, sel2[1] if sel2 else None)
+        J = oracle.join(Rs.reshape(-1, c1), Ss.reshape(-1, c2), k1, k2)
+        diffs = [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, c1), k1),
+                 first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, c2), k2),
+                 first_diff("J", gJ.cpu().numpy(), J.reshape(-1, c1 + c2 - 1), k1)]
         diffs = [d for d in diffs if d]
         done += 1
         if done % 10 == 0:
             print(f"  {done} seeds, {bad} failures, {time.time() - t0:.0f} s", flush=True)
         if diffs:
             bad += 1
-            print(f"FAIL seed {seed}: layout {layout} cols {cols} key {kc} n {nr}/{ns} sel {sel} segmented {nseg}", flush=True)
+            print(f"FAIL seed {seed}: layout {layout} cols {c1}/{c2} keys {k1}/{k2} n {nr}/{ns} sel {sel}/{sel2} "
+                  f"parts {parts} segmented {nseg}", flush=True)
             if seeds is not None:
                 print(f"    packb {info[0]} groups {info[1]} stats {info[2]}", flush=True)
                 for d in diffs:
