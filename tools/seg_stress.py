@@ -8,7 +8,9 @@ failing seed and a summary.
     python tools/seg_stress.py [first_seed] [seeds] [seconds]
     python tools/seg_stress.py --seeds=11,25   (those seeds, each failure in detail)
     python tools/seg_stress.py --mixed 0 200   (case_mixed: two shapes, WHEREs on both, partitioned mode)
+    python tools/seg_stress.py --host 0 200    (the mixed cases through smj_sort_merge_join, host pointers)
 """
+import ctypes
 import os
 import sys
 import time
@@ -113,6 +115,37 @@ def first_diff(name, g, o, kc):
             f" (prev {o[max(i - 1, 0)].tolist()}) sorted {srt} same-multiset {same}")
 
 
+class Block(ctypes.Structure):  # user.h's block_t (smj.h)
+    _fields_ = [("table_num", ctypes.c_int), ("col_num", ctypes.c_int), ("row_num", ctypes.c_int)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("cpu_gpu_ms", ctypes.c_double), ("gpu_ms", ctypes.c_double), ("gpu_cpu_ms", ctypes.c_double)]
+
+
+def host_join(lib, R, S, k1, k2, s1, s2):
+    """smj_sort_merge_join on host tables, as app.c calls it (a WHERE on both
+    tables always: None -> row[0] > INT64_MIN)."""
+    c1, c2 = R.shape[1], S.shape[1]
+    R, S = np.ascontiguousarray(R), np.ascontiguousarray(S)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    res, rows, tm = ctypes.c_void_p(), ctypes.c_int64(0), Timing()
+    rc = lib.smj_sort_merge_join(ctypes.byref(Block(0, c1, len(R))), p(R), ctypes.byref(Block(1, c2, len(S))), p(S),
+                                 s1[0], s1[1], s2[0], s2[1], k1, k2, ctypes.byref(res), ctypes.byref(rows),
+                                 ctypes.byref(tm))
+    if rc != 0:
+        raise RuntimeError(f"smj_sort_merge_join -> {rc}")
+    tc = c1 + c2 - 1
+    got = np.empty((0, tc), dtype=np.int64)
+    if res.value:
+        got = np.ctypeslib.as_array(ctypes.cast(res, ctypes.POINTER(ctypes.c_int64)),
+                                    shape=(rows.value * tc,)).copy().reshape(-1, tc)
+        libc = ctypes.CDLL(None)
+        libc.free.argtypes = [ctypes.c_void_p]
+        libc.free(res)
+    return got
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     seeds = None
@@ -123,7 +156,12 @@ def main():
     count = int(args[1]) if len(args) > 1 else 100
     budget = float(args[2]) if len(args) > 2 else 240.0
     t0 = time.time()
-    mixed = "--mixed" in sys.argv
+    mixed = "--mixed" in sys.argv or "--host" in sys.argv
+    hostp = "--host" in sys.argv  # the C-ABI host-pointer call (app.c's drop-in) on the mixed cases
+    if hostp:
+        from smj import _lib
+        lib = _lib.load()
+        assert lib.smj_init(1) >= 1
     bad = done = seg_runs = 0
     for seed in seeds if seeds is not None else range(first, first + count):
         if time.time() - t0 > budget:
@@ -134,9 +172,21 @@ def main():
             layout, cols, kc, R, S, sel = case(seed)
             parts, c1, c2, k1, k2, sel2 = 0, cols, cols, kc, kc, None
         nr, ns = len(R), len(S)
+        if hostp:
+            sel = sel or (0, int(I64.min))
+            sel2 = sel2 or (0, int(I64.min))
+            parts = 0
         ops.force_parts(parts)
         try:
-            gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), k1, k2, sel, sel2)
+            if hostp:
+                try:
+                    gJ = torch.from_numpy(host_join(lib, R.reshape(-1, c1), S.reshape(-1, c2), k1, k2, sel, sel2))
+                except RuntimeError as e:  # an error code: a failure of this seed, not of the run
+                    gJ = None
+                    print(f"seed {seed}: {e} (n {nr}/{ns} cols {c1}/{c2})", flush=True)
+            else:
+                gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), k1, k2, sel,
+                                                 sel2)
             torch.cuda.synchronize()
         finally:
             ops.force_parts(0)
@@ -146,9 +196,10 @@ def main():
         Rs = oracle.select_sort(R.reshape(-1, c1), k1, sel[0] if sel else 0, sel[1] if sel else None)
         Ss = oracle.select_sort(S.reshape(-1, c2), k2, sel2[0] if sel2 else 0, sel2[1] if sel2 else None)
         J = oracle.join(Rs.reshape(-1, c1), Ss.reshape(-1, c2), k1, k2)
-        diffs = [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, c1), k1),
-                 first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, c2), k2),
-                 first_diff("J", gJ.cpu().numpy(), J.reshape(-1, c1 + c2 - 1), k1)]
+        diffs = [first_diff("J", gJ.cpu().numpy(), J.reshape(-1, c1 + c2 - 1), k1) if gJ is not None else "error code"]
+        if not hostp:
+            diffs += [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, c1), k1),
+                      first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, c2), k2)]
         diffs = [d for d in diffs if d]
         done += 1
         if done % 10 == 0:
