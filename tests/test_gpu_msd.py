@@ -955,22 +955,24 @@ def test_far_outliers_wide_groups(gpu, oracle_built, outl, min_r, min_s, nmax, m
     np.testing.assert_array_equal(host(gJ), J.reshape(-1, 3))
 
 
-def test_random_layout_stress(gpu, oracle_built):
+@pytest.mark.parametrize("mode,seeds", [
+    ("plain", [11, 25, 29, 38, 86, 146, 399] + list(range(1000, 1040))),
+    ("mixed", list(range(2000, 2030))),
+    ("host", list(range(3000, 3015))),
+    ("typed", list(range(4000, 4020))),
+])
+def test_random_layout_stress(gpu, oracle_built, mode, seeds):
     """tools/seg_stress.py's seeded random tables (cluster count, gap, width,
-    outliers, duplicates, the extremes; 1-3 columns, either key column, WHEREs):
-    the seeds that failed before the round-6 plan re-read, and 40 more."""
+    outliers, duplicates, the extremes; column counts, key columns, WHEREs,
+    the partitioned mode; the host-pointer call; T = uint64 / double), bit for
+    bit against the oracle.  The plain seeds include the 7 that failed before
+    the round-6 plan re-read."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
-    from seg_stress import case, first_diff
-    from smj import ops
+    from seg_stress import check_seed
     bad = []
-    for seed in [11, 25, 29, 38, 86, 146, 399] + list(range(1000, 1040)):
-        _, cols, kc, R, S, sel = case(seed)
-        gR, gS, gJ = ops.sort_merge_join(dev(R), dev(S), kc, kc, sel, None)
-        torch.cuda.synchronize()
-        Rs, Ss, J = ref_pipeline(R, S, kc, kc, sel, None)
-        d = [first_diff("R", host(gR), Rs.reshape(-1, cols), kc), first_diff("S", host(gS), Ss.reshape(-1, cols), kc),
-             first_diff("J", host(gJ), J.reshape(-1, 2 * cols - 1), kc)]
-        bad += [f"seed {seed}: {x}" for x in d if x]
+    for seed in seeds:
+        diffs, desc, _, _ = check_seed(seed, mode)
+        bad += [f"seed {seed} ({desc}): {x}" for x in diffs]
     assert not bad, bad
 
 

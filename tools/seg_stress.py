@@ -9,6 +9,7 @@ failing seed and a summary.
     python tools/seg_stress.py --seeds=11,25   (those seeds, each failure in detail)
     python tools/seg_stress.py --mixed 0 200   (case_mixed: two shapes, WHEREs on both, partitioned mode)
     python tools/seg_stress.py --host 0 200    (the mixed cases through smj_sort_merge_join, host pointers)
+    python tools/seg_stress.py --typed 0 200   (the mixed cases with T = uint64 / double)
 """
 import ctypes
 import os
@@ -146,6 +147,72 @@ def host_join(lib, R, S, k1, k2, s1, s2):
     return got
 
 
+_LIB = None
+
+
+def check_seed(seed, mode="plain"):
+    """One seed of a mode (plain / mixed / host / typed): (diffs, description,
+    segmented buckets, plan info).  diffs is empty when the device output
+    equals the oracle's bit for bit."""
+    global _LIB
+    typed, hostp = mode == "typed", mode == "host"
+    if mode == "plain":
+        layout, cols, kc, R, S, sel = case(seed)
+        parts, c1, c2, k1, k2, sel2 = 0, cols, cols, kc, kc, None
+    else:
+        (layout, parts), (c1, c2), (k1, k2), R, S, (sel, sel2) = case_mixed(seed)
+    nr, ns = len(R), len(S)
+    if hostp:  # app.c always selects: None -> row[0] > INT64_MIN
+        sel = sel or (0, int(I64.min))
+        sel2 = sel2 or (0, int(I64.min))
+        parts = 0
+        if _LIB is None:
+            from smj import _lib
+            _LIB = _lib.load()
+            assert _LIB.smj_init(1) >= 1
+    kt = (1 + seed % 2) if typed else 0  # T = uint64 (odd seeds) / double (even seeds)
+    if kt == 1:  # the int64 patterns as uint64 (negative keys wrap past 2^63); WHERE values likewise
+        sel = sel and (sel[0], sel[1] % (1 << 64))
+        sel2 = sel2 and (sel2[0], sel2[1] % (1 << 64))
+    elif kt == 2:  # the same values as doubles (clusters up to 2^62 round to 53 bits: duplicates)
+        R, S = R.astype(np.float64), S.astype(np.float64)
+        sel = sel and (sel[0], float(sel[1]))
+        sel2 = sel2 and (sel2[0], float(sel2[1]))
+    desc = (f"layout {layout} cols {c1}/{c2} keys {k1}/{k2} n {nr}/{ns} sel {sel}/{sel2} parts {parts}"
+            + (f" T {kt}" if kt else ""))
+    cuda = (lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda())
+    gR = gS = gJ = None
+    ops.force_parts(parts)
+    try:
+        if hostp:
+            try:
+                gJ = torch.from_numpy(host_join(_LIB, R.reshape(-1, c1), S.reshape(-1, c2), k1, k2, sel, sel2))
+            except RuntimeError as e:  # an error code: a failure of this seed, not of the run
+                desc += f" ({e})"
+        else:
+            gR, gS, gJ = ops.sort_merge_join(cuda(R), cuda(S), k1, k2, sel, sel2, key_type=kt)
+        torch.cuda.synchronize()
+    finally:
+        ops.force_parts(0)
+    nseg = ops.msd_segmented()
+    info = (ops.msd_packb(), ops.msd_groups(), ops.msd_stats())
+    if kt:
+        bits = (lambda a: np.ascontiguousarray(a).view(np.int64))
+        Rs = bits(oracle.select_sort_t(R.reshape(-1, c1), kt, k1, *(sel or (0, None))))
+        Ss = bits(oracle.select_sort_t(S.reshape(-1, c2), kt, k2, *(sel2 or (0, None))))
+        J = bits(oracle.join_t(Rs.reshape(-1, c1), Ss.reshape(-1, c2), kt, k1, k2))
+        gR, gS, gJ = (t.view(torch.int64) for t in (gR, gS, gJ))
+    else:
+        Rs = oracle.select_sort(R.reshape(-1, c1), k1, sel[0] if sel else 0, sel[1] if sel else None)
+        Ss = oracle.select_sort(S.reshape(-1, c2), k2, sel2[0] if sel2 else 0, sel2[1] if sel2 else None)
+        J = oracle.join(Rs.reshape(-1, c1), Ss.reshape(-1, c2), k1, k2)
+    diffs = [first_diff("J", gJ.cpu().numpy(), J.reshape(-1, c1 + c2 - 1), k1) if gJ is not None else "error code"]
+    if not hostp:
+        diffs += [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, c1), k1),
+                  first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, c2), k2)]
+    return [d for d in diffs if d], desc, nseg, info
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     seeds = None
@@ -155,64 +222,26 @@ def main():
     first = int(args[0]) if len(args) > 0 else 0
     count = int(args[1]) if len(args) > 1 else 100
     budget = float(args[2]) if len(args) > 2 else 240.0
+    mode = next((m for m in ("mixed", "host", "typed") if f"--{m}" in sys.argv), "plain")
     t0 = time.time()
-    mixed = "--mixed" in sys.argv or "--host" in sys.argv
-    hostp = "--host" in sys.argv  # the C-ABI host-pointer call (app.c's drop-in) on the mixed cases
-    if hostp:
-        from smj import _lib
-        lib = _lib.load()
-        assert lib.smj_init(1) >= 1
     bad = done = seg_runs = 0
     for seed in seeds if seeds is not None else range(first, first + count):
         if time.time() - t0 > budget:
             break
-        if mixed:
-            (layout, parts), (c1, c2), (k1, k2), R, S, (sel, sel2) = case_mixed(seed)
-        else:
-            layout, cols, kc, R, S, sel = case(seed)
-            parts, c1, c2, k1, k2, sel2 = 0, cols, cols, kc, kc, None
-        nr, ns = len(R), len(S)
-        if hostp:
-            sel = sel or (0, int(I64.min))
-            sel2 = sel2 or (0, int(I64.min))
-            parts = 0
-        ops.force_parts(parts)
-        try:
-            if hostp:
-                try:
-                    gJ = torch.from_numpy(host_join(lib, R.reshape(-1, c1), S.reshape(-1, c2), k1, k2, sel, sel2))
-                except RuntimeError as e:  # an error code: a failure of this seed, not of the run
-                    gJ = None
-                    print(f"seed {seed}: {e} (n {nr}/{ns} cols {c1}/{c2})", flush=True)
-            else:
-                gR, gS, gJ = ops.sort_merge_join(torch.from_numpy(R).cuda(), torch.from_numpy(S).cuda(), k1, k2, sel,
-                                                 sel2)
-            torch.cuda.synchronize()
-        finally:
-            ops.force_parts(0)
-        nseg = ops.msd_segmented()
-        info = (ops.msd_packb(), ops.msd_groups(), ops.msd_stats())
+        diffs, desc, nseg, info = check_seed(seed, mode)
         seg_runs += nseg > 0
-        Rs = oracle.select_sort(R.reshape(-1, c1), k1, sel[0] if sel else 0, sel[1] if sel else None)
-        Ss = oracle.select_sort(S.reshape(-1, c2), k2, sel2[0] if sel2 else 0, sel2[1] if sel2 else None)
-        J = oracle.join(Rs.reshape(-1, c1), Ss.reshape(-1, c2), k1, k2)
-        diffs = [first_diff("J", gJ.cpu().numpy(), J.reshape(-1, c1 + c2 - 1), k1) if gJ is not None else "error code"]
-        if not hostp:
-            diffs += [first_diff("R", gR.cpu().numpy(), Rs.reshape(-1, c1), k1),
-                      first_diff("S", gS.cpu().numpy(), Ss.reshape(-1, c2), k2)]
-        diffs = [d for d in diffs if d]
         done += 1
         if done % 10 == 0:
             print(f"  {done} seeds, {bad} failures, {time.time() - t0:.0f} s", flush=True)
         if diffs:
             bad += 1
-            print(f"FAIL seed {seed}: layout {layout} cols {c1}/{c2} keys {k1}/{k2} n {nr}/{ns} sel {sel}/{sel2} "
-                  f"parts {parts} segmented {nseg}", flush=True)
+            print(f"FAIL seed {seed}: {desc} segmented {nseg}", flush=True)
             if seeds is not None:
                 print(f"    packb {info[0]} groups {info[1]} stats {info[2]}", flush=True)
                 for d in diffs:
                     print("    " + d, flush=True)
-    print(f"seg_stress: {done} seeds, {bad} failures, {seg_runs} with segmented buckets, {time.time() - t0:.0f} s", flush=True)
+    print(f"seg_stress: {done} seeds ({mode}), {bad} failures, {seg_runs} with segmented buckets, "
+          f"{time.time() - t0:.0f} s", flush=True)
     sys.exit(1 if bad else 0)
 
 
