@@ -164,6 +164,17 @@ def make_tables(kind, n):
         S[rng.random(n) < 0.5, 0] = 17
         R[:, 1], S[:, 1] = np.arange(n), -np.arange(n)
         return R, S
+    if kind == "farout":  # dense keys, 1 % far outliers and the int64 extremes (round 6's stress shape)
+        tabs = []
+        for x in range(2):
+            k = rng.integers(0, 10 ** 6, size=n, dtype=np.int64)
+            m = rng.random(n) < 0.01
+            k[m] = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, size=int(m.sum()), dtype=np.int64,
+                                endpoint=True)
+            k[rng.choice(n, 40, replace=False)] = np.iinfo(np.int64).min
+            k[rng.choice(n, 30, replace=False)] = np.iinfo(np.int64).max
+            tabs.append(np.stack([k, x * 10 ** 9 + np.arange(n, dtype=np.int64)], axis=1))
+        return tabs[0], tabs[1]
     raise ValueError(kind)
 
 
@@ -187,6 +198,7 @@ def test_distributed_equals_single(tmp_path, oracle_built, world, kind, cfg):
     ("dups", {"select": (2, 5, 0, 5), "keys": (1, 1), "samples": 256, "gpu": True}),
     ("skew", {"select": (0, -900, 0, -2000), "keys": (0, 0), "samples": 1024, "gpu": True}),
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "stages": 1}),
+    ("farout", {"select": (0, -(1 << 63), 0, -(1 << 63)), "keys": (0, 0), "samples": 4096, "gpu": True}),
 ])
 def test_distributed_hip_two_ranks_one_gpu(tmp_path, oracle_built, pkg_built, kind, cfg):
     """The product path of smj/dist.py -- HIP smj_dev_partition and the
@@ -253,6 +265,8 @@ def test_loopback_exchange_gloo(tmp_path, oracle_built, world):
     # full-range keys: not packed to begin with (no thrown-away packed partition)
     ("widekeys", {"select": (0, -(1 << 63), 0, -(1 << 63)), "keys": (0, 0), "samples": 4096, "gpu": True,
                   "expect_pack": ([False, False], 0)}),
+    # dense keys with far outliers and the extremes (the final tiers' oversized groups, round 6)
+    ("farout", {"select": (0, -(1 << 63), 0, -(1 << 63)), "keys": (0, 0), "samples": 4096, "gpu": True}),
     ("uniform", {"select": (0, 5000, 0, 5000), "keys": (0, 0), "samples": 4096, "gpu": True, "expect_pack": (
         [True, True], 0)}),
     # the packed exchange turned off
