@@ -10,6 +10,7 @@ failing seed and a summary.
     python tools/seg_stress.py --mixed 0 200   (case_mixed: two shapes, WHEREs on both, partitioned mode)
     python tools/seg_stress.py --host 0 200    (the mixed cases through smj_sort_merge_join, host pointers)
     python tools/seg_stress.py --typed 0 200   (the mixed cases with T = uint64 / double)
+    python tools/seg_stress.py --hostbig 0 40  (host tables of 3M-9M rows: several staged chunks)
 """
 import ctypes
 import os
@@ -72,7 +73,7 @@ def case(seed):
     return layout, cols, kc, R, S, sel
 
 
-def case_mixed(seed):
+def case_mixed(seed, big=False):
     """Mixed shapes: R and S of their own column counts (1-5) and key
     columns, a WHERE on either, tiny to 2M-row tables, and the partitioned
     mode forced on some seeds (parts)."""
@@ -86,6 +87,8 @@ def case_mixed(seed):
     k1, k2 = int(rng.integers(0, c1)), int(rng.integers(0, c2))
     nr, ns = (int(rng.choice([0, 1, 100, 5000, 300_000, 2_000_000])) if rng.random() < 0.3
               else int(rng.integers(20_000, 900_000)) for _ in range(2))
+    if big:  # several of the staged host path's 3,440,640-row chunks, ragged last ones
+        nr, ns = (int(rng.integers(3_000_000, 9_000_000)) for _ in range(2))
     R = table(rng, nr, c1, k1, 0, layout)
     S = table(rng, ns, c2, k2, 10 ** 9, layout)
     if nr and ns:
@@ -155,12 +158,12 @@ def check_seed(seed, mode="plain"):
     segmented buckets, plan info).  diffs is empty when the device output
     equals the oracle's bit for bit."""
     global _LIB
-    typed, hostp = mode == "typed", mode == "host"
+    typed, hostp = mode == "typed", mode in ("host", "hostbig")
     if mode == "plain":
         layout, cols, kc, R, S, sel = case(seed)
         parts, c1, c2, k1, k2, sel2 = 0, cols, cols, kc, kc, None
     else:
-        (layout, parts), (c1, c2), (k1, k2), R, S, (sel, sel2) = case_mixed(seed)
+        (layout, parts), (c1, c2), (k1, k2), R, S, (sel, sel2) = case_mixed(seed, mode == "hostbig")
     nr, ns = len(R), len(S)
     if hostp:  # app.c always selects: None -> row[0] > INT64_MIN
         sel = sel or (0, int(I64.min))
@@ -222,7 +225,7 @@ def main():
     first = int(args[0]) if len(args) > 0 else 0
     count = int(args[1]) if len(args) > 1 else 100
     budget = float(args[2]) if len(args) > 2 else 240.0
-    mode = next((m for m in ("mixed", "host", "typed") if f"--{m}" in sys.argv), "plain")
+    mode = next((m for m in ("mixed", "hostbig", "host", "typed") if f"--{m}" in sys.argv), "plain")
     t0 = time.time()
     bad = done = seg_runs = 0
     for seed in seeds if seeds is not None else range(first, first + count):
