@@ -361,6 +361,7 @@ while True:
     segmix2) test_run segmix2 600 python -u tools/seg_stress.py --mixed 400 1200 420 ;;
     segtyped) test_run segtyped 600 python -u tools/seg_stress.py --typed 0 400 420 ;;
     seghostbig) test_run seghostbig 600 python -u tools/seg_stress.py --hostbig 0 60 400 ;;
+    bigst) run bigst 600 python -u tools/big_stress.py ;;
     extp)  run extp 300 python -u tools/ext_probe.py ${EXTP_SEEDS:-25 29 38 86} ;;
     segd)  SD=--seeds=${SEGD_SEEDS:-11,25,29,38,86,146,399}  # failing stress seeds in detail, under each switch
            run segd_def 300 python -u tools/seg_stress.py $SD
